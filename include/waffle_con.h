@@ -1,0 +1,202 @@
+/*
+ * waffle_con MI355X library — C ABI (the drop-in boundary).
+ *
+ * The reference (PacificBiosciences/waffle_con v0.4.4) is a Rust crate with no
+ * FFI; its public API is ConsensusDWFA / DualConsensusDWFA /
+ * PriorityConsensusDWFA + CdwfaConfig. A Rust shim keeps that
+ * API and calls these entry points; consensus() of each engine maps to one
+ * wc_*_batch call with a batch of one problem (or many, for throughput).
+ *
+ * Conventions: return 0 = OK, otherwise a WC_E_* code; wc_last_error() holds
+ * the message. Caller owns inputs (copied during the call); result sets are
+ * owned by the library until wc_results_free. A context is bound to one HIP
+ * device and must be used from one host thread at a time.
+ */
+#ifndef WAFFLE_CON_H
+#define WAFFLE_CON_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes; messages match the reference's bail!/panic sites */
+enum {
+  WC_OK = 0,
+  WC_E_FINALIZE_UNINIT = 1, /* consensus.rs:473, dual_consensus.rs:1078 */
+  WC_E_NO_START = 2,        /* consensus.rs:205, dual_consensus.rs:303 */
+  WC_E_COVERAGE_GAP = 3,    /* consensus.rs:305 */
+  WC_E_CAPACITY = 4,        /* pqueue_tracker.rs:90 */
+  WC_E_LOCKED = 5,          /* dual_consensus.rs:917,919 */
+  WC_E_DUAL_TWICE = 6,      /* dual_consensus.rs:959 */
+  WC_E_SAME_SYMBOL = 7,     /* dual_consensus.rs:964 */
+  WC_E_ROOT_INACTIVE = 8,   /* consensus.rs:396, dual_consensus.rs:843 */
+  WC_E_BAD_INPUT = 9,       /* priority_consensus.rs:144,148; empty inputs */
+  WC_E_INVARIANT = 10,      /* reference assert!/panic sites */
+  WC_E_LIMIT = 11,          /* a device capacity limit was exceeded after retries */
+  WC_E_HIP = 12,            /* HIP runtime failure (no device, launch failure) */
+};
+
+/* cdwfa_config.rs:38-103 (CdwfaConfig); wc_config_default gives :71-103 */
+typedef struct wc_config {
+  int32_t consensus_cost; /* 0 = L1Distance, 1 = L2Distance */
+  int32_t wildcard;       /* -1 = None, else the wildcard byte */
+  uint64_t max_queue_size;
+  uint64_t max_capacity_per_size;
+  uint64_t max_return_size;
+  uint64_t max_nodes_wo_constraint;
+  uint64_t min_count;
+  double min_af;
+  uint64_t dual_max_ed_delta;
+  uint64_t offset_window;
+  uint64_t offset_compare_length;
+  uint8_t weighted_by_ed;
+  uint8_t allow_early_termination;
+  uint8_t auto_shift_offsets;
+  uint8_t _pad[5];
+} wc_config;
+
+void wc_config_default(wc_config* cfg);
+
+typedef struct wc_ctx wc_ctx;
+typedef struct wc_results wc_results;
+
+int wc_ctx_create(int device, wc_ctx** out);
+void wc_ctx_destroy(wc_ctx* ctx);
+const char* wc_last_error(const wc_ctx* ctx);
+
+/* One consensus problem (a locus): its reads and optional activation offsets
+ * (add_sequence_offset, consensus.rs:120; NULL or -1 entries = None). */
+typedef struct wc_problem {
+  uint32_t n_reads;
+  const uint8_t* const* reads;
+  const uint64_t* lens;
+  const int64_t* offsets;
+} wc_problem;
+
+/* One priority problem: n_chains read chains of `levels` sequences each,
+ * row-major (reads[i*levels + l]); offsets likewise (NULL = all None);
+ * seed_groups[i] (-1 = None, NULL = all None). priority_consensus.rs:141-167. */
+typedef struct wc_chain_problem {
+  uint32_t n_chains;
+  uint32_t levels;
+  const uint8_t* const* reads;
+  const uint64_t* lens;
+  const int64_t* offsets;
+  const int64_t* seed_groups;
+} wc_chain_problem;
+
+/* Batched engines: every problem runs the reference search bit-exactly; the
+ * whole batch is resident in HBM and runs as one device-resident launch
+ * (one workgroup per problem). Per-problem failures are reported through
+ * wc_results_status, not the return value. Replaces:
+ *   ConsensusDWFA::consensus          consensus.rs:139
+ *   DualConsensusDWFA::consensus      dual_consensus.rs:240
+ *   PriorityConsensusDWFA::consensus  priority_consensus.rs:172 */
+int wc_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, const wc_problem* problems,
+                       wc_results** out);
+int wc_dual_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, const wc_problem* problems,
+                            wc_results** out);
+int wc_priority_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, const wc_chain_problem* problems,
+                                wc_results** out);
+
+void wc_results_free(wc_results* r);
+uint32_t wc_results_problems(const wc_results* r);
+int wc_results_status(const wc_results* r, uint32_t p);
+const char* wc_results_error(const wc_results* r, uint32_t p);
+uint32_t wc_results_count(const wc_results* r, uint32_t p);
+
+/* Consensus (consensus.rs:42-74): sequence bytes + per-read scores. Pointers
+ * stay valid until wc_results_free. */
+int wc_results_single(const wc_results* r, uint32_t p, uint32_t k, const uint8_t** seq, uint64_t* seq_len,
+                      const uint64_t** scores, uint64_t* n_scores);
+
+/* DualConsensus (dual_consensus.rs:52-177). scores1/scores2 use -1 for None. */
+typedef struct wc_dual_view {
+  const uint8_t* seq1;
+  uint64_t len1;
+  const uint64_t* scores_c1; /* Consensus::scores of consensus1 */
+  uint64_t n_scores_c1;
+  uint8_t has_c2;
+  const uint8_t* seq2;
+  uint64_t len2;
+  const uint64_t* scores_c2;
+  uint64_t n_scores_c2;
+  const uint8_t* is_consensus1; /* n_reads */
+  const int64_t* scores1;       /* n_reads, -1 = None */
+  const int64_t* scores2;
+  uint64_t n_reads;
+} wc_dual_view;
+int wc_results_dual(const wc_results* r, uint32_t p, uint32_t k, wc_dual_view* out);
+
+/* PriorityConsensus (priority_consensus.rs:64-88): for chain k of problem p,
+ * wc_results_count gives the number of chains; each chain has `levels`
+ * consensuses (wc_results_chain_len). sequence_indices has n_chains entries. */
+uint32_t wc_results_chain_len(const wc_results* r, uint32_t p, uint32_t k);
+int wc_results_chain(const wc_results* r, uint32_t p, uint32_t k, uint32_t level, const uint8_t** seq,
+                     uint64_t* seq_len, const uint64_t** scores, uint64_t* n_scores);
+int wc_results_sequence_indices(const wc_results* r, uint32_t p, const uint64_t** idx, uint64_t* n);
+
+/* Work counters and timings of the run that produced `r`. */
+typedef struct wc_stats {
+  uint64_t updates;      /* DWFALite::update-equivalent calls */
+  uint64_t w_out;        /* sum of post-update wavefront lengths */
+  uint64_t compares;     /* byte compares the reference extend would make */
+  uint64_t ed_increases; /* increase_edit_distance calls */
+  uint64_t finalizes;    /* DWFALite::finalize calls */
+  uint64_t pops;
+  uint64_t nodes_explored;
+  uint64_t nodes_ignored;
+  uint64_t peak_queue_size; /* max over problems */
+  uint64_t launches;        /* engine kernel launches (incl. capacity retries) */
+  double kernel_ms;         /* device time of the engine launches (HIP events) */
+  double wall_ms;           /* host wall time of the whole call */
+} wc_stats;
+int wc_results_stats(const wc_results* r, wc_stats* out);
+/* per-problem counters (same fields; kernel_ms/wall_ms/launches zero) */
+int wc_results_problem_stats(const wc_results* r, uint32_t p, wc_stats* out);
+
+/* Standalone DWFALite (dynamic_wfa.rs:48-265) on the device: one job = one
+ * read-DWFA state advanced by `op` against (baseline, other). Batched: one
+ * wave per job. State in/out: e, wavefront[0..wf_len) (capacity wf_cap). */
+typedef struct wc_dwfa_job {
+  const uint8_t* baseline;
+  uint64_t baseline_len;
+  const uint8_t* other;
+  uint64_t other_len;
+  uint64_t offset;
+  int32_t wildcard;       /* -1 = None */
+  uint8_t early;          /* allow_early_termination */
+  uint8_t op;             /* 0 = update, 1 = finalize, 2 = candidates (read-only) */
+  uint8_t _pad[2];
+  uint64_t e;             /* in/out */
+  uint64_t* wavefront;    /* in/out, host memory */
+  uint64_t wf_len;        /* in/out */
+  uint64_t wf_cap;
+  /* op 2 output: symbols in FxHashMap iteration order with counts */
+  uint8_t cand_syms[16];
+  uint64_t cand_counts[16];
+  uint32_t n_cand;
+  int32_t status;
+} wc_dwfa_job;
+int wc_dwfa_batch(wc_ctx* ctx, uint32_t n, wc_dwfa_job* jobs);
+
+/* example_gen.rs:11-64 generate_test with the reference RNG (StdRng::seed_from_u64);
+ * the reference hardcodes seed 0. Writes consensus (seq_len bytes) and samples
+ * into library-owned storage returned through *handle (free with wc_gen_free). */
+typedef struct wc_gen wc_gen;
+int wc_generate_test(uint8_t alphabet, uint64_t seq_len, uint64_t num_samples, double error_rate, uint64_t seed,
+                     wc_gen** handle);
+const uint8_t* wc_gen_consensus(const wc_gen* g, uint64_t* len);
+const uint8_t* wc_gen_sample(const wc_gen* g, uint64_t i, uint64_t* len);
+void wc_gen_free(wc_gen* g);
+
+/* sequence_alignment.rs:18,36 — pairwise WFA edit distance (host reference API). */
+uint64_t wc_wfa_ed_config(const uint8_t* v1, uint64_t l1, const uint8_t* v2, uint64_t l2, uint8_t require_both_end,
+                          int32_t wildcard);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

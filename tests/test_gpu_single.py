@@ -1,0 +1,48 @@
+"""GPU parity: ConsensusDWFA on the HIP engine vs the reference's golden
+vectors and vs the CPU oracle (bit-exact sequences, scores and work counters)."""
+import pytest
+
+import oracle_ffi as orc
+import ref_cases as rc
+
+pytestmark = pytest.mark.gpu
+
+hip = pytest.importorskip("hip_runner")
+
+OFFSET_CASES = {"offset_windows", "offset_gap_err"}
+
+
+@pytest.mark.parametrize("name", sorted(rc.SINGLE_CASES))
+def test_reference_single(name):
+    if name in OFFSET_CASES:
+        pytest.xfail("device activation (add_sequence_offset) lands in a later milestone")
+    rc.check_single(rc.SINGLE_CASES[name], hip)
+
+
+COUNTER_KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
+                "nodes_ignored", "peak_queue_size")
+
+
+def _gen(L, N, err, seed):
+    import waffle_con_amd as w
+    return w.generate_test(4, L, N, err, seed)[1]
+
+
+@pytest.mark.parametrize("L,N,err,seed", [(1000, 30, 0.01, 0), (1000, 8, 0.02, 0), (300, 8, 0.05, 1),
+                                          (2000, 12, 0.03, 2), (500, 5, 0.08, 3)])
+def test_example_gen_vs_oracle(L, N, err, seed):
+    seqs = _gen(L, N, err, seed)
+    cfg = dict(min_count=max(1, N // 4))
+    exp, ec = orc.consensus(seqs, counters=True, **cfg)
+    got, gc = hip.consensus(seqs, counters=True, **cfg)
+    assert got == exp
+    for k in COUNTER_KEYS:
+        assert gc[k] == ec[k], (k, gc[k], ec[k])
+
+
+def test_batch_matches_individual():
+    probs = [_gen(400, 10, 0.04, s) for s in range(12)]
+    cfg = dict(min_count=2)
+    got = hip.consensus_batch(probs, **cfg)
+    for p, g in zip(probs, got):
+        assert g == orc.consensus(p, **cfg)

@@ -1,0 +1,259 @@
+"""ctypes binding of the in-tree HIP library (waffle_con_amd/libwaffle_con.so).
+
+The library is the product: there is no CPU fallback. Loading fails loudly
+when the shared object is missing, and creating a context fails loudly when
+no HIP device is visible.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwaffle_con.so")
+
+_lib = None
+_lock = threading.Lock()
+_ctx_local = threading.local()
+
+# error codes (include/waffle_con.h)
+WC_OK = 0
+WC_E_FINALIZE_UNINIT = 1
+WC_E_NO_START = 2
+WC_E_COVERAGE_GAP = 3
+WC_E_CAPACITY = 4
+WC_E_LIMIT = 11
+WC_E_HIP = 12
+
+
+class WaffleConError(Exception):
+    """Error raised for a failed consensus; str() is the reference's message."""
+
+    def __init__(self, message, code=0):
+        super().__init__(message)
+        self.code = code
+
+
+class WcConfig(ctypes.Structure):
+    _fields_ = [
+        ("consensus_cost", ctypes.c_int32),
+        ("wildcard", ctypes.c_int32),
+        ("max_queue_size", ctypes.c_uint64),
+        ("max_capacity_per_size", ctypes.c_uint64),
+        ("max_return_size", ctypes.c_uint64),
+        ("max_nodes_wo_constraint", ctypes.c_uint64),
+        ("min_count", ctypes.c_uint64),
+        ("min_af", ctypes.c_double),
+        ("dual_max_ed_delta", ctypes.c_uint64),
+        ("offset_window", ctypes.c_uint64),
+        ("offset_compare_length", ctypes.c_uint64),
+        ("weighted_by_ed", ctypes.c_uint8),
+        ("allow_early_termination", ctypes.c_uint8),
+        ("auto_shift_offsets", ctypes.c_uint8),
+        ("_pad", ctypes.c_uint8 * 5),
+    ]
+
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class WcProblem(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_uint32),
+                ("reads", ctypes.POINTER(_u8p)),
+                ("lens", ctypes.POINTER(ctypes.c_uint64)),
+                ("offsets", ctypes.POINTER(ctypes.c_int64))]
+
+
+class WcChainProblem(ctypes.Structure):
+    _fields_ = [("n_chains", ctypes.c_uint32),
+                ("levels", ctypes.c_uint32),
+                ("reads", ctypes.POINTER(_u8p)),
+                ("lens", ctypes.POINTER(ctypes.c_uint64)),
+                ("offsets", ctypes.POINTER(ctypes.c_int64)),
+                ("seed_groups", ctypes.POINTER(ctypes.c_int64))]
+
+
+class WcDualView(ctypes.Structure):
+    _fields_ = [("seq1", _u8p), ("len1", ctypes.c_uint64),
+                ("scores_c1", ctypes.POINTER(ctypes.c_uint64)), ("n_scores_c1", ctypes.c_uint64),
+                ("has_c2", ctypes.c_uint8),
+                ("seq2", _u8p), ("len2", ctypes.c_uint64),
+                ("scores_c2", ctypes.POINTER(ctypes.c_uint64)), ("n_scores_c2", ctypes.c_uint64),
+                ("is_consensus1", _u8p),
+                ("scores1", ctypes.POINTER(ctypes.c_int64)),
+                ("scores2", ctypes.POINTER(ctypes.c_int64)),
+                ("n_reads", ctypes.c_uint64)]
+
+
+class WcStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
+        "nodes_ignored", "peak_queue_size", "launches")] + [("kernel_ms", ctypes.c_double),
+                                                            ("wall_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class WcDwfaJob(ctypes.Structure):
+    _fields_ = [("baseline", _u8p), ("baseline_len", ctypes.c_uint64),
+                ("other", _u8p), ("other_len", ctypes.c_uint64),
+                ("offset", ctypes.c_uint64), ("wildcard", ctypes.c_int32),
+                ("early", ctypes.c_uint8), ("op", ctypes.c_uint8), ("_pad", ctypes.c_uint8 * 2),
+                ("e", ctypes.c_uint64), ("wavefront", ctypes.POINTER(ctypes.c_uint64)),
+                ("wf_len", ctypes.c_uint64), ("wf_cap", ctypes.c_uint64),
+                ("cand_syms", ctypes.c_uint8 * 16), ("cand_counts", ctypes.c_uint64 * 16),
+                ("n_cand", ctypes.c_uint32), ("status", ctypes.c_int32)]
+
+
+# every symbol include/waffle_con.h declares (checked by tests/test_cabi.py)
+EXPORTED = (
+    "wc_config_default", "wc_ctx_create", "wc_ctx_destroy", "wc_last_error",
+    "wc_consensus_batch", "wc_dual_consensus_batch", "wc_priority_consensus_batch",
+    "wc_results_free", "wc_results_problems", "wc_results_status", "wc_results_error",
+    "wc_results_count", "wc_results_single", "wc_results_dual", "wc_results_chain_len",
+    "wc_results_chain", "wc_results_sequence_indices", "wc_results_stats",
+    "wc_results_problem_stats", "wc_dwfa_batch", "wc_generate_test", "wc_gen_consensus",
+    "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config",
+)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise WaffleConError(
+                "HIP library %s is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950)" % LIB_PATH, WC_E_HIP)
+        L = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        L.wc_config_default.argtypes = [ctypes.POINTER(WcConfig)]
+        L.wc_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        L.wc_ctx_destroy.argtypes = [vp]
+        L.wc_last_error.argtypes = [vp]
+        L.wc_last_error.restype = ctypes.c_char_p
+        for f, pt in (("wc_consensus_batch", WcProblem), ("wc_dual_consensus_batch", WcProblem),
+                      ("wc_priority_consensus_batch", WcChainProblem)):
+            fn = getattr(L, f)
+            fn.argtypes = [vp, ctypes.POINTER(WcConfig), ctypes.c_uint32, ctypes.POINTER(pt), ctypes.POINTER(vp)]
+        L.wc_results_free.argtypes = [vp]
+        L.wc_results_problems.argtypes = [vp]
+        L.wc_results_problems.restype = ctypes.c_uint32
+        L.wc_results_status.argtypes = [vp, ctypes.c_uint32]
+        L.wc_results_error.argtypes = [vp, ctypes.c_uint32]
+        L.wc_results_error.restype = ctypes.c_char_p
+        L.wc_results_count.argtypes = [vp, ctypes.c_uint32]
+        L.wc_results_count.restype = ctypes.c_uint32
+        L.wc_results_single.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_u8p),
+                                        ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                        ctypes.POINTER(ctypes.c_uint64)]
+        L.wc_results_dual.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(WcDualView)]
+        L.wc_results_chain_len.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32]
+        L.wc_results_chain_len.restype = ctypes.c_uint32
+        L.wc_results_chain.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.POINTER(_u8p), ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                       ctypes.POINTER(ctypes.c_uint64)]
+        L.wc_results_sequence_indices.argtypes = [vp, ctypes.c_uint32,
+                                                  ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                                  ctypes.POINTER(ctypes.c_uint64)]
+        L.wc_results_stats.argtypes = [vp, ctypes.POINTER(WcStats)]
+        L.wc_results_problem_stats.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(WcStats)]
+        L.wc_dwfa_batch.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(WcDwfaJob)]
+        L.wc_generate_test.argtypes = [ctypes.c_uint8, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
+                                       ctypes.c_uint64, ctypes.POINTER(vp)]
+        L.wc_gen_consensus.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.wc_gen_consensus.restype = ctypes.c_void_p
+        L.wc_gen_sample.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+        L.wc_gen_sample.restype = ctypes.c_void_p
+        L.wc_gen_free.argtypes = [vp]
+        L.wc_wfa_ed_config.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
+                                       ctypes.c_uint8, ctypes.c_int32]
+        L.wc_wfa_ed_config.restype = ctypes.c_uint64
+        _lib = L
+        return L
+
+
+class Context:
+    """One HIP device context (stream, events, cached HBM arenas)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = ctypes.c_void_p()
+        rc = L.wc_ctx_create(int(device), ctypes.byref(h))
+        if rc != WC_OK:
+            raise WaffleConError("no usable HIP device %d for waffle_con (wc_ctx_create rc=%d)" % (device, rc), rc)
+        self.handle = h
+        self.device = device
+
+    def last_error(self):
+        return lib().wc_last_error(self.handle).decode()
+
+    def close(self):
+        if self.handle:
+            lib().wc_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+def default_context():
+    """Per-thread default context on the current device (LOCAL_RANK or 0)."""
+    ctx = getattr(_ctx_local, "ctx", None)
+    if ctx is None:
+        dev = int(os.environ.get("WAFFLE_CON_DEVICE", "0"))
+        ctx = Context(dev)
+        _ctx_local.ctx = ctx
+    return ctx
+
+
+def make_config(config):
+    c = WcConfig()
+    lib().wc_config_default(ctypes.byref(c))
+    c.consensus_cost = int(config.consensus_cost.value)
+    c.wildcard = -1 if config.wildcard is None else int(config.wildcard)
+    c.max_queue_size = int(config.max_queue_size)
+    c.max_capacity_per_size = int(config.max_capacity_per_size)
+    c.max_return_size = int(config.max_return_size)
+    c.max_nodes_wo_constraint = int(config.max_nodes_wo_constraint)
+    c.min_count = int(config.min_count)
+    c.min_af = float(config.min_af)
+    c.dual_max_ed_delta = int(config.dual_max_ed_delta)
+    c.offset_window = int(config.offset_window)
+    c.offset_compare_length = int(config.offset_compare_length)
+    c.weighted_by_ed = int(bool(config.weighted_by_ed))
+    c.allow_early_termination = int(bool(config.allow_early_termination))
+    c.auto_shift_offsets = int(bool(config.auto_shift_offsets))
+    return c
+
+
+class PackedReads:
+    """Keeps ctypes buffers alive for one call."""
+
+    def __init__(self, seqs):
+        self.bufs = [ctypes.create_string_buffer(bytes(s), max(1, len(s))) for s in seqs]
+        n = max(1, len(seqs))
+        self.ptrs = (_u8p * n)(*[ctypes.cast(b, _u8p) for b in self.bufs])
+        self.lens = (ctypes.c_uint64 * n)(*[len(s) for s in seqs])
+
+
+def offsets_array(offsets):
+    if offsets is None or all(o is None for o in offsets):
+        return None
+    return (ctypes.c_int64 * max(1, len(offsets)))(*[-1 if o is None else int(o) for o in offsets])
+
+
+def u8_bytes(ptr, n):
+    return ctypes.string_at(ptr, n) if n else b""
+
+
+def u64_list(ptr, n):
+    return [ptr[i] for i in range(n)]

@@ -1,0 +1,145 @@
+// Structures shared by the host orchestration (host.cpp) and the device
+// engines (engine.hip). Plain data only.
+#pragma once
+#include <stdint.h>
+
+namespace wc {
+
+constexpr int kBlock = 256;       // threads per engine workgroup (4 waves)
+constexpr int kWaves = kBlock / 64;
+constexpr int kKmax = 8;          // distinct symbols at one read's tips
+constexpr int kKout = 16;         // distinct symbols voted across a node side
+constexpr uint32_t kInactive = 0xFFFFFFFFu;  // Option<DWFALite>::None
+
+// per-problem status (device → host)
+enum : uint32_t {
+  ST_OK = 0,
+  // 1..12 = WC_E_* error codes (include/waffle_con.h)
+  ST_RETRY = 0x100,          // capacity retry flags below (OR-ed)
+  ST_RETRY_WCAP = 0x1,       // a wavefront outgrew wcap
+  ST_RETRY_PCAP = 0x2,       // node pool exhausted
+  ST_RETRY_LCAP = 0x4,       // consensus outgrew lcap
+  ST_RETRY_HEAP = 0x8,       // priority queue outgrew pcap
+};
+
+enum StatIdx : int {
+  S_UPDATES = 0,
+  S_WOUT,
+  S_COMPARES,
+  S_EDINC,
+  S_FINALIZES,
+  S_POPS,
+  S_EXPLORED,
+  S_IGNORED,
+  S_PEAKQ,
+  S_NSTAT
+};
+
+struct DevConfig {
+  uint64_t max_queue_size;
+  uint64_t max_capacity_per_size;
+  uint64_t max_return_size;
+  uint64_t max_nodes_wo_constraint;
+  uint64_t min_count;
+  uint64_t dual_max_ed_delta;
+  uint64_t offset_window;
+  uint64_t offset_compare_length;
+  double min_af;
+  int32_t cost_mode;
+  int32_t wildcard;
+  uint32_t weighted;
+  uint32_t early;
+};
+
+struct DevProblem {
+  uint32_t read_begin;  // first read index in the batch read tables
+  uint32_t n_reads;
+  uint32_t max_read_len;
+  uint32_t n_active;    // reads with offset None (after auto-shift)
+};
+
+// Device result record (one per returned consensus); the host turns these into
+// Consensus / DualConsensus values. Layout inside the per-problem output area:
+//   u32 n_results, u32 pad, then R records of
+//   [u32 len1, u32 len2, u32 is_dual, u32 pad][con1: lcap][con2: lcap (dual)]
+//   [fe1: nmax u32][fe2: nmax u32 (dual)]  — finalized edit distances, kInactive = None
+struct EngineArgs {
+  DevConfig cfg;
+  const DevProblem* problems;
+  uint32_t n_problems;
+  uint32_t sides;        // 1 = ConsensusDWFA, 2 = DualConsensusDWFA
+  const uint8_t* rbytes;
+  const uint64_t* roff;
+  const uint32_t* rlen;
+  const int64_t* ractivate;  // per read activation length (-1 = active at root)
+  uint8_t* ws;           // per-workgroup workspace
+  uint64_t ws_stride;
+  uint32_t pcap;         // node slots per workgroup (also heap capacity)
+  uint32_t wcap;         // wavefront entries per read per slot
+  uint32_t lcap;         // consensus capacity per side
+  uint32_t nmax;         // max reads per problem in this batch
+  uint32_t rmax;         // result records per problem
+  uint32_t _pad;
+  uint8_t* out;
+  uint64_t out_stride;
+  uint32_t* status;      // per problem
+  uint64_t* stats;       // per problem x S_NSTAT
+  uint32_t* work_counter;
+};
+
+// ---- byte layouts (host and device compute them identically) ----
+__host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+// one node slot: per side: e[nmax] u32, off[nmax] u32, wf[nmax*wcap] u32, con[lcap]
+__host__ __device__ inline uint64_t side_bytes(uint32_t nmax, uint32_t wcap, uint32_t lcap) {
+  return align16((uint64_t)nmax * 8 + (uint64_t)nmax * wcap * 4) + align16(lcap);
+}
+__host__ __device__ inline uint64_t slot_bytes(uint32_t sides, uint32_t nmax, uint32_t wcap, uint32_t lcap) {
+  return sides * side_bytes(nmax, wcap, lcap);
+}
+// workspace: slots | trackers (2 x 2 arrays of lcap+2 u32) | active arrays (2 x lcap+2 u32) | finalize scratch
+__host__ __device__ inline uint64_t ws_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t wcap,
+                                             uint32_t lcap) {
+  uint64_t t = (uint64_t)pcap * slot_bytes(sides, nmax, wcap, lcap);
+  t += align16((uint64_t)4 * (lcap + 2) * 4);
+  t += align16((uint64_t)2 * (lcap + 2) * 4);
+  t += align16((uint64_t)kWaves * (wcap + 2) * 4);
+  return align16(t);
+}
+__host__ __device__ inline uint64_t result_bytes(uint32_t sides, uint32_t nmax, uint32_t lcap) {
+  return 16 + sides * align16(lcap) + sides * align16((uint64_t)nmax * 4);
+}
+__host__ __device__ inline uint64_t out_bytes(uint32_t sides, uint32_t rmax, uint32_t nmax, uint32_t lcap) {
+  return align16(16 + (uint64_t)rmax * result_bytes(sides, nmax, lcap));
+}
+
+// LDS carve (dynamic shared memory)
+struct HeapEntry {
+  uint64_t cost;
+  uint32_t len;
+  uint32_t slot;
+};
+struct SlotMeta {
+  uint32_t len[2];
+  uint32_t nsome[2];
+  uint32_t flags;  // bit0 dual, bit1 lock1, bit2 lock2
+  uint32_t pad[3];
+};
+struct RInfo {
+  uint8_t n;      // distinct tip symbols (iteration order below)
+  uint8_t end;    // reached_baseline_end
+  uint16_t split; // sum of occurrences
+  uint8_t sym[kKmax];
+  uint16_t occ[kKmax];
+  uint32_t e;     // current edit distance (kInactive = None)
+};
+__host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax) {
+  uint64_t t = (uint64_t)pcap * sizeof(HeapEntry);
+  t += align16((uint64_t)pcap * 4);
+  t += (uint64_t)pcap * sizeof(SlotMeta);
+  t += (uint64_t)sides * nmax * sizeof(RInfo);
+  t += align16((uint64_t)sides * nmax * 4);
+  return align16(t);
+}
+
+}  // namespace wc
