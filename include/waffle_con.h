@@ -101,6 +101,16 @@ int wc_dual_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, const
 int wc_priority_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, const wc_chain_problem* problems,
                                 wc_results** out);
 
+/* Resident batches: upload the reads of many problems to HBM once, then run
+ * any engine over them repeatedly (the throughput path; bench.py times
+ * wc_batch_consensus with the reads already resident). */
+typedef struct wc_batch wc_batch;
+int wc_batch_create(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch** out);
+void wc_batch_free(wc_batch* b);
+uint64_t wc_batch_bytes(const wc_batch* b);
+int wc_batch_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out);
+int wc_batch_dual_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out);
+
 void wc_results_free(wc_results* r);
 uint32_t wc_results_problems(const wc_results* r);
 int wc_results_status(const wc_results* r, uint32_t p);
@@ -191,6 +201,13 @@ int wc_generate_test(uint8_t alphabet, uint64_t seq_len, uint64_t num_samples, d
 const uint8_t* wc_gen_consensus(const wc_gen* g, uint64_t* len);
 const uint8_t* wc_gen_sample(const wc_gen* g, uint64_t i, uint64_t* len);
 void wc_gen_free(wc_gen* g);
+
+/* Known-answer hooks for the RNG restatement: raw ChaCha(rounds) words from a
+ * 32-byte seed; StdRng::from_seed -> next_u64, then StdRng::from_rng -> next_u64;
+ * StdRng::seed_from_u64 words. */
+void wc_rng_words(const uint8_t* seed32, int rounds, uint32_t n, uint32_t* out);
+void wc_rng_stdrng_chain(const uint8_t* seed32, uint64_t* out2);
+void wc_rng_seed_from_u64(uint64_t seed, uint32_t n, uint32_t* out);
 
 /* sequence_alignment.rs:18,36 — pairwise WFA edit distance (host reference API). */
 uint64_t wc_wfa_ed_config(const uint8_t* v1, uint64_t l1, const uint8_t* v2, uint64_t l2, uint8_t require_both_end,

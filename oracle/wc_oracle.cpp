@@ -11,6 +11,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <unordered_map>
@@ -689,6 +691,14 @@ std::vector<DualOut> consensus_dual(const Config& cfg, const std::vector<Seq>& s
   int root = alloc();
   pool[root] = make_root(offsets);
   PQHeap pq;
+  // debug trace of pops (ORC_TRACE=<file>), same record shape as the device trace
+  FILE* trace = getenv("ORC_TRACE") ? fopen(getenv("ORC_TRACE"), "w") : nullptr;
+  struct TraceCloser {
+    FILE*& f;
+    ~TraceCloser() {
+      if (f) fclose(f);
+    }
+  } trace_closer{trace};
   st.insert(0);
   pq.push(root, Prio{dnode_total(pool[root], mode), 0});
 
@@ -741,7 +751,17 @@ std::vector<DualOut> consensus_dual(const Config& cfg, const std::vector<Seq>& s
       at_cap = st.at_capacity(top_len);
     }
     if (top_len >= active_min.size()) throw Error(E_INVARIANT, "active_min_count index out of range");
-    if (top.p.cost > maximum_error || top_len < thr_cut || at_cap || dnode_imbalanced(pool[tid], active_min[top_len])) {
+    const bool ignore =
+        top.p.cost > maximum_error || top_len < thr_cut || at_cap || dnode_imbalanced(pool[tid], active_min[top_len]);
+    if (trace) {
+      uint64_t s1 = 0, s2 = 0;
+      for (auto x : pool[tid].a1) s1 += x;
+      for (auto x : pool[tid].a2) s2 += x;
+      fprintf(trace, "%u %u %u %u\n", (unsigned)top.p.cost, (unsigned)top_len,
+              (unsigned)(pool[tid].is_dual | ((ignore ? 1 : 0) << 1) | (s1 << 8) | (s2 << 20)),
+              (unsigned)active_min[top_len]);
+    }
+    if (ignore) {
       if (c) c->nodes_ignored++;
       free_ids.push_back(tid);
       continue;

@@ -109,11 +109,13 @@ class WcDwfaJob(ctypes.Structure):
 EXPORTED = (
     "wc_config_default", "wc_ctx_create", "wc_ctx_destroy", "wc_last_error",
     "wc_consensus_batch", "wc_dual_consensus_batch", "wc_priority_consensus_batch",
+    "wc_batch_create", "wc_batch_free", "wc_batch_bytes", "wc_batch_consensus", "wc_batch_dual_consensus",
     "wc_results_free", "wc_results_problems", "wc_results_status", "wc_results_error",
     "wc_results_count", "wc_results_single", "wc_results_dual", "wc_results_chain_len",
     "wc_results_chain", "wc_results_sequence_indices", "wc_results_stats",
     "wc_results_problem_stats", "wc_dwfa_batch", "wc_generate_test", "wc_gen_consensus",
-    "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config",
+    "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_rng_words", "wc_rng_stdrng_chain",
+    "wc_rng_seed_from_u64",
 )
 
 
@@ -139,6 +141,12 @@ def lib():
                       ("wc_priority_consensus_batch", WcChainProblem)):
             fn = getattr(L, f)
             fn.argtypes = [vp, ctypes.POINTER(WcConfig), ctypes.c_uint32, ctypes.POINTER(pt), ctypes.POINTER(vp)]
+        L.wc_batch_create.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(WcProblem), ctypes.POINTER(vp)]
+        L.wc_batch_free.argtypes = [vp]
+        L.wc_batch_bytes.argtypes = [vp]
+        L.wc_batch_bytes.restype = ctypes.c_uint64
+        for f in ("wc_batch_consensus", "wc_batch_dual_consensus"):
+            getattr(L, f).argtypes = [vp, vp, ctypes.POINTER(WcConfig), ctypes.POINTER(vp)]
         L.wc_results_free.argtypes = [vp]
         L.wc_results_problems.argtypes = [vp]
         L.wc_results_problems.restype = ctypes.c_uint32

@@ -1,18 +1,19 @@
 // Device-resident consensus engines for MI355X (gfx950).
 //
-// ConsensusDWFA::consensus (consensus.rs:139-351) runs entirely on the GPU:
-// one workgroup per consensus problem pulls problems from a global work
-// counter and executes the reference's least-cost-first search with the
-// reference's exact pop order (priority-queue 1.x heap),
-// candidate order (hashbrown/FxHash iteration, Appendix B) and f64 vote
-// summation order. Node DWFA state lives in a per-workgroup node pool in HBM
-// (copy on branch, in place on single extension); the heap, node metadata and
-// per-read nomination summaries live in LDS.
+// ConsensusDWFA::consensus (consensus.rs:139-351) and
+// DualConsensusDWFA::consensus (dual_consensus.rs:240-787) run entirely on the
+// GPU: one workgroup (4 x wave64) per consensus problem pulls problems from a
+// global work counter and executes the reference's least-cost-first search
+// with the reference's exact pop order (priority-queue 1.x heap, SURVEY
+// Appendix A), candidate order (hashbrown/FxHash iteration, Appendix B) and
+// f64 vote summation order. Node DWFA state lives in a per-workgroup node pool
+// in HBM (clone on branch, in place for the last child); the heap, node
+// metadata and per-read nomination summaries live in LDS.
 //
 // Per pop: ANALYZE (per-read tips + end flags), optional FINALIZE of the
 // popped node on scratch, VOTES (ordered f64 sums), then PUSH of every child
-// (the per-read DWFA update, dynamic_wfa.rs:75-99) with the cost reduction
-// fused in.
+// (the per-read DWFA update, dynamic_wfa.rs:75-99) followed by a prune + cost
+// reduction pass.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -20,31 +21,41 @@
 
 namespace wc {
 
+constexpr int kMaxChild = 64;
+constexpr uint32_t WC_E_INVARIANT_CODE = 10;  // include/waffle_con.h
+constexpr uint32_t WC_E_LIMIT_CODE = 11;
+
 struct Ctl {
-  uint32_t prob, n, read_begin, max_read_len;
+  uint32_t prob;
   uint32_t heap_n, nfree;
   uint32_t status;
   uint32_t action;  // 0 expand, 1 ignore, 2 done
   uint32_t top_slot, top_len;
+  uint32_t top_dual;
   uint64_t top_cost;
-  uint32_t n_end;
-  uint32_t multi;
+  uint32_t n_end[2];
+  uint32_t n_either;
   uint32_t ovf;
   uint32_t reached;
+  uint32_t fin[2];
   uint64_t cost_acc;
+  uint32_t some_acc[2];
   uint64_t max_err;
   uint64_t farthest[2], last_constraint[2];
   uint64_t trk_total[2], trk_thr[2];
+  uint32_t am_len;
   uint32_t n_ret;
   int32_t store_idx;
+  uint32_t nkeys[2];
+  uint8_t keys[2][kKout];
+  double vals[2][kKout];
   uint32_t nchild;
-  uint32_t cur_child;
-  uint8_t child_sym[kKout];
-  uint32_t child_slot[kKout];
-  uint64_t child_cost[kKout];
-  uint32_t nkeys;
-  uint8_t keys[kKout];
-  double vals[kKout];
+  int16_t ch_s[kMaxChild][2];  // symbol per side, -1 = none (lock for dual children)
+  uint8_t ch_kind[kMaxChild];  // 0 dual child, 1 stay-single, 2 split (activate_dual)
+  uint32_t ch_slot[kMaxChild];
+  uint64_t ch_cost[kMaxChild];
+  uint32_t ch_len[kMaxChild];
+  uint32_t cur_slot;
   uint64_t cnt[S_NSTAT];
 };
 
@@ -52,8 +63,8 @@ struct Lds {
   HeapEntry* heap;
   uint32_t* freestack;
   SlotMeta* meta;
-  RInfo* rinfo;    // [sides][nmax]
-  uint32_t* fe;    // [sides][nmax]
+  RInfo* rinfo;  // [sides][nmax]
+  uint32_t* fe;  // [sides][nmax]
 };
 
 __device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32_t nmax) {
@@ -135,6 +146,13 @@ struct TrackerRef {
   }
 };
 
+__device__ inline uint64_t ceil_u64(double x) {
+  double c = ceil(x);
+  if (!(c > 0.0)) return 0;  // Rust `as u64` saturates negatives / NaN to 0
+  if (c >= 18446744073709551615.0) return ~0ull;
+  return (uint64_t)c;
+}
+
 __device__ inline void flush_counters(Ctl& ctl, const WaveCounters& wc) {
   if (lane_id() == 0) {
     if (wc.updates) atomicAdd((unsigned long long*)&ctl.cnt[S_UPDATES], (unsigned long long)wc.updates);
@@ -145,148 +163,323 @@ __device__ inline void flush_counters(Ctl& ctl, const WaveCounters& wc) {
   }
 }
 
-// ---- VOTES: ConsensusNode::get_extension_candidates (consensus.rs:540-564) ----
-// Wave 0 only. Outer-map insertion order = first appearance over (read index,
-// inner iteration position); values are summed per key strictly in read order
-// (the reference's f64 order). Writes ctl.keys/vals in iteration order, with
-// the wildcard removed when other keys exist. Returns false on > kKout keys.
-__device__ inline bool wave_votes(Ctl& ctl, const RInfo* ri, uint32_t n, const float* weights_unused, int wc) {
+// per-workgroup engine context (registers)
+struct Eng {
+  const EngineArgs* A;
+  uint8_t* ws;
+  uint64_t sbytes;
+  uint32_t nmax, wcap, lcap, pcap, sides, n;
+  uint32_t* trk_lc[2];
+  uint32_t* trk_pc[2];
+  uint32_t* total_active;
+  uint32_t* active_min;
+  uint32_t* scratch;
+  DevProblem P;
+  Lds L;
+  __device__ SideView sv(uint32_t slot, uint32_t side) const {
+    return side_view(ws + (uint64_t)slot * sbytes, side, nmax, wcap, lcap);
+  }
+  __device__ const uint8_t* read(uint32_t r) const { return A->rbytes + A->roff[P.read_begin + r]; }
+  __device__ uint32_t rlen(uint32_t r) const { return A->rlen[P.read_begin + r]; }
+  __device__ TrackerRef tracker(Ctl& ctl, int k) const {
+    return TrackerRef{trk_lc[k], trk_pc[k], &ctl.trk_total[k], &ctl.trk_thr[k], A->cfg.max_capacity_per_size};
+  }
+};
+
+__device__ inline Eng make_eng(const EngineArgs& A, uint8_t* smem) {
+  Eng E;
+  E.A = &A;
+  E.nmax = A.nmax;
+  E.wcap = A.wcap;
+  E.lcap = A.lcap;
+  E.pcap = A.pcap;
+  E.sides = A.sides;
+  E.ws = A.ws + (uint64_t)blockIdx.x * A.ws_stride;
+  E.sbytes = slot_bytes(A.sides, A.nmax, A.wcap, A.lcap);
+  uint32_t* t = (uint32_t*)(E.ws + (uint64_t)A.pcap * E.sbytes);
+  const uint32_t L2 = A.lcap + 2;
+  E.trk_lc[0] = t;
+  E.trk_pc[0] = t + L2;
+  E.trk_lc[1] = t + 2 * L2;
+  E.trk_pc[1] = t + 3 * L2;
+  uint8_t* q = E.ws + (uint64_t)A.pcap * E.sbytes + align16((uint64_t)4 * L2 * 4);
+  E.total_active = (uint32_t*)q;
+  E.active_min = E.total_active + L2;
+  q += align16((uint64_t)2 * L2 * 4);
+  E.scratch = (uint32_t*)q + (uint64_t)wave_id() * (A.wcap + 2);
+  E.L = carve(smem, A.sides, A.pcap, A.nmax);
+  return E;
+}
+
+// ---- per-problem init: free stack, trackers, root node ----
+__device__ inline void init_problem(Eng& E, Ctl& ctl) {
+  const int tid = threadIdx.x;
+  const DevConfig& cfg = E.A->cfg;
+  if (tid == 0) {
+    ctl.heap_n = 0;
+    ctl.nfree = E.pcap - 1;  // slot 0 (stack top) becomes the root
+    ctl.status = ST_OK;
+    ctl.max_err = ~0ull;
+    for (int k = 0; k < 2; ++k) {
+      ctl.farthest[k] = 0;
+      ctl.last_constraint[k] = 0;
+      ctl.trk_total[k] = 0;
+      ctl.trk_thr[k] = 0;
+    }
+    ctl.n_ret = 0;
+    ctl.am_len = 1;
+    for (int s = 0; s < S_NSTAT; ++s) ctl.cnt[s] = 0;
+  }
+  for (uint32_t i = tid; i < E.pcap; i += kBlock) E.L.freestack[i] = E.pcap - 1 - i;
+  for (uint32_t i = tid; i < 4 * (E.lcap + 2); i += kBlock) E.trk_lc[0][i] = 0;
+  SideView v = E.sv(0, 0);
+  for (uint32_t r = tid; r < E.n; r += kBlock) {
+    const bool act = E.A->ractivate[E.P.read_begin + r] < 0;
+    v.e[r] = act ? 0u : kInactive;
+    v.off[r] = 0;
+    v.wf[(uint64_t)r * E.wcap] = 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    SlotMeta& m = E.L.meta[0];
+    m.len[0] = m.len[1] = 0;
+    m.nsome[0] = E.P.n_active;
+    m.nsome[1] = 0;
+    m.flags = 0;
+    E.total_active[0] = E.P.n_active;
+    E.active_min[0] = (uint32_t)max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.P.n_active));
+    E.tracker(ctl, 0).insert(0);
+    heap_push(E.L.heap, ctl.heap_n, HeapEntry{0, 0, 0});
+  }
+  __syncthreads();
+}
+
+// ---- ANALYZE one side of a node: per-read tips / end flags into rinfo ----
+__device__ inline void analyze_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t side, uint32_t len, RInfo* out) {
   const int lane = lane_id();
+  SideView v = E.sv(slot, side);
+  for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
+    const uint32_t e = v.e[r];
+    if (e == kInactive) {
+      if (lane == 0) {
+        out[r].e = kInactive;
+        out[r].n = 0;
+        out[r].end = 0;
+      }
+      continue;
+    }
+    bool ok = wave_analyze_read(v.wf + (uint64_t)r * E.wcap, e, v.off[r], E.read(r), E.rlen(r), len, &out[r]);
+    if (lane == 0) {
+      if (!ok) atomicOr(&ctl.ovf, 1u);
+      if (out[r].end) atomicAdd(&ctl.n_end[side], 1u);
+    }
+  }
+}
+
+// ---- FINALIZE one side on scratch (the node is not modified) ----
+__device__ inline void finalize_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t side, uint32_t len, uint32_t* fe,
+                                     WaveCounters& cnt) {
+  const int lane = lane_id();
+  SideView v = E.sv(slot, side);
+  for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
+    const uint32_t e = v.e[r];
+    if (e == kInactive) {
+      if (lane == 0) fe[r] = kInactive;
+      continue;
+    }
+    uint32_t f = 0;
+    bool ok = wave_finalize_read(v.wf + (uint64_t)r * E.wcap, e, v.off[r], E.read(r), E.rlen(r), v.con, len,
+                                 E.A->cfg.wildcard, E.scratch, E.wcap, f, cnt);
+    if (lane == 0) {
+      if (!ok) atomicOr(&ctl.ovf, 4u);
+      fe[r] = ok ? f : kInactive;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ---- PUSH symbols onto up to two sides of one node (sym < 0 = untouched) ----
+// Work items are (side, read) pairs spread over the waves. The new symbol is
+// already written at con[len-1] of each pushed side. Optional single-side
+// cost accumulation (ConsensusNode::priority, consensus.rs:480-510).
+__device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
+                                  bool want_cost, WaveCounters& cnt) {
+  const int lane = lane_id();
+  const DevConfig& cfg = E.A->cfg;
+  uint64_t cost = 0;
+  const uint32_t items = 2 * E.n;
+  for (uint32_t it = wave_id(); it < items; it += kWaves) {
+    const uint32_t side = it / E.n, r = it % E.n;
+    const int sym = side == 0 ? s0 : s1;
+    if (sym < 0) continue;
+    SideView v = E.sv(slot, side);
+    uint32_t e = v.e[r];
+    if (e == kInactive) continue;
+    const uint32_t olen = side == 0 ? len0 : len1;
+    bool ok = wave_push_read(v.wf + (uint64_t)r * E.wcap, e, v.off[r], E.read(r), E.rlen(r), v.con, olen,
+                             (uint8_t)sym, cfg.wildcard, cfg.early != 0, E.wcap, cnt);
+    if (!ok) {
+      if (lane == 0) atomicOr(&ctl.ovf, 4u);
+      continue;
+    }
+    if (lane == 0) v.e[r] = e;
+    cost += cost_of(e, cfg.cost_mode);
+  }
+  if (want_cost && lane == 0 && cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);
+}
+
+// ---- clone a node (consensus bytes + live wavefront rows) ----
+__device__ inline void copy_node(Eng& E, uint32_t src, uint32_t dst, uint32_t nsides, const uint32_t* lens) {
+  const int tid = threadIdx.x, lane = lane_id();
+  for (uint32_t s = 0; s < nsides; ++s) {
+    SideView a = E.sv(src, s), b = E.sv(dst, s);
+    for (uint32_t i = tid; i < lens[s]; i += kBlock) b.con[i] = a.con[i];
+    for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
+      const uint32_t e = a.e[r];
+      if (lane == 0) {
+        b.e[r] = e;
+        b.off[r] = a.off[r];
+      }
+      if (e == kInactive) continue;
+      const uint32_t W = 2 * e + 1;
+      for (uint32_t i = lane; i < W; i += 64) b.wf[(uint64_t)r * E.wcap + i] = a.wf[(uint64_t)r * E.wcap + i];
+    }
+  }
+}
+
+// ---- VOTES (consensus.rs:540-564 / dual_consensus.rs:1242-1290) ----
+// One wave. Outer-map insertion order = first appearance over (read index,
+// inner iteration position); values are summed per key strictly in read order
+// (the reference's f64 order), weight * occ / split. Weights follow
+// get_ed_weights (dual_consensus.rs:1299-1336) when `weighted`. Writes keys /
+// vals of `side` in iteration order with the wildcard removed when other keys
+// exist. Returns false on > kKout keys.
+__device__ inline double vote_weight(const RInfo* r0, const RInfo* r1, uint32_t r, bool is_dual, bool side1) {
+  if (!is_dual) return 1.0;
+  const bool h1 = r0[r].e != kInactive, h2 = r1[r].e != kInactive;
+  const double v1 = h1 ? fmax((double)r0[r].e, 0.5) : 0.0;
+  const double v2 = h2 ? fmax((double)r1[r].e, 0.5) : 0.0;
+  if (h1 && h2) return (side1 ? v2 : v1) / (v1 + v2);
+  if ((h1 && side1) || (h2 && !side1)) return 1.0;
+  return 0.0;
+}
+
+__device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, const RInfo* r0, const RInfo* r1,
+                                  uint32_t n, bool weighted, bool is_dual, int wc) {
+  const int lane = lane_id();
+  const bool side1 = side == 0;
   uint32_t known[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint8_t ins[kKout];
   uint32_t nk = 0;
-  bool ok = true;
-  for (uint32_t base = 0; base < n && ok; base += 64) {
-    uint32_t r = base + lane;
+  for (uint32_t base = 0; base < n; base += 64) {
+    const uint32_t r = base + lane;
+    bool voter = r < n && ri[r].e != kInactive;
+    if (voter && weighted) voter = vote_weight(r0, r1, r, is_dual, side1) > 0.0;
     for (;;) {
       uint32_t cand = 0xFFFF;
-      if (r < n && ri[r].e != kInactive) {
+      if (voter) {
         const RInfo& x = ri[r];
         for (uint32_t k = 0; k < x.n; ++k) {
-          uint8_t s = x.sym[k];
+          const uint8_t s = x.sym[k];
           if (!((known[s >> 5] >> (s & 31)) & 1u)) {
             cand = s;
             break;
           }
         }
       }
-      uint64_t m = ballot(cand != 0xFFFF);
+      const uint64_t m = ballot(cand != 0xFFFF);
       if (!m) break;
-      int first = __ffsll((unsigned long long)m) - 1;
-      uint32_t s = (uint32_t)__shfl((int)cand, first, 64);
-      if (nk == kKout) {
-        ok = false;
-        break;
-      }
+      const int first = __ffsll((unsigned long long)m) - 1;
+      const uint32_t s = (uint32_t)__shfl((int)cand, first, 64);
+      if (nk == kKout) return false;
       ins[nk++] = (uint8_t)s;
       known[s >> 5] |= 1u << (s & 31);
     }
   }
-  if (!ok) return false;
   uint8_t ord[kKout];
   fx_order(ins, nk, ord);
-  // iteration order keys, wildcard removal (consensus.rs:556-561)
   uint8_t keys[kKout];
   uint32_t m = 0;
-  bool drop_wc = wc >= 0 && nk > 1;
+  const bool drop_wc = wc >= 0 && nk > 1;
   for (uint32_t k = 0; k < nk; ++k) {
-    uint8_t s = ins[ord[k]];
+    const uint8_t s = ins[ord[k]];
     if (drop_wc && s == (uint8_t)wc) continue;
     keys[m++] = s;
   }
-  // per-key ordered sums: lane j owns key j
-  double acc = 0.0;
   if ((uint32_t)lane < m) {
-    uint8_t key = keys[lane];
+    const uint8_t key = keys[lane];
+    double acc = 0.0;
     for (uint32_t r = 0; r < n; ++r) {
       const RInfo& x = ri[r];
       if (x.e == kInactive) continue;
+      double w = 1.0;
+      if (weighted) {
+        w = vote_weight(r0, r1, r, is_dual, side1);
+        if (!(w > 0.0)) continue;
+      }
       for (uint32_t k = 0; k < x.n; ++k) {
         if (x.sym[k] == key) {
-          acc += (double)x.occ[k] / (double)x.split;
+          acc += w * (double)x.occ[k] / (double)x.split;
           break;
         }
       }
     }
-    ctl.keys[lane] = key;
-    ctl.vals[lane] = acc;
+    ctl.keys[side][lane] = key;
+    ctl.vals[side][lane] = acc;
   }
-  if (lane == 0) ctl.nkeys = m;
+  if (lane == 0) ctl.nkeys[side] = m;
   return true;
 }
 
-// ---- ConsensusDWFA engine ----
+// ---- write one result record (finalized node) ----
+__device__ inline void store_record(Eng& E, Ctl& ctl, uint8_t* outp, uint32_t slot, uint32_t nsides,
+                                    const uint32_t* lens, bool is_dual) {
+  const int tid = threadIdx.x;
+  const uint64_t rb = result_bytes(E.sides, E.nmax, E.lcap);
+  uint8_t* rec = outp + 16 + (uint64_t)ctl.store_idx * rb;
+  for (uint32_t s = 0; s < E.sides; ++s) {
+    uint8_t* rcon = rec + 16 + s * align16(E.lcap);
+    uint32_t* rfe = (uint32_t*)(rec + 16 + E.sides * align16(E.lcap) + s * align16((uint64_t)E.nmax * 4));
+    if (s < nsides) {
+      SideView v = E.sv(slot, s);
+      for (uint32_t i = tid; i < lens[s]; i += kBlock) rcon[i] = v.con[i];
+    }
+    for (uint32_t r = tid; r < E.n; r += kBlock) rfe[r] = s < nsides ? E.L.fe[s * E.nmax + r] : kInactive;
+  }
+  if (tid == 0) {
+    uint32_t* h = (uint32_t*)rec;
+    h[0] = lens[0];
+    h[1] = nsides > 1 ? lens[1] : 0;
+    h[2] = is_dual ? 1u : 0u;
+  }
+}
+
+// =====================================================================
+// ConsensusDWFA engine (consensus.rs:139-351)
+// =====================================================================
 __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl;
   const int tid = threadIdx.x;
   const int lane = lane_id();
-  const int wave = wave_id();
   const DevConfig& cfg = A.cfg;
-  const int wc = cfg.wildcard;
   const bool early = cfg.early != 0;
-  const uint32_t nmax = A.nmax, wcap = A.wcap, lcap = A.lcap, pcap = A.pcap;
-  Lds L = carve(smem, 1, pcap, nmax);
-  uint8_t* ws = A.ws + (uint64_t)blockIdx.x * A.ws_stride;
-  const uint64_t sbytes = slot_bytes(1, nmax, wcap, lcap);
-  uint32_t* trk_lc = (uint32_t*)(ws + (uint64_t)pcap * sbytes);
-  uint32_t* trk_pc = trk_lc + (lcap + 2);
-  uint32_t* scratch_base =
-      (uint32_t*)(ws + (uint64_t)pcap * sbytes + align16((uint64_t)4 * (lcap + 2) * 4) + align16((uint64_t)2 * (lcap + 2) * 4));
-  uint32_t* scratch = scratch_base + (uint64_t)wave * (wcap + 2);
-  const uint32_t rmax = A.rmax;
-  const uint64_t rbytes_sz = result_bytes(1, nmax, lcap);
+  Eng E = make_eng(A, smem);
 
   for (;;) {
     if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
     __syncthreads();
     const uint32_t prob = ctl.prob;
     if (prob >= A.n_problems) break;
-    const DevProblem P = A.problems[prob];
-    const uint32_t n = P.n_reads;
+    E.P = A.problems[prob];
+    E.n = E.P.n_reads;
     uint8_t* outp = A.out + (uint64_t)prob * A.out_stride;
+    init_problem(E, ctl);
 
-    // ---- init ----
-    if (tid == 0) {
-      ctl.heap_n = 0;
-      ctl.nfree = pcap;
-      ctl.status = ST_OK;
-      ctl.max_err = ~0ull;
-      ctl.farthest[0] = 0;
-      ctl.last_constraint[0] = 0;
-      ctl.trk_total[0] = 0;
-      ctl.trk_thr[0] = 0;
-      ctl.n_ret = 0;
-      for (int s = 0; s < S_NSTAT; ++s) ctl.cnt[s] = 0;
-    }
-    for (uint32_t i = tid; i < pcap; i += kBlock) L.freestack[i] = pcap - 1 - i;
-    for (uint32_t i = tid; i < 2 * (lcap + 2); i += kBlock) trk_lc[i] = 0;
-    __syncthreads();
-    // root node (consensus.rs:384-403): reads with offset None start active
-    const uint32_t root = pcap - 1;  // top of the free stack
-    {
-      SideView v = side_view(ws + (uint64_t)root * sbytes, 0, nmax, wcap, lcap);
-      for (uint32_t r = tid; r < n; r += kBlock) {
-        const bool act = A.ractivate[P.read_begin + r] < 0;
-        v.e[r] = act ? 0u : kInactive;
-        v.off[r] = 0;
-        v.wf[(uint64_t)r * wcap] = 0;
-      }
-    }
-    if (tid == 0) {
-      ctl.nfree = pcap - 1;
-      L.meta[root].len[0] = 0;
-      L.meta[root].flags = 0;
-      TrackerRef t{trk_lc, trk_pc, &ctl.trk_total[0], &ctl.trk_thr[0], cfg.max_capacity_per_size};
-      t.insert(0);
-      heap_push(L.heap, ctl.heap_n, HeapEntry{0, 0, root});
-    }
-    __syncthreads();
-
-    // ---- search loop (consensus.rs:224-340) ----
     for (;;) {
+      // ---- pop (consensus.rs:224-251) ----
       if (tid == 0) {
-        TrackerRef t{trk_lc, trk_pc, &ctl.trk_total[0], &ctl.trk_thr[0], cfg.max_capacity_per_size};
+        TrackerRef t = E.tracker(ctl, 0);
         if (ctl.heap_n == 0) {
           ctl.action = 2;
         } else {
@@ -297,14 +490,14 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
             t.increment_threshold();
             ctl.last_constraint[0] = 0;
           }
-          HeapEntry top = heap_pop(L.heap, ctl.heap_n);
+          HeapEntry top = heap_pop(E.L.heap, ctl.heap_n);
           t.remove(top.len);
           ctl.top_slot = top.slot;
           ctl.top_len = top.len;
           ctl.top_cost = top.cost;
           if (top.cost > ctl.max_err || top.len < ctl.trk_thr[0] || t.at_capacity(top.len)) {
             ctl.cnt[S_IGNORED]++;
-            L.freestack[ctl.nfree++] = top.slot;
+            E.L.freestack[ctl.nfree++] = top.slot;
             ctl.action = 1;
           } else {
             ctl.farthest[0] = max(ctl.farthest[0], (uint64_t)top.len);
@@ -314,10 +507,8 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
             ctl.action = 0;
           }
         }
-        ctl.n_end = 0;
-        ctl.multi = 0;
+        ctl.n_end[0] = 0;
         ctl.ovf = 0;
-        ctl.cost_acc = 0;
       }
       __syncthreads();
       if (ctl.action == 2) break;
@@ -326,221 +517,144 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
 
       const uint32_t top = ctl.top_slot;
       const uint32_t len = ctl.top_len;
-      SideView tv = side_view(ws + (uint64_t)top * sbytes, 0, nmax, wcap, lcap);
+      SideView tv = E.sv(top, 0);
 
-      // ---- ANALYZE: tips + reached_baseline_end per read ----
-      {
-        for (uint32_t r = wave; r < n; r += kWaves) {
-          const uint32_t e = tv.e[r];
-          if (e == kInactive) {
-            if (lane == 0) {
-              L.rinfo[r].e = kInactive;
-              L.rinfo[r].n = 0;
-              L.rinfo[r].end = 0;
-            }
-            continue;
-          }
-          const uint64_t ro = A.roff[P.read_begin + r];
-          const uint32_t blen = A.rlen[P.read_begin + r];
-          bool ok = wave_analyze_read(tv.wf + (uint64_t)r * wcap, e, tv.off[r], A.rbytes + ro, blen, len, &L.rinfo[r]);
-          if (lane == 0) {
-            if (!ok) atomicOr(&ctl.ovf, 1u);
-            if (L.rinfo[r].end) atomicAdd(&ctl.n_end, 1u);
-          }
-        }
-      }
+      analyze_side(E, ctl, top, 0, len, E.L.rinfo);
       __syncthreads();
       if (tid == 0) {
-        const uint32_t ne = ctl.n_end;
-        ctl.reached = early ? (ne == n) : (ne > 0);
-        if (ctl.ovf) ctl.status = 11u;
+        const uint32_t ne = ctl.n_end[0];
+        ctl.reached = early ? (ne == E.n) : (ne > 0);  // consensus.rs:516-532
+        if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
       }
       __syncthreads();
       if (ctl.status != ST_OK) break;
 
-      // ---- FINALIZE a clone when any (all, with early termination) read is at its end ----
+      // ---- finalize a clone (consensus.rs:254-279) ----
       if (ctl.reached) {
         WaveCounters cnt = {0, 0, 0, 0, 0};
-        for (uint32_t r = wave; r < n; r += kWaves) {
-          const uint32_t e = tv.e[r];
-          if (e == kInactive) {
-            if (lane == 0) atomicOr(&ctl.ovf, 2u);  // Finalize called on DWFA that was never initialized.
-            continue;
-          }
-          const uint64_t ro = A.roff[P.read_begin + r];
-          const uint32_t blen = A.rlen[P.read_begin + r];
-          uint32_t fe;
-          bool ok = wave_finalize_read(tv.wf + (uint64_t)r * wcap, e, tv.off[r], A.rbytes + ro, blen, tv.con, len, wc,
-                                       scratch, wcap, fe, cnt);
-          if (!ok) {
-            if (lane == 0) atomicOr(&ctl.ovf, 4u);
-            continue;
-          }
-          if (lane == 0) L.fe[r] = fe;
-          __builtin_amdgcn_wave_barrier();
-        }
+        finalize_side(E, ctl, top, 0, len, E.L.fe, cnt);
         flush_counters(ctl, cnt);
         __syncthreads();
         if (tid == 0) {
           ctl.store_idx = -1;
-          if (ctl.ovf & 2u) {
-            ctl.status = 1;
-          } else if (ctl.ovf & 4u) {
+          if (ctl.ovf & 4u) {
             ctl.status = ST_RETRY | ST_RETRY_WCAP;
           } else {
             uint64_t total = 0;
-            for (uint32_t r = 0; r < n; ++r) total += cost_of(L.fe[r], cfg.cost_mode);
-            if (total < ctl.max_err) {
-              ctl.max_err = total;
-              ctl.n_ret = 0;
+            bool uninit = false;
+            for (uint32_t r = 0; r < E.n; ++r) {
+              if (E.L.fe[r] == kInactive) uninit = true;
+              else total += cost_of(E.L.fe[r], cfg.cost_mode);
             }
-            if (total <= ctl.max_err && ctl.n_ret < cfg.max_return_size) {
-              if (ctl.n_ret < rmax) ctl.store_idx = (int32_t)ctl.n_ret;
-              ctl.n_ret++;
+            if (uninit) {
+              ctl.status = 1;  // "Finalize called on DWFA that was never initialized."
+            } else {
+              if (total < ctl.max_err) {
+                ctl.max_err = total;
+                ctl.n_ret = 0;
+              }
+              if (total <= ctl.max_err && ctl.n_ret < cfg.max_return_size) {
+                if (ctl.n_ret < A.rmax) ctl.store_idx = (int32_t)ctl.n_ret;
+                ctl.n_ret++;
+              }
             }
           }
         }
         __syncthreads();
         if (ctl.status != ST_OK) break;
         if (ctl.store_idx >= 0) {
-          uint8_t* rec = outp + 16 + (uint64_t)ctl.store_idx * rbytes_sz;
-          uint8_t* rcon = rec + 16;
-          uint32_t* rfe = (uint32_t*)(rec + 16 + align16(lcap));
-          for (uint32_t i = tid; i < len; i += kBlock) rcon[i] = tv.con[i];
-          for (uint32_t r = tid; r < n; r += kBlock) rfe[r] = L.fe[r];
-          if (tid == 0) {
-            uint32_t* h = (uint32_t*)rec;
-            h[0] = len;
-            h[1] = 0;
-            h[2] = 0;
-          }
+          const uint32_t lens[2] = {len, 0};
+          store_record(E, ctl, outp, top, 1, lens, false);
         }
       }
 
-      // ---- VOTES + child selection (consensus.rs:283-321) ----
-      if (wave == 0) {
-        bool ok = wave_votes(ctl, L.rinfo, n, nullptr, wc);
+      // ---- votes + child selection (consensus.rs:283-321) ----
+      if (wave_id() == 0) {
+        const bool ok = wave_votes(ctl, 0, E.L.rinfo, E.L.rinfo, E.L.rinfo, E.n, false, false, cfg.wildcard);
         if (lane == 0) {
           if (!ok) {
-            ctl.status = 11u;
+            ctl.status = WC_E_LIMIT_CODE;
           } else {
             double max_obs = 0.0;
             bool have = false;
-            for (uint32_t k = 0; k < ctl.nkeys; ++k) {
-              if (!have || ctl.vals[k] >= max_obs) max_obs = ctl.vals[k];
+            for (uint32_t k = 0; k < ctl.nkeys[0]; ++k) {
+              if (!have || ctl.vals[0][k] >= max_obs) max_obs = ctl.vals[0][k];
               have = true;
             }
             if (!have) max_obs = (double)cfg.min_count;
             const double thr = fmin((double)cfg.min_count, max_obs);
             uint32_t nc = 0;
-            for (uint32_t k = 0; k < ctl.nkeys; ++k)
-              if (ctl.vals[k] >= thr) ctl.child_sym[nc++] = ctl.keys[k];
+            for (uint32_t k = 0; k < ctl.nkeys[0]; ++k)
+              if (ctl.vals[0][k] >= thr) {
+                ctl.ch_s[nc][0] = ctl.keys[0][k];
+                ctl.ch_s[nc][1] = -1;
+                nc++;
+              }
             ctl.nchild = nc;
-            if (nc == 0 && len < ctl.max_read_len) {
-              // coverage gap: only reachable with activation offsets (max_activate)
-            }
           }
         }
       }
       __syncthreads();
       if (ctl.status != ST_OK) break;
-
       const uint32_t nc = ctl.nchild;
       if (nc == 0) {
-        if (tid == 0) L.freestack[ctl.nfree++] = top;
+        if (tid == 0) E.L.freestack[ctl.nfree++] = top;
         __syncthreads();
         continue;
       }
-      if (len + 1 > lcap) {
+      if (len + 1 > E.lcap) {
         if (tid == 0) ctl.status = ST_RETRY | ST_RETRY_LCAP;
         __syncthreads();
         break;
       }
-      // ---- PUSH each child: clone when 2+, in place when 1 ----
+      // ---- push every child: clones first, the last child in place ----
       for (uint32_t c = 0; c < nc; ++c) {
         if (tid == 0) {
           uint32_t slot = top;
-          if (nc > 1) {
-            if (ctl.nfree == 0) {
-              ctl.status = ST_RETRY | ST_RETRY_PCAP;
-            } else {
-              slot = L.freestack[--ctl.nfree];
-            }
+          if (c + 1 < nc) {
+            if (ctl.nfree == 0) ctl.status = ST_RETRY | ST_RETRY_PCAP;
+            else slot = E.L.freestack[--ctl.nfree];
           }
-          ctl.child_slot[c] = slot;
+          ctl.cur_slot = slot;
           ctl.cost_acc = 0;
           ctl.ovf = 0;
         }
         __syncthreads();
         if (ctl.status != ST_OK) break;
-        const uint32_t slot = ctl.child_slot[c];
-        SideView cv = side_view(ws + (uint64_t)slot * sbytes, 0, nmax, wcap, lcap);
-        const uint8_t sym = ctl.child_sym[c];
+        const uint32_t slot = ctl.cur_slot;
         if (slot != top) {
-          // clone: consensus bytes + per-read (e, off, live wavefront)
-          for (uint32_t i = tid; i < len; i += kBlock) cv.con[i] = tv.con[i];
-          for (uint32_t r = wave; r < n; r += kWaves) {
-            const uint32_t e = tv.e[r];
-            if (lane == 0) {
-              cv.e[r] = e;
-              cv.off[r] = tv.off[r];
-            }
-            if (e == kInactive) continue;
-            const uint32_t W = 2 * e + 1;
-            for (uint32_t i = lane; i < W; i += 64) cv.wf[(uint64_t)r * wcap + i] = tv.wf[(uint64_t)r * wcap + i];
-          }
+          const uint32_t lens[2] = {len, 0};
+          copy_node(E, top, slot, 1, lens);
         }
-        if (tid == 0) cv.con[len] = sym;
+        if (tid == 0) E.sv(slot, 0).con[len] = (uint8_t)ctl.ch_s[c][0];
         __syncthreads();
         WaveCounters cnt = {0, 0, 0, 0, 0};
-        uint64_t cost = 0;
-        for (uint32_t r = wave; r < n; r += kWaves) {
-          uint32_t e = cv.e[r];
-          if (e == kInactive) continue;
-          const uint64_t ro = A.roff[P.read_begin + r];
-          const uint32_t blen = A.rlen[P.read_begin + r];
-          bool ok = wave_push_read(cv.wf + (uint64_t)r * wcap, e, cv.off[r], A.rbytes + ro, blen, cv.con, len + 1, sym,
-                                   wc, early, wcap, cnt);
-          if (!ok) {
-            if (lane == 0) atomicOr(&ctl.ovf, 4u);
-            continue;
-          }
-          if (lane == 0) cv.e[r] = e;
-          cost += cost_of(e, cfg.cost_mode);
-        }
+        push_sides(E, ctl, slot, ctl.ch_s[c][0], -1, len + 1, 0, true, cnt);
         flush_counters(ctl, cnt);
-        if (lane == 0 && cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);
         __syncthreads();
         if (tid == 0) {
           if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
-          ctl.child_cost[c] = ctl.cost_acc;
-          L.meta[slot].len[0] = len + 1;
+          ctl.ch_cost[c] = ctl.cost_acc;
+          ctl.ch_slot[c] = slot;
+          E.L.meta[slot].len[0] = len + 1;
         }
         __syncthreads();
         if (ctl.status != ST_OK) break;
       }
       if (ctl.status != ST_OK) break;
       if (tid == 0) {
-        if (nc > 1) L.freestack[ctl.nfree++] = top;
-        TrackerRef t{trk_lc, trk_pc, &ctl.trk_total[0], &ctl.trk_thr[0], cfg.max_capacity_per_size};
+        TrackerRef t = E.tracker(ctl, 0);
         for (uint32_t c = 0; c < nc; ++c) {
           t.insert(len + 1);
-          if (ctl.heap_n >= pcap) {
-            ctl.status = ST_RETRY | ST_RETRY_HEAP;
-            break;
-          }
-          heap_push(L.heap, ctl.heap_n, HeapEntry{ctl.child_cost[c], len + 1, ctl.child_slot[c]});
+          heap_push(E.L.heap, ctl.heap_n, HeapEntry{ctl.ch_cost[c], len + 1, ctl.ch_slot[c]});
         }
       }
       __syncthreads();
-      if (ctl.status != ST_OK) break;
     }
 
-    // ---- outputs ----
     __syncthreads();
     if (tid == 0) {
-      uint32_t* h = (uint32_t*)outp;
-      h[0] = min(ctl.n_ret, rmax);
+      ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
       A.status[prob] = ctl.status;
       for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)prob * S_NSTAT + s] = ctl.cnt[s];
     }
@@ -548,18 +662,471 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
   }
 }
 
-}  // namespace wc
+// =====================================================================
+// DualConsensusDWFA engine (dual_consensus.rs:240-787)
+// =====================================================================
+__global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Ctl ctl;
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const DevConfig& cfg = A.cfg;
+  const bool early = cfg.early != 0;
+  const bool weighted = cfg.weighted != 0;
+  Eng E = make_eng(A, smem);
+  RInfo* R0 = E.L.rinfo;
+  RInfo* R1 = E.L.rinfo + E.nmax;
 
-namespace wc {
+  for (;;) {
+    if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
+    __syncthreads();
+    const uint32_t prob = ctl.prob;
+    if (prob >= A.n_problems) break;
+    E.P = A.problems[prob];
+    E.n = E.P.n_reads;
+    uint8_t* outp = A.out + (uint64_t)prob * A.out_stride;
+    init_problem(E, ctl);
+    const uint64_t full_min = max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.n));
+
+    for (;;) {
+      // ---- pop (dual_consensus.rs:340-397) ----
+      if (tid == 0) {
+        if (ctl.heap_n == 0) {
+          ctl.action = 2;
+        } else {
+          ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)ctl.heap_n);
+          ctl.cnt[S_POPS]++;
+          for (int k = 0; k < 2; ++k) {
+            TrackerRef t = E.tracker(ctl, k);
+            while ((ctl.trk_total[k] > cfg.max_queue_size || ctl.last_constraint[k] >= cfg.max_nodes_wo_constraint) &&
+                   ctl.trk_thr[k] < ctl.farthest[k]) {
+              t.increment_threshold();
+              ctl.last_constraint[k] = 0;
+            }
+          }
+          HeapEntry top = heap_pop(E.L.heap, ctl.heap_n);
+          const SlotMeta& m = E.L.meta[top.slot];
+          const uint32_t dual = m.flags & 1u;
+          TrackerRef t = E.tracker(ctl, dual);
+          t.remove(top.len);
+          ctl.top_slot = top.slot;
+          ctl.top_len = top.len;
+          ctl.top_cost = top.cost;
+          ctl.top_dual = dual;
+          const uint64_t am = top.len < ctl.am_len ? E.active_min[top.len] : 0;
+          const bool imbalanced = dual && (m.nsome[0] < am || m.nsome[1] < am);
+          if (top.len >= ctl.am_len) ctl.status = WC_E_INVARIANT_CODE;
+          if (top.cost > ctl.max_err || top.len < ctl.trk_thr[dual] || t.at_capacity(top.len) || imbalanced) {
+            ctl.cnt[S_IGNORED]++;
+            E.L.freestack[ctl.nfree++] = top.slot;
+            ctl.action = 1;
+          } else {
+            ctl.farthest[dual] = max(ctl.farthest[dual], (uint64_t)top.len);
+            ctl.last_constraint[dual]++;
+            if (!t.process(top.len)) ctl.status = 4;
+            ctl.cnt[S_EXPLORED]++;
+            ctl.action = 0;
+          }
+          if (A.trace && prob == 0) {
+            uint32_t k = A.trace[0];
+            if (k < A.trace_cap) {
+              uint32_t* rec = A.trace + 4 + 4 * k;
+              rec[0] = (uint32_t)top.cost;
+              rec[1] = top.len;
+              rec[2] = dual | (ctl.action << 1) | (m.nsome[0] << 8) | (m.nsome[1] << 20);
+              rec[3] = (uint32_t)am;
+              A.trace[0] = k + 1;
+            }
+          }
+        }
+        ctl.n_end[0] = ctl.n_end[1] = 0;
+        ctl.n_either = 0;
+        ctl.ovf = 0;
+      }
+      __syncthreads();
+      if (ctl.action == 2) break;
+      if (ctl.action == 1) continue;
+      if (ctl.status != ST_OK) break;
+
+      const uint32_t top = ctl.top_slot;
+      const uint32_t tlen = ctl.top_len;
+      const bool tdual = ctl.top_dual != 0;
+      const SlotMeta tm = E.L.meta[top];
+      const uint32_t tlens[2] = {tm.len[0], tm.len[1]};
+
+      analyze_side(E, ctl, top, 0, tlens[0], R0);
+      if (tdual) analyze_side(E, ctl, top, 1, tlens[1], R1);
+      __syncthreads();
+      // reached_all_end (dual_consensus.rs:1174-1195): per read, either side at its end
+      for (uint32_t r = tid; r < E.n; r += kBlock) {
+        const bool v = (R0[r].e != kInactive && R0[r].end) || (tdual && R1[r].e != kInactive && R1[r].end);
+        if (v) atomicAdd(&ctl.n_either, 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        ctl.reached = early ? (ctl.n_either == E.n) : (ctl.n_either > 0);
+        // reached_consensus_end (dual_consensus.rs:1203-1233); inactive counts as require_all
+        ctl.fin[0] = early ? (ctl.n_end[0] == tm.nsome[0]) : (ctl.n_end[0] > 0);
+        ctl.fin[1] = !tdual ? 0u : (early ? (ctl.n_end[1] == tm.nsome[1]) : (ctl.n_end[1] > 0));
+        if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
+      }
+      __syncthreads();
+      if (ctl.status != ST_OK) break;
+
+      // ---- finalize a clone (dual_consensus.rs:438-492) ----
+      if (ctl.reached) {
+        WaveCounters cnt = {0, 0, 0, 0, 0};
+        finalize_side(E, ctl, top, 0, tlens[0], E.L.fe, cnt);
+        if (tdual) finalize_side(E, ctl, top, 1, tlens[1], E.L.fe + E.nmax, cnt);
+        flush_counters(ctl, cnt);
+        __syncthreads();
+        if (tid == 0) {
+          ctl.store_idx = -1;
+          if (ctl.ovf & 4u) {
+            ctl.status = ST_RETRY | ST_RETRY_WCAP;
+          } else {
+            uint64_t total = 0, c1 = 0;
+            bool uninit = false;
+            for (uint32_t r = 0; r < E.n; ++r) {
+              const uint32_t f1 = E.L.fe[r];
+              const uint32_t f2 = tdual ? E.L.fe[E.nmax + r] : kInactive;
+              int idx = -1;
+              uint64_t best = ~0ull;
+              if (f1 != kInactive) {
+                best = cost_of(f1, cfg.cost_mode);
+                idx = 0;
+              }
+              if (f2 != kInactive && cost_of(f2, cfg.cost_mode) < best) {
+                best = cost_of(f2, cfg.cost_mode);
+                idx = 1;
+              }
+              if (idx < 0) uninit = true;
+              else total += best;
+              c1 += (idx == 0);
+            }
+            if (uninit) {
+              ctl.status = 1;  // "Finalize called on DWFA that was never initialized."
+            } else {
+              const uint64_t c2 = E.n - c1;
+              const bool imbalanced = tdual && (c1 < full_min || c2 < full_min);
+              if (!imbalanced) {
+                if (total < ctl.max_err) {
+                  ctl.max_err = total;
+                  ctl.n_ret = 0;
+                }
+                if (total <= ctl.max_err && ctl.n_ret < cfg.max_return_size) {
+                  if (ctl.n_ret < A.rmax) ctl.store_idx = (int32_t)ctl.n_ret;
+                  ctl.n_ret++;
+                }
+              }
+            }
+          }
+        }
+        __syncthreads();
+        if (ctl.status != ST_OK) break;
+        if (ctl.store_idx >= 0) store_record(E, ctl, outp, top, tdual ? 2 : 1, tlens, tdual);
+      }
+
+      // ---- active_min_count growth (dual_consensus.rs:497-513) ----
+      if (tid == 0 && ctl.am_len == tlen + 1 && tlen + 1 < E.lcap + 2) {
+        const uint32_t nt = E.total_active[tlen];  // + activations at tlen (offset path)
+        E.total_active[tlen + 1] = nt;
+        E.active_min[tlen + 1] = (uint32_t)max(cfg.min_count, ceil_u64(cfg.min_af * (double)nt));
+        ctl.am_len++;
+      }
+
+      // ---- votes on both sides (waves 0 and 1 in parallel) ----
+      if (wave_id() < (tdual ? 2 : 1)) {
+        const uint32_t side = wave_id();
+        const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, E.n, weighted, tdual, cfg.wildcard);
+        if (!ok && lane == 0) atomicOr(&ctl.ovf, 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
+        double thr[2];
+        uint64_t mc[2];
+        for (uint32_t s = 0; s < (tdual ? 2u : 1u); ++s) {
+          double sum = -0.0, mx = 0.0;
+          bool have = false;
+          for (uint32_t k = 0; k < ctl.nkeys[s]; ++k) {
+            sum += ctl.vals[s][k];
+            if (!have || ctl.vals[s][k] >= mx) mx = ctl.vals[s][k];
+            have = true;
+          }
+          mc[s] = max(cfg.min_count, ceil_u64(cfg.min_af * sum));
+          if (!have) mx = (double)mc[s];
+          thr[s] = fmin((double)mc[s], mx);
+        }
+        uint32_t nc = 0;
+        bool overflow = false;
+        if (tdual) {
+          // dual_consensus.rs:554-650: options per side, None first
+          int16_t o[2][kKout + 1];
+          uint32_t no[2] = {0, 0};
+          const bool lock[2] = {(tm.flags & 2u) != 0, (tm.flags & 4u) != 0};
+          for (int s = 0; s < 2; ++s) {
+            if (ctl.fin[s] || ctl.nkeys[s] == 0 || lock[s]) o[s][no[s]++] = -1;
+            if (!lock[s])
+              for (uint32_t k = 0; k < ctl.nkeys[s]; ++k)
+                if (!(ctl.vals[s][k] < thr[s])) o[s][no[s]++] = ctl.keys[s][k];
+          }
+          for (uint32_t a = 0; a < no[0]; ++a)
+            for (uint32_t b = 0; b < no[1]; ++b) {
+              if (o[0][a] < 0 && o[1][b] < 0) continue;
+              if (nc == kMaxChild) {
+                overflow = true;
+                continue;
+              }
+              ctl.ch_s[nc][0] = o[0][a];
+              ctl.ch_s[nc][1] = o[1][b];
+              ctl.ch_kind[nc] = 0;
+              nc++;
+            }
+        } else {
+          // stay-single children (dual_consensus.rs:655-679)
+          for (uint32_t k = 0; k < ctl.nkeys[0]; ++k) {
+            if (ctl.vals[0][k] < thr[0]) continue;
+            ctl.ch_s[nc][0] = ctl.keys[0][k];
+            ctl.ch_s[nc][1] = -1;
+            ctl.ch_kind[nc] = 1;
+            nc++;
+          }
+          // split children from every pair of sorted candidates (:682-734)
+          double cv[kKout];
+          uint8_t cs[kKout];
+          uint32_t ns = 0, passing = 0;
+          for (uint32_t k = 0; k < ctl.nkeys[0]; ++k) {
+            if (cfg.wildcard >= 0 && ctl.keys[0][k] == (uint8_t)cfg.wildcard) continue;
+            if (ctl.vals[0][k] >= (double)mc[0]) passing++;
+            // insertion sort by (Reverse(count), symbol), stable
+            uint32_t p = ns;
+            while (p > 0 && (cv[p - 1] < ctl.vals[0][k] || (cv[p - 1] == ctl.vals[0][k] && cs[p - 1] > ctl.keys[0][k]))) {
+              cv[p] = cv[p - 1];
+              cs[p] = cs[p - 1];
+              --p;
+            }
+            cv[p] = ctl.vals[0][k];
+            cs[p] = ctl.keys[0][k];
+            ns++;
+          }
+          if (passing > 1)
+            for (uint32_t i = 0; i < ns; ++i)
+              for (uint32_t j = i + 1; j < ns; ++j) {
+                if (nc == kMaxChild) {
+                  overflow = true;
+                  continue;
+                }
+                ctl.ch_s[nc][0] = cs[i];
+                ctl.ch_s[nc][1] = cs[j];
+                ctl.ch_kind[nc] = 2;
+                nc++;
+              }
+        }
+        if (overflow) ctl.status = WC_E_LIMIT_CODE;
+        ctl.nchild = nc;
+      }
+      __syncthreads();
+      if (ctl.status != ST_OK) break;
+      const uint32_t nc = ctl.nchild;
+      if (nc == 0) {
+        if (tid == 0) E.L.freestack[ctl.nfree++] = top;
+        __syncthreads();
+        continue;
+      }
+      if (tlens[0] + 1 > E.lcap || tlens[1] + 1 > E.lcap) {
+        if (tid == 0) ctl.status = ST_RETRY | ST_RETRY_LCAP;
+        __syncthreads();
+        break;
+      }
+
+      // ---- build every child: clones first, the last child in place ----
+      for (uint32_t c = 0; c < nc; ++c) {
+        if (tid == 0) {
+          uint32_t slot = top;
+          if (c + 1 < nc) {
+            if (ctl.nfree == 0) ctl.status = ST_RETRY | ST_RETRY_PCAP;
+            else slot = E.L.freestack[--ctl.nfree];
+          }
+          ctl.cur_slot = slot;
+          ctl.cost_acc = 0;
+          ctl.some_acc[0] = ctl.some_acc[1] = 0;
+          ctl.ovf = 0;
+        }
+        __syncthreads();
+        if (ctl.status != ST_OK) break;
+        const uint32_t slot = ctl.cur_slot;
+        const uint8_t kind = ctl.ch_kind[c];
+        const int s0 = ctl.ch_s[c][0], s1 = ctl.ch_s[c][1];
+        if (slot != top) copy_node(E, top, slot, tdual ? 2 : 1, tlens);
+        __syncthreads();
+        if (kind == 2) {
+          // activate_dual (dual_consensus.rs:957-976): side 2 := side 1
+          SideView a = E.sv(slot, 0), b = E.sv(slot, 1);
+          for (uint32_t i = tid; i < tlens[0]; i += kBlock) b.con[i] = a.con[i];
+          for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
+            const uint32_t e = a.e[r];
+            if (lane == 0) {
+              b.e[r] = e;
+              b.off[r] = a.off[r];
+            }
+            if (e == kInactive) continue;
+            const uint32_t W = 2 * e + 1;
+            for (uint32_t i = lane; i < W; i += 64) b.wf[(uint64_t)r * E.wcap + i] = a.wf[(uint64_t)r * E.wcap + i];
+          }
+        }
+        uint32_t nl[2];
+        if (tid == 0) {
+          SlotMeta m = tm;
+          if (kind == 2) {
+            m.flags |= 1u;
+            m.len[1] = m.len[0];
+            m.nsome[1] = m.nsome[0];
+          }
+          for (int s = 0; s < 2; ++s) {
+            const int sym = s == 0 ? s0 : s1;
+            if (sym >= 0) {
+              E.sv(slot, s).con[m.len[s]] = (uint8_t)sym;
+              m.len[s]++;
+            } else if (kind == 0) {
+              m.flags |= (s == 0 ? 2u : 4u);  // lock_sequence
+            }
+          }
+          E.L.meta[slot] = m;
+        }
+        __syncthreads();
+        nl[0] = E.L.meta[slot].len[0];
+        nl[1] = E.L.meta[slot].len[1];
+        WaveCounters cnt = {0, 0, 0, 0, 0};
+        push_sides(E, ctl, slot, s0, s1, nl[0], nl[1], false, cnt);
+        flush_counters(ctl, cnt);
+        __syncthreads();
+        // prune (dual_consensus.rs:1030-1045) + priority (:1092-1168)
+        const bool cdual = (E.L.meta[slot].flags & 1u) != 0;
+        {
+          SideView a = E.sv(slot, 0), b = E.sv(slot, 1);
+          uint64_t cost = 0;
+          uint32_t n0 = 0, n1 = 0;
+          for (uint32_t r = tid; r < E.n; r += kBlock) {
+            uint32_t e1 = a.e[r], e2 = cdual ? b.e[r] : kInactive;
+            if (cdual && e1 != kInactive && e2 != kInactive) {
+              if ((uint64_t)e1 + cfg.dual_max_ed_delta < (uint64_t)e2) {
+                b.e[r] = kInactive;
+                e2 = kInactive;
+              } else if ((uint64_t)e2 + cfg.dual_max_ed_delta < (uint64_t)e1) {
+                a.e[r] = kInactive;
+                e1 = kInactive;
+              }
+            }
+            uint64_t best = ~0ull;
+            if (e1 != kInactive) best = cost_of(e1, cfg.cost_mode);
+            if (e2 != kInactive && cost_of(e2, cfg.cost_mode) < best) best = cost_of(e2, cfg.cost_mode);
+            if (best != ~0ull) cost += best;
+            n0 += e1 != kInactive;
+            n1 += e2 != kInactive;
+          }
+          if (cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);
+          if (n0) atomicAdd(&ctl.some_acc[0], n0);
+          if (n1) atomicAdd(&ctl.some_acc[1], n1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
+          SlotMeta& m = E.L.meta[slot];
+          m.nsome[0] = ctl.some_acc[0];
+          m.nsome[1] = ctl.some_acc[1];
+          ctl.ch_cost[c] = ctl.cost_acc;
+          ctl.ch_slot[c] = slot;
+          ctl.ch_len[c] = max(m.len[0], m.len[1]);
+        }
+        __syncthreads();
+        if (ctl.status != ST_OK) break;
+      }
+      if (ctl.status != ST_OK) break;
+      if (tid == 0) {
+        for (uint32_t c = 0; c < nc; ++c) {
+          const uint32_t k = (E.L.meta[ctl.ch_slot[c]].flags & 1u) ? 1 : 0;
+          E.tracker(ctl, k).insert(ctl.ch_len[c]);
+          heap_push(E.L.heap, ctl.heap_n, HeapEntry{ctl.ch_cost[c], ctl.ch_len[c], ctl.ch_slot[c]});
+        }
+      }
+      __syncthreads();
+    }
+
+    __syncthreads();
+    if (tid == 0) {
+      ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
+      A.status[prob] = ctl.status;
+      for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)prob * S_NSTAT + s] = ctl.cnt[s];
+    }
+    __syncthreads();
+  }
+}
+
+// =====================================================================
+// standalone DWFALite jobs (dynamic_wfa.rs:48-265): one wave per job
+// =====================================================================
+__global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
+  DwfaDevJob& j = jobs[blockIdx.x];
+  const int lane = lane_id();
+  uint32_t e = j.e;
+  WaveCounters cnt = {0, 0, 0, 0, 0};
+  uint32_t status = 0;
+  if (j.op == 0) {
+    uint32_t mo = 0, mb = 0;
+    if (!wave_update_general(j.wf, e, j.offset, j.baseline, j.blen, j.other, j.olen, j.wildcard, j.early != 0, j.wf_cap,
+                             cnt, mo, mb))
+      status = WC_E_LIMIT_CODE;
+    else if (!(mo == j.olen || (j.early && mb == j.blen)))
+      status = WC_E_INVARIANT_CODE;  // dynamic_wfa.rs:94-97 assert
+  } else if (j.op == 1) {
+    uint32_t W = 2 * e + 1, mb = 0;
+    for (uint32_t i = lane; i < W; i += 64) mb = max(mb, j.wf[i] + e - i);
+    mb = wave_max_u32(mb);
+    uint32_t cmp = 0;
+    while (mb < j.blen) {
+      if (W + 2 > j.wf_cap) {
+        status = WC_E_LIMIT_CODE;
+        break;
+      }
+      wave_grow(j.wf, W);
+      W += 2;
+      e += 1;
+      uint32_t mo;
+      wave_extend_all(j.wf, W, e, j.offset, j.baseline, j.blen, j.other, j.olen, j.wildcard, mo, mb, cmp);
+    }
+  } else {
+    __shared__ RInfo ri;
+    if (!wave_analyze_read(j.wf, e, j.offset, j.baseline, j.blen, j.olen, &ri)) status = WC_E_LIMIT_CODE;
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0 && status == 0) {
+      j.n_cand = ri.n;
+      for (uint32_t k = 0; k < ri.n; ++k) {
+        j.cand_syms[k] = ri.sym[k];
+        j.cand_counts[k] = ri.occ[k];
+      }
+    }
+  }
+  if (lane == 0) {
+    j.e = e;
+    j.status = status;
+  }
+}
+
 void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(single_engine_kernel, dim3(grid), dim3(kBlock), lds, s, a);
 }
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
-  (void)a; (void)grid; (void)lds; (void)s;
+  hipLaunchKernelGGL(dual_engine_kernel, dim3(grid), dim3(kBlock), lds, s, a);
 }
 int engine_blocks_per_cu(uint32_t sides, size_t lds) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kBlock, lds) != hipSuccess) nb = 1;
-  return nb;
+  hipError_t e = sides == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kBlock, lds)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kBlock, lds);
+  return e == hipSuccess && nb > 0 ? nb : 1;
 }
+void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s) {
+  hipLaunchKernelGGL(dwfa_jobs_kernel, dim3(n), dim3(64), 0, s, jobs);
+}
+
 }  // namespace wc

@@ -214,8 +214,8 @@ __device__ inline bool wave_push_read(uint32_t* wf, uint32_t& e, uint32_t off, c
 // dynamic_wfa.rs:75-99 with a full extend first.
 __device__ inline bool wave_update_general(uint32_t* wf, uint32_t& e, uint32_t off, const uint8_t* rd, uint32_t blen,
                                            const uint8_t* con, uint32_t olen, int wc, bool early, uint32_t wcap,
-                                           WaveCounters& cnt) {
-  uint32_t W = 2 * e + 1, mo, mb, cmp = 0;
+                                           WaveCounters& cnt, uint32_t& mo, uint32_t& mb) {
+  uint32_t W = 2 * e + 1, cmp = 0;
   wave_extend_all(wf, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
   mo += off;
   while (mo < olen && !(early && mb == blen)) {

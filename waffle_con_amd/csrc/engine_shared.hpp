@@ -85,6 +85,9 @@ struct EngineArgs {
   uint32_t* status;      // per problem
   uint64_t* stats;       // per problem x S_NSTAT
   uint32_t* work_counter;
+  uint32_t* trace;       // debug: per-pop records of problem 0 (nullptr = off)
+  uint32_t trace_cap;    // records (4 u32 each); trace[0] = count
+  uint32_t _pad2;
 };
 
 // ---- byte layouts (host and device compute them identically) ----
@@ -142,4 +145,19 @@ __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uin
   return align16(t);
 }
 
+}  // namespace wc
+
+namespace wc {
+// one standalone DWFALite job (wc_dwfa_batch); device pointers
+struct DwfaDevJob {
+  const uint8_t* baseline;
+  const uint8_t* other;
+  uint32_t* wf;
+  uint32_t blen, olen, offset, wf_cap;
+  int32_t wildcard;
+  uint32_t early, op, e;
+  uint32_t status, n_cand;
+  uint8_t cand_syms[16];
+  uint32_t cand_counts[16];
+};
 }  // namespace wc

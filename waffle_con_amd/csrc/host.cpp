@@ -1,18 +1,21 @@
 // Host orchestration and C ABI of the waffle_con MI355X library.
 //
-// A batch call packs every problem's reads into one HBM arena, launches the
-// device-resident engine once for the whole batch (one workgroup per problem,
-// persistent grid pulling problems from an atomic counter, longest problems
-// first), and turns the device result records into the reference's result
-// types (Consensus, DualConsensus, PriorityConsensus). Problems that outgrow
-// a device capacity (wavefront length, node pool, consensus length) are
-// re-run with doubled capacities; no work is ever done on the CPU instead.
+// A batch uploads every problem's reads once into an HBM arena (wc_batch);
+// each run launches the device-resident engine once for the whole batch (one
+// workgroup per problem, persistent grid pulling problems from an atomic
+// counter, longest problems first) and turns the device result records into
+// the reference's result types (Consensus, DualConsensus, PriorityConsensus).
+// Problems that outgrow a device capacity (wavefront length, node pool,
+// consensus length) are re-run on the device with doubled capacities; no
+// consensus work is ever done on the CPU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <array>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -27,23 +30,25 @@ namespace wc {
 void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 int engine_blocks_per_cu(uint32_t sides, size_t lds);
+void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s);
 }  // namespace wc
 
 using namespace wc;
 
 // ------------------------------------------------------------------------
-// context
+// context and device buffers
 // ------------------------------------------------------------------------
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
   bool ensure(size_t bytes) {
     if (bytes <= cap) return true;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = std::max<size_t>(bytes, 1 << 20);
-    if (hipMalloc(&p, want) != hipSuccess) return false;
+    release();
+    size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+    if (hipMalloc(&p, want) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
     cap = want;
     return true;
   }
@@ -60,11 +65,11 @@ struct wc_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string err;
-  DevBuf reads, roff, rlen, ract, probs, ws, out, status, stats, counter;
+  DevBuf ract, probs, ws, out, status, stats, counter, jobs;
 };
 
 namespace {
-const char* err_msg(int code) {
+std::string err_msg(int code) {
   switch (code) {
     case WC_E_FINALIZE_UNINIT: return "Finalize called on DWFA that was never initialized.";
     case WC_E_NO_START: return "Must have at least one initial offset of None to see the consensus.";
@@ -87,9 +92,9 @@ inline int set_err(wc_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
-#define HIPCHK(call)                                                                             \
-  do {                                                                                           \
-    hipError_t _e = (call);                                                                      \
+#define HIPCHK(call)                                                                                       \
+  do {                                                                                                     \
+    hipError_t _e = (call);                                                                                \
     if (_e != hipSuccess) return set_err(ctx, WC_E_HIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
@@ -113,6 +118,30 @@ DevConfig to_dev(const wc_config& c) {
 
 inline uint64_t cost_of_h(uint32_t e, int mode) { return mode == 0 ? (uint64_t)e : (uint64_t)e * (uint64_t)e; }
 }  // namespace
+
+// ------------------------------------------------------------------------
+// resident batch: reads of many problems in one HBM arena
+// ------------------------------------------------------------------------
+struct BatchProblem {
+  uint32_t read_begin = 0;
+  uint32_t n_reads = 0;
+  uint32_t max_len = 0;
+  uint64_t work = 0;             // sum of read lengths (scheduling order)
+  std::vector<int64_t> offsets;  // raw add_sequence_offset values (-1 = None)
+};
+
+struct wc_batch {
+  wc_ctx* ctx = nullptr;
+  std::vector<BatchProblem> probs;
+  std::vector<uint32_t> rlen_h;
+  DevBuf reads, roff, rlen;
+  uint64_t bytes = 0;
+  ~wc_batch() {
+    reads.release();
+    roff.release();
+    rlen.release();
+  }
+};
 
 // ------------------------------------------------------------------------
 // results
@@ -142,28 +171,60 @@ struct wc_results {
   wc_stats stats;
 };
 
-// ------------------------------------------------------------------------
-// engine batch runner (shared by single and dual)
-// ------------------------------------------------------------------------
-namespace {
-struct PackedProblem {
-  std::vector<const uint8_t*> reads;
-  std::vector<uint64_t> lens;
-  std::vector<int64_t> activate;  // activation length or -1
-  uint32_t n_active = 0;
+struct RawRecord {
+  uint32_t len[2] = {0, 0};
+  bool dual = false;
+  std::vector<uint8_t> con[2];
+  std::vector<uint32_t> fe[2];
 };
 
-// auto_shift_offsets + activation points (consensus.rs:151-202)
-int prepare_problem(const wc_config& cfg, const wc_problem& p, PackedProblem& out, std::string& err) {
-  if (p.n_reads == 0) {
+namespace {
+int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* b) {
+  b->ctx = ctx;
+  b->probs.resize(n);
+  std::vector<uint64_t> roff;
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    for (uint32_t r = 0; r < problems[i].n_reads; ++r) total += (problems[i].lens[r] + 15) & ~15ull;
+  std::vector<uint8_t> h(std::max<uint64_t>(total, 16));
+  uint64_t pos = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const wc_problem& p = problems[i];
+    BatchProblem& q = b->probs[i];
+    q.read_begin = (uint32_t)roff.size();
+    q.n_reads = p.n_reads;
+    q.offsets.assign(p.n_reads, -1);
+    for (uint32_t r = 0; r < p.n_reads; ++r) {
+      if (p.offsets) q.offsets[r] = p.offsets[r] < 0 ? -1 : p.offsets[r];
+      roff.push_back(pos);
+      b->rlen_h.push_back((uint32_t)p.lens[r]);
+      if (p.lens[r]) memcpy(h.data() + pos, p.reads[r], p.lens[r]);
+      pos += (p.lens[r] + 15) & ~15ull;
+      q.max_len = std::max<uint32_t>(q.max_len, (uint32_t)p.lens[r]);
+      q.work += p.lens[r];
+    }
+  }
+  b->bytes = h.size();
+  if (!b->reads.ensure(h.size()) || !b->roff.ensure(std::max<size_t>(roff.size(), 1) * 8) ||
+      !b->rlen.ensure(std::max<size_t>(b->rlen_h.size(), 1) * 4))
+    return set_err(ctx, WC_E_HIP, "device allocation failed (reads)");
+  HIPCHK(hipMemcpyAsync(b->reads.p, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream));
+  if (!roff.empty()) HIPCHK(hipMemcpyAsync(b->roff.p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  if (!b->rlen_h.empty())
+    HIPCHK(hipMemcpyAsync(b->rlen.p, b->rlen_h.data(), b->rlen_h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return WC_OK;
+}
+
+// auto_shift_offsets + activation points (consensus.rs:151-202); returns a
+// per-read activation length (-1 = active at the root) or an error code.
+int activation_plan(const wc_config& cfg, const BatchProblem& q, std::vector<int64_t>& act, uint32_t& n_active,
+                    std::string& err) {
+  if (q.n_reads == 0) {
     err = "No sequences provided";
     return WC_E_BAD_INPUT;
   }
-  out.reads.assign(p.reads, p.reads + p.n_reads);
-  out.lens.assign(p.lens, p.lens + p.n_reads);
-  std::vector<int64_t> offs(p.n_reads, -1);
-  if (p.offsets)
-    for (uint32_t i = 0; i < p.n_reads; ++i) offs[i] = p.offsets[i];
+  std::vector<int64_t> offs = q.offsets;
   if (cfg.auto_shift_offsets) {
     int64_t mn = INT64_MAX;
     bool start = false;
@@ -174,18 +235,18 @@ int prepare_problem(const wc_config& cfg, const wc_problem& p, PackedProblem& ou
     if (!start)
       for (auto& o : offs) o = (o == mn) ? -1 : o - mn;
   }
-  out.activate.assign(p.n_reads, -1);
-  out.n_active = 0;
-  for (uint32_t i = 0; i < p.n_reads; ++i) {
-    if (offs[i] >= 0) out.activate[i] = offs[i] + (int64_t)cfg.offset_compare_length;
-    else out.n_active++;
+  act.assign(q.n_reads, -1);
+  n_active = 0;
+  for (uint32_t i = 0; i < q.n_reads; ++i) {
+    if (offs[i] >= 0) act[i] = offs[i] + (int64_t)cfg.offset_compare_length;
+    else n_active++;
   }
-  if (out.n_active == 0) {
+  if (n_active == 0) {
     err = err_msg(WC_E_NO_START);
     return WC_E_NO_START;
   }
-  for (uint32_t i = 0; i < p.n_reads; ++i) {
-    if (out.activate[i] >= 0) {
+  for (auto a : act) {
+    if (a >= 0) {
       err = "activation offsets (add_sequence_offset) are not supported by this build's device engine yet";
       return WC_E_LIMIT;
     }
@@ -193,82 +254,91 @@ int prepare_problem(const wc_config& cfg, const wc_problem& p, PackedProblem& ou
   return WC_OK;
 }
 
-struct RawRecord {
-  uint32_t len[2];
-  bool dual;
-  std::vector<uint8_t> con[2];
-  std::vector<uint32_t> fe[2];
+struct EngineRun {
+  std::vector<std::vector<RawRecord>> recs;
+  std::vector<int> status;
+  std::vector<std::string> error;
+  std::vector<std::array<uint64_t, S_NSTAT>> stats;
+  double kernel_ms = 0;
+  uint64_t launches = 0;
 };
 
-// Runs problems `ids` of `pp` through the engine; fills raw records/status/stats.
-int run_engine(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vector<PackedProblem>& pp,
-               std::vector<uint32_t> ids, std::vector<std::vector<RawRecord>>& recs, std::vector<int>& status,
-               std::vector<std::array<uint64_t, S_NSTAT>>& stats, double& kernel_ms, uint64_t& launches) {
-  // capacities
+// Runs the problems `ids` (indices into b->probs) through the engine.
+int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, std::vector<uint32_t> ids,
+               EngineRun& R) {
+  const uint32_t NP = (uint32_t)b->probs.size();
+  R.recs.assign(NP, {});
+  R.status.assign(NP, WC_OK);
+  R.error.assign(NP, "");
+  R.stats.assign(NP, {});
+  for (auto& s : R.stats) s.fill(0);
+
+  // per-read activation lengths for the whole batch (indexed by global read)
+  std::vector<int64_t> ract(std::max<size_t>(b->rlen_h.size(), 1), -1);
+  std::vector<uint32_t> n_active(NP, 0);
+  std::vector<uint32_t> runnable;
+  for (uint32_t id : ids) {
+    std::vector<int64_t> act;
+    int rc = activation_plan(cfg, b->probs[id], act, n_active[id], R.error[id]);
+    if (rc != WC_OK) {
+      R.status[id] = rc;
+      continue;
+    }
+    std::copy(act.begin(), act.end(), ract.begin() + b->probs[id].read_begin);
+    runnable.push_back(id);
+  }
+  ids = runnable;
+  if (ids.empty()) return WC_OK;
+  if (!ctx->ract.ensure(ract.size() * 8)) return set_err(ctx, WC_E_HIP, "device allocation failed");
+  HIPCHK(hipMemcpyAsync(ctx->ract.p, ract.data(), ract.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+
   uint32_t nmax = 1, maxlen = 1;
   for (uint32_t id : ids) {
-    nmax = std::max<uint32_t>(nmax, (uint32_t)pp[id].reads.size());
-    for (auto l : pp[id].lens) maxlen = std::max<uint32_t>(maxlen, (uint32_t)l);
+    nmax = std::max<uint32_t>(nmax, b->probs[id].n_reads);
+    maxlen = std::max<uint32_t>(maxlen, b->probs[id].max_len);
   }
   uint32_t ecap = std::max<uint32_t>(31, maxlen / 64);
   uint32_t wcap = ((2 * ecap + 1 + 63) / 64) * 64;
   uint32_t lcap = ((maxlen + maxlen / 8 + 64 + 15) / 16) * 16;
-  uint32_t pcap = sides == 1 ? 16 : 64;
+  // node pool: as many slots as ~16 MiB of workspace per workgroup allows
+  // (16..256), bounded by the LDS the heap/metadata need
+  uint32_t pcap = 16;
+  {
+    const uint64_t sb = slot_bytes(sides, nmax, wcap, lcap);
+    while (pcap < 256 && (uint64_t)(pcap * 2) * sb <= (16ull << 20) && lds_bytes(sides, pcap * 2, nmax) <= 40 * 1024)
+      pcap *= 2;
+  }
   const uint32_t rmax = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cfg.max_return_size, 1), 256);
 
   for (int attempt = 0; attempt < 8 && !ids.empty(); ++attempt) {
-    // longest problems first (cost ~ n_reads * len)
-    std::sort(ids.begin(), ids.end(), [&](uint32_t a, uint32_t b) {
-      uint64_t ca = 0, cb = 0;
-      for (auto l : pp[a].lens) ca += l;
-      for (auto l : pp[b].lens) cb += l;
-      return ca > cb;
-    });
+    std::stable_sort(ids.begin(), ids.end(),
+                     [&](uint32_t x, uint32_t y) { return b->probs[x].work > b->probs[y].work; });
     const uint32_t P = (uint32_t)ids.size();
-    // pack reads
     std::vector<DevProblem> dp(P);
-    std::vector<uint64_t> roff;
-    std::vector<uint32_t> rlen;
-    std::vector<int64_t> ract;
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < P; ++i)
-      for (auto l : pp[ids[i]].lens) total += (l + 15) & ~15ull;
-    std::vector<uint8_t> hreads(std::max<uint64_t>(total, 16));
-    uint64_t pos = 0;
     for (uint32_t i = 0; i < P; ++i) {
-      const PackedProblem& q = pp[ids[i]];
-      dp[i].read_begin = (uint32_t)roff.size();
-      dp[i].n_reads = (uint32_t)q.reads.size();
-      dp[i].n_active = q.n_active;
-      uint32_t ml = 0;
-      for (size_t r = 0; r < q.reads.size(); ++r) {
-        roff.push_back(pos);
-        rlen.push_back((uint32_t)q.lens[r]);
-        ract.push_back(q.activate[r]);
-        if (q.lens[r]) memcpy(hreads.data() + pos, q.reads[r], q.lens[r]);
-        pos += (q.lens[r] + 15) & ~15ull;
-        ml = std::max<uint32_t>(ml, (uint32_t)q.lens[r]);
-      }
-      dp[i].max_read_len = ml;
+      const BatchProblem& q = b->probs[ids[i]];
+      dp[i].read_begin = q.read_begin;
+      dp[i].n_reads = q.n_reads;
+      dp[i].max_read_len = q.max_len;
+      dp[i].n_active = n_active[ids[i]];
     }
     size_t lds = (size_t)lds_bytes(sides, pcap, nmax);
-    if (lds > 160 * 1024 - 4096) return set_err(ctx, WC_E_LIMIT, "problem needs more LDS than a CU has");
+    if (lds > 60 * 1024) {
+      for (uint32_t id : ids) {
+        R.status[id] = WC_E_LIMIT;
+        R.error[id] = "problem needs more LDS than the engine allows (reads x node pool)";
+      }
+      return WC_OK;
+    }
     int per_cu = engine_blocks_per_cu(sides, lds);
     uint32_t grid = std::min<uint32_t>(P, (uint32_t)std::max(1, per_cu) * (uint32_t)ctx->n_cu);
     uint64_t wsb = ws_bytes(sides, pcap, nmax, wcap, lcap);
     uint64_t ob = out_bytes(sides, rmax, nmax, lcap);
-    if (!ctx->reads.ensure(hreads.size()) || !ctx->roff.ensure(roff.size() * 8) || !ctx->rlen.ensure(rlen.size() * 4) ||
-        !ctx->ract.ensure(ract.size() * 8) || !ctx->probs.ensure(P * sizeof(DevProblem)) ||
-        !ctx->ws.ensure(wsb * grid) || !ctx->out.ensure(ob * P) || !ctx->status.ensure(P * 4) ||
-        !ctx->stats.ensure((size_t)P * S_NSTAT * 8) || !ctx->counter.ensure(4))
-      return set_err(ctx, WC_E_HIP, "device allocation failed");
-    HIPCHK(hipMemcpyAsync(ctx->reads.p, hreads.data(), hreads.size(), hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->roff.p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->rlen.p, rlen.data(), rlen.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->ract.p, ract.data(), ract.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (!ctx->probs.ensure(P * sizeof(DevProblem)) || !ctx->ws.ensure(wsb * grid) || !ctx->out.ensure(ob * P) ||
+        !ctx->status.ensure(P * 4) || !ctx->stats.ensure((size_t)P * S_NSTAT * 8) || !ctx->counter.ensure(4))
+      return set_err(ctx, WC_E_HIP, "device allocation failed (workspace)");
     HIPCHK(hipMemcpyAsync(ctx->probs.p, dp.data(), P * sizeof(DevProblem), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->counter.p, 0, 4, ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->out.p, 0, 16, ctx->stream));
 
     EngineArgs a;
     memset(&a, 0, sizeof(a));
@@ -276,9 +346,9 @@ int run_engine(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vec
     a.problems = (const DevProblem*)ctx->probs.p;
     a.n_problems = P;
     a.sides = sides;
-    a.rbytes = (const uint8_t*)ctx->reads.p;
-    a.roff = (const uint64_t*)ctx->roff.p;
-    a.rlen = (const uint32_t*)ctx->rlen.p;
+    a.rbytes = (const uint8_t*)b->reads.p;
+    a.roff = (const uint64_t*)b->roff.p;
+    a.rlen = (const uint32_t*)b->rlen.p;
     a.ractivate = (const int64_t*)ctx->ract.p;
     a.ws = (uint8_t*)ctx->ws.p;
     a.ws_stride = wsb;
@@ -292,6 +362,15 @@ int run_engine(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vec
     a.status = (uint32_t*)ctx->status.p;
     a.stats = (uint64_t*)ctx->stats.p;
     a.work_counter = (uint32_t*)ctx->counter.p;
+    // debug trace of problem 0's pops (WC_TRACE=<file>); off by default
+    const char* trace_path = getenv("WC_TRACE");
+    DevBuf tbuf;
+    const uint32_t tcap = 1u << 20;
+    if (trace_path && tbuf.ensure((size_t)(4 + 4 * tcap) * 4)) {
+      a.trace = (uint32_t*)tbuf.p;
+      a.trace_cap = tcap;
+      HIPCHK(hipMemsetAsync(tbuf.p, 0, 16, ctx->stream));
+    }
 
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (sides == 1) launch_single_engine(a, grid, lds, ctx->stream);
@@ -301,73 +380,83 @@ int run_engine(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vec
     HIPCHK(hipStreamSynchronize(ctx->stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-    kernel_ms += ms;
-    launches++;
+    R.kernel_ms += ms;
+    R.launches++;
+    if (a.trace) {
+      uint32_t cnt = 0;
+      HIPCHK(hipMemcpy(&cnt, tbuf.p, 4, hipMemcpyDeviceToHost));
+      std::vector<uint32_t> t((size_t)4 * std::min(cnt, tcap));
+      if (!t.empty()) HIPCHK(hipMemcpy(t.data(), (uint32_t*)tbuf.p + 4, t.size() * 4, hipMemcpyDeviceToHost));
+      if (FILE* f = fopen(trace_path, "w")) {
+        for (size_t k = 0; k < t.size(); k += 4) fprintf(f, "%u %u %u %u\n", t[k], t[k + 1], t[k + 2], t[k + 3]);
+        fclose(f);
+      }
+      tbuf.release();
+    }
 
+    // read back: status, stats, and the first record of every problem in one
+    // strided copy; further records only for problems that returned ties
     std::vector<uint32_t> hst(P);
     std::vector<uint64_t> hstats((size_t)P * S_NSTAT);
-    std::vector<uint8_t> hout(ob * P);
+    const uint64_t rb = result_bytes(sides, nmax, lcap);
+    const uint64_t first = 16 + rb;
+    std::vector<uint8_t> hout((size_t)first * P);
     HIPCHK(hipMemcpy(hst.data(), ctx->status.p, P * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(hstats.data(), ctx->stats.p, hstats.size() * 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(hout.data(), ctx->out.p, hout.size(), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy2D(hout.data(), first, ctx->out.p, ob, first, P, hipMemcpyDeviceToHost));
 
     std::vector<uint32_t> retry;
     uint32_t rflags = 0;
-    const uint64_t rb = result_bytes(sides, nmax, lcap);
+    std::vector<uint8_t> extra;
     for (uint32_t i = 0; i < P; ++i) {
       const uint32_t id = ids[i];
       const uint32_t st = hst[i];
-      for (int s = 0; s < S_NSTAT; ++s) stats[id][s] = hstats[(size_t)i * S_NSTAT + s];
+      // counters of the attempt that completed (a capacity retry restarts the search)
+      for (int s = 0; s < S_NSTAT; ++s) R.stats[id][s] = hstats[(size_t)i * S_NSTAT + s];
       if (st & ST_RETRY) {
         retry.push_back(id);
         rflags |= st;
         continue;
       }
-      status[id] = (int)st;
-      if (st != ST_OK) continue;
-      const uint8_t* base = hout.data() + (size_t)i * ob;
-      uint32_t nres = ((const uint32_t*)base)[0];
-      const uint32_t n = (uint32_t)pp[id].reads.size();
-      recs[id].clear();
+      R.status[id] = (int)st;
+      if (st != ST_OK) {
+        R.error[id] = err_msg((int)st);
+        continue;
+      }
+      const uint8_t* base = hout.data() + (size_t)i * first;
+      const uint32_t nres = ((const uint32_t*)base)[0];
+      if (nres > 1) {
+        extra.resize((size_t)nres * rb);
+        HIPCHK(hipMemcpy(extra.data(), (uint8_t*)ctx->out.p + (size_t)i * ob + 16, extra.size(),
+                         hipMemcpyDeviceToHost));
+      }
+      const uint32_t n = b->probs[id].n_reads;
       for (uint32_t k = 0; k < nres; ++k) {
-        const uint8_t* rec = base + 16 + k * rb;
+        const uint8_t* rec = k == 0 ? base + 16 : extra.data() + (size_t)k * rb;
         const uint32_t* h = (const uint32_t*)rec;
-        RawRecord R;
-        R.len[0] = h[0];
-        R.len[1] = h[1];
-        R.dual = h[2] != 0;
+        RawRecord rr;
+        rr.len[0] = h[0];
+        rr.len[1] = h[1];
+        rr.dual = h[2] != 0;
         for (uint32_t s = 0; s < sides; ++s) {
           const uint8_t* con = rec + 16 + s * align16(lcap);
-          R.con[s].assign(con, con + R.len[s]);
+          rr.con[s].assign(con, con + rr.len[s]);
           const uint32_t* fe = (const uint32_t*)(rec + 16 + sides * align16(lcap) + s * align16((uint64_t)nmax * 4));
-          R.fe[s].assign(fe, fe + n);
+          rr.fe[s].assign(fe, fe + n);
         }
-        recs[id].push_back(std::move(R));
+        R.recs[id].push_back(std::move(rr));
       }
     }
     ids = retry;
     if (rflags & ST_RETRY_WCAP) wcap = wcap * 2;
-    if (rflags & (ST_RETRY_PCAP | ST_RETRY_HEAP)) pcap = pcap * 4;
+    if (rflags & (ST_RETRY_PCAP | ST_RETRY_HEAP)) pcap = pcap * 2;
     if (rflags & ST_RETRY_LCAP) lcap = lcap * 2;
   }
-  for (uint32_t id : ids) status[id] = WC_E_LIMIT;
-  return WC_OK;
-}
-
-std::vector<PackedProblem> prepare_all(const wc_config& cfg, uint32_t n, const wc_problem* problems,
-                                       std::vector<ProbRes>& res, std::vector<uint32_t>& runnable) {
-  std::vector<PackedProblem> pp(n);
-  for (uint32_t i = 0; i < n; ++i) {
-    std::string err;
-    int rc = prepare_problem(cfg, problems[i], pp[i], err);
-    if (rc != WC_OK) {
-      res[i].status = rc;
-      res[i].error = err;
-    } else {
-      runnable.push_back(i);
-    }
+  for (uint32_t id : ids) {
+    R.status[id] = WC_E_LIMIT;
+    R.error[id] = err_msg(WC_E_LIMIT);
   }
-  return pp;
+  return WC_OK;
 }
 
 void fill_stats(wc_results* R, double kernel_ms, uint64_t launches, double wall_ms) {
@@ -387,6 +476,168 @@ void fill_stats(wc_results* R, double kernel_ms, uint64_t launches, double wall_
   R->stats.launches = launches;
   R->stats.wall_ms = wall_ms;
 }
+
+// consensus.rs:345 — single results sorted by sequence
+void build_single(const EngineRun& E, uint32_t id, int mode, ProbRes& pr) {
+  for (int s = 0; s < S_NSTAT; ++s) pr.stats[s] = E.stats[id][s];
+  pr.status = E.status[id];
+  pr.error = E.error[id];
+  if (pr.status != WC_OK) return;
+  for (const RawRecord& rr : E.recs[id]) {
+    ConsRec c;
+    c.seq = rr.con[0];
+    for (auto e : rr.fe[0]) c.scores.push_back(cost_of_h(e, mode));
+    pr.single.push_back(std::move(c));
+  }
+  std::stable_sort(pr.single.begin(), pr.single.end(), [](const ConsRec& a, const ConsRec& b) { return a.seq < b.seq; });
+}
+
+// DualConsensus::from_node (dual_consensus.rs:102-150) on a finalized record
+bool dual_from_record(const RawRecord& rr, uint32_t n, int mode, DualRec& d) {
+  std::vector<uint64_t> sc[2];
+  const bool swap = rr.dual && (rr.con[1] < rr.con[0]);
+  d.is_c1.clear();
+  for (uint32_t r = 0; r < n; ++r) {
+    const uint32_t e1 = rr.fe[0][r], e2 = rr.dual ? rr.fe[1][r] : kInactive;
+    int idx = -1;
+    uint64_t best = UINT64_MAX;
+    if (e1 != kInactive) {
+      best = cost_of_h(e1, mode);
+      idx = 0;
+    }
+    if (e2 != kInactive && cost_of_h(e2, mode) < best) {
+      best = cost_of_h(e2, mode);
+      idx = 1;
+    }
+    if (idx < 0) return false;  // assert!(best_con_index <= 1)
+    d.is_c1.push_back((uint8_t)((idx == 0) ^ swap));
+    sc[idx].push_back(best);
+  }
+  ConsRec c1{rr.con[0], sc[0]}, c2{rr.dual ? rr.con[1] : std::vector<uint8_t>(), sc[1]};
+  std::vector<int64_t> s1(n), s2(n);
+  for (uint32_t r = 0; r < n; ++r) {
+    s1[r] = rr.fe[0][r] == kInactive ? -1 : (int64_t)cost_of_h(rr.fe[0][r], mode);
+    uint32_t e2 = rr.dual ? rr.fe[1][r] : kInactive;
+    s2[r] = e2 == kInactive ? -1 : (int64_t)cost_of_h(e2, mode);
+  }
+  if (swap) {
+    d.c1 = c2;
+    d.c2 = c1;
+    d.has_c2 = true;
+    d.s1 = s2;
+    d.s2 = s1;
+  } else {
+    d.c1 = c1;
+    d.has_c2 = rr.dual;
+    if (rr.dual) d.c2 = c2;
+    d.s1 = s1;
+    d.s2 = s2;
+  }
+  return true;
+}
+
+void build_dual(const EngineRun& E, uint32_t id, uint32_t n, int mode, ProbRes& pr) {
+  for (int s = 0; s < S_NSTAT; ++s) pr.stats[s] = E.stats[id][s];
+  pr.status = E.status[id];
+  pr.error = E.error[id];
+  if (pr.status != WC_OK) return;
+  for (const RawRecord& rr : E.recs[id]) {
+    DualRec d;
+    if (!dual_from_record(rr, n, mode, d)) {
+      pr.status = WC_E_INVARIANT;
+      pr.error = "read without a tracked consensus in a result";
+      return;
+    }
+    pr.dual.push_back(std::move(d));
+  }
+  if (pr.dual.size() > 1) {
+    // dual_consensus.rs:744-766
+    std::stable_sort(pr.dual.begin(), pr.dual.end(), [](const DualRec& a, const DualRec& b) {
+      static const std::vector<uint8_t> empty;
+      const auto& a2 = a.has_c2 ? a.c2.seq : empty;
+      const auto& b2 = b.has_c2 ? b.c2.seq : empty;
+      if (a.c1.seq != b.c1.seq) return a.c1.seq < b.c1.seq;
+      return a2 < b2;
+    });
+  }
+  if (pr.dual.empty()) {
+    // dual_consensus.rs:772-779: fallback to the root (every read active, empty consensus)
+    RawRecord root;
+    root.fe[0].assign(n, 0);
+    DualRec d;
+    dual_from_record(root, n, mode, d);
+    pr.dual.push_back(std::move(d));
+  }
+}
+
+template <class F>
+int with_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, F&& fn) {
+  std::unique_ptr<wc_batch> b(new wc_batch());
+  int rc = upload_batch(ctx, n, problems, b.get());
+  if (rc != WC_OK) return rc;
+  return fn(b.get());
+}
+
+// ---- PriorityConsensusDWFA helpers ----
+uint64_t fx_add(uint64_t h, uint64_t w) { return (((h << 5) | (h >> 59)) ^ w) * 0x517cc1b727220a95ULL; }
+uint64_t fx_hash_opt(int64_t v) { return v < 0 ? fx_add(0, 0) : fx_add(fx_add(0, 1), (uint64_t)v); }
+size_t fx_cap_h(size_t b) { return b == 0 ? 0 : (b < 8 ? b - 1 : b / 8 * 7); }
+size_t fx_buckets_h(size_t cap) {
+  if (cap < 8) return cap < 4 ? 4 : 8;
+  size_t adj = cap * 8 / 7, p = 1;
+  while (p < adj) p <<= 1;
+  return p;
+}
+// FxHashSet<Option<usize>> iteration order of the seed groups (priority_consensus.rs:180)
+std::vector<int64_t> seed_order(const std::vector<int64_t>& groups) {
+  std::vector<int64_t> keys;
+  std::vector<uint64_t> hashes;
+  std::vector<int64_t> tab;
+  size_t items = 0, growth = 0;
+  auto slot = [&](uint64_t h) -> size_t {
+    size_t B = tab.size(), mask = B - 1, pos = (size_t)h & mask;
+    if (B < 16) {
+      for (size_t i = pos; i < B; ++i)
+        if (tab[i] < 0) return i;
+      for (size_t i = 0; i < B; ++i)
+        if (tab[i] < 0) return i;
+      return 0;
+    }
+    size_t stride = 0;
+    for (;;) {
+      for (size_t j = 0; j < 16; ++j)
+        if (tab[(pos + j) & mask] < 0) return (pos + j) & mask;
+      stride += 16;
+      pos = (pos + stride) & mask;
+    }
+  };
+  for (int64_t g : groups) {
+    if (std::find(keys.begin(), keys.end(), g) != keys.end()) continue;
+    if (growth == 0) {
+      size_t nb = fx_buckets_h(std::max(items + 1, fx_cap_h(tab.size()) + 1));
+      std::vector<int64_t> old = tab;
+      tab.assign(nb, -1);
+      for (auto o : old)
+        if (o >= 0) tab[slot(hashes[o])] = o;
+      growth = fx_cap_h(nb) - items;
+    }
+    keys.push_back(g);
+    hashes.push_back(fx_hash_opt(g));
+    tab[slot(hashes.back())] = (int64_t)keys.size() - 1;
+    items++;
+    growth--;
+  }
+  std::vector<int64_t> out;
+  for (auto t : tab)
+    if (t >= 0) out.push_back(keys[t]);
+  return out;
+}
+
+struct PWork {
+  std::vector<uint8_t> inc;
+  uint32_t level;
+  std::vector<ConsRec> chain;
+};
 }  // namespace
 
 // ------------------------------------------------------------------------
@@ -414,12 +665,11 @@ void wc_config_default(wc_config* c) {
 
 int wc_ctx_create(int device, wc_ctx** out) {
   *out = nullptr;
-  wc_ctx* ctx = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return WC_E_HIP;
   if (device < 0 || device >= ndev) return WC_E_HIP;
   if (hipSetDevice(device) != hipSuccess) return WC_E_HIP;
-  ctx = new wc_ctx();
+  wc_ctx* ctx = new wc_ctx();
   ctx->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
@@ -435,8 +685,7 @@ int wc_ctx_create(int device, wc_ctx** out) {
 void wc_ctx_destroy(wc_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  for (DevBuf* b : {&ctx->reads, &ctx->roff, &ctx->rlen, &ctx->ract, &ctx->probs, &ctx->ws, &ctx->out, &ctx->status,
-                    &ctx->stats, &ctx->counter})
+  for (DevBuf* b : {&ctx->ract, &ctx->probs, &ctx->ws, &ctx->out, &ctx->status, &ctx->stats, &ctx->counter, &ctx->jobs})
     b->release();
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -446,42 +695,205 @@ void wc_ctx_destroy(wc_ctx* ctx) {
 
 const char* wc_last_error(const wc_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 
+int wc_batch_create(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch** out) {
+  *out = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
+  std::unique_ptr<wc_batch> b(new wc_batch());
+  int rc = upload_batch(ctx, n, problems, b.get());
+  if (rc != WC_OK) return rc;
+  *out = b.release();
+  return WC_OK;
+}
+
+void wc_batch_free(wc_batch* b) { delete b; }
+
+uint64_t wc_batch_bytes(const wc_batch* b) { return b ? b->bytes : 0; }
+
+int wc_batch_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  *out = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
+  const uint32_t n = (uint32_t)b->probs.size();
+  std::unique_ptr<wc_results> R(new wc_results());
+  R->kind = 0;
+  R->probs.resize(n);
+  std::vector<uint32_t> ids(n);
+  std::iota(ids.begin(), ids.end(), 0u);
+  EngineRun E;
+  int rc = run_engine(ctx, b, *cfg, 1, ids, E);
+  if (rc != WC_OK) return rc;
+  for (uint32_t id = 0; id < n; ++id) build_single(E, id, cfg->consensus_cost, R->probs[id]);
+  double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  fill_stats(R.get(), E.kernel_ms, E.launches, wall);
+  *out = R.release();
+  return WC_OK;
+}
+
+int wc_batch_dual_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  *out = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
+  const uint32_t n = (uint32_t)b->probs.size();
+  std::unique_ptr<wc_results> R(new wc_results());
+  R->kind = 1;
+  R->probs.resize(n);
+  std::vector<uint32_t> ids(n);
+  std::iota(ids.begin(), ids.end(), 0u);
+  EngineRun E;
+  int rc = run_engine(ctx, b, *cfg, 2, ids, E);
+  if (rc != WC_OK) return rc;
+  for (uint32_t id = 0; id < n; ++id) build_dual(E, id, b->probs[id].n_reads, cfg->consensus_cost, R->probs[id]);
+  double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  fill_stats(R.get(), E.kernel_ms, E.launches, wall);
+  *out = R.release();
+  return WC_OK;
+}
+
 int wc_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, const wc_problem* problems, wc_results** out) {
+  *out = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
+  return with_batch(ctx, n, problems, [&](wc_batch* b) { return wc_batch_consensus(ctx, b, cfg, out); });
+}
+
+int wc_dual_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, const wc_problem* problems,
+                            wc_results** out) {
+  *out = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
+  return with_batch(ctx, n, problems, [&](wc_batch* b) { return wc_batch_dual_consensus(ctx, b, cfg, out); });
+}
+
+// ---- PriorityConsensusDWFA (priority_consensus.rs:172-341) ----
+// Each problem keeps the reference's LIFO work stack; every round takes the
+// top item of every problem and runs all of them as one dual-engine batch.
+// Within a problem the processing order is exactly the reference's.
+int wc_priority_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, const wc_chain_problem* problems,
+                                wc_results** out) {
   auto t0 = std::chrono::steady_clock::now();
   *out = nullptr;
   if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
   std::unique_ptr<wc_results> R(new wc_results());
-  R->kind = 0;
+  R->kind = 2;
   R->probs.resize(n);
-  std::vector<uint32_t> runnable;
-  std::vector<PackedProblem> pp = prepare_all(*cfg, n, problems, R->probs, runnable);
-  std::vector<std::vector<RawRecord>> recs(n);
-  std::vector<int> status(n, WC_OK);
-  std::vector<std::array<uint64_t, S_NSTAT>> stats(n);
-  for (auto& s : stats) s.fill(0);
-  double kms = 0;
-  uint64_t launches = 0;
-  if (!runnable.empty()) {
-    int rc = run_engine(ctx, *cfg, 1, pp, runnable, recs, status, stats, kms, launches);
-    if (rc != WC_OK) return rc;
-  }
-  for (uint32_t id : runnable) {
-    ProbRes& pr = R->probs[id];
-    for (int s = 0; s < S_NSTAT; ++s) pr.stats[s] = stats[id][s];
-    pr.status = status[id];
-    if (pr.status != WC_OK) {
-      pr.error = err_msg(pr.status);
+  std::vector<std::vector<PWork>> stacks(n);
+  std::vector<std::vector<std::vector<ConsRec>>> cons(n);
+  std::vector<std::vector<std::vector<uint8_t>>> assigns(n);
+  std::vector<bool> alive(n, true);
+  for (uint32_t i = 0; i < n; ++i) {
+    const wc_chain_problem& q = problems[i];
+    if (q.n_chains == 0 || q.levels == 0) {
+      R->probs[i].status = WC_E_BAD_INPUT;
+      R->probs[i].error = "Must provide a non-empty sequences Vec";
+      alive[i] = false;
       continue;
     }
-    for (auto& rr : recs[id]) {
-      ConsRec c;
-      c.seq = rr.con[0];
-      for (auto e : rr.fe[0]) c.scores.push_back(cost_of_h(e, cfg->consensus_cost));
-      pr.single.push_back(std::move(c));
+    std::vector<int64_t> groups(q.n_chains, -1);
+    if (q.seed_groups)
+      for (uint32_t c = 0; c < q.n_chains; ++c) groups[c] = q.seed_groups[c] < 0 ? -1 : q.seed_groups[c];
+    for (int64_t g : seed_order(groups)) {
+      PWork w;
+      w.inc.resize(q.n_chains);
+      for (uint32_t c = 0; c < q.n_chains; ++c) w.inc[c] = groups[c] == g;
+      w.level = 0;
+      stacks[i].push_back(std::move(w));
     }
-    // consensus.rs:345 — sort by sequence
-    std::stable_sort(pr.single.begin(), pr.single.end(),
-                     [](const ConsRec& a, const ConsRec& b) { return a.seq < b.seq; });
+  }
+  double kms = 0;
+  uint64_t launches = 0;
+  for (;;) {
+    std::vector<uint32_t> active;
+    for (uint32_t i = 0; i < n; ++i)
+      if (alive[i] && !stacks[i].empty()) active.push_back(i);
+    if (active.empty()) break;
+    // this round's sub-problems: the top of every live stack
+    std::vector<PWork> items;
+    std::vector<std::vector<const uint8_t*>> rp(active.size());
+    std::vector<std::vector<uint64_t>> rl(active.size());
+    std::vector<std::vector<int64_t>> ro(active.size());
+    std::vector<wc_problem> sub(active.size());
+    for (size_t k = 0; k < active.size(); ++k) {
+      const uint32_t i = active[k];
+      const wc_chain_problem& q = problems[i];
+      items.push_back(std::move(stacks[i].back()));
+      stacks[i].pop_back();
+      const PWork& w = items.back();
+      for (uint32_t c = 0; c < q.n_chains; ++c) {
+        if (!w.inc[c]) continue;
+        rp[k].push_back(q.reads[c * q.levels + w.level]);
+        rl[k].push_back(q.lens[c * q.levels + w.level]);
+        ro[k].push_back(q.offsets ? q.offsets[c * q.levels + w.level] : -1);
+      }
+      sub[k].n_reads = (uint32_t)rp[k].size();
+      sub[k].reads = rp[k].data();
+      sub[k].lens = rl[k].data();
+      sub[k].offsets = ro[k].data();
+    }
+    wc_results* dr = nullptr;
+    int rc = wc_dual_consensus_batch(ctx, cfg, (uint32_t)sub.size(), sub.data(), &dr);
+    if (rc != WC_OK) return rc;
+    std::unique_ptr<wc_results> D(dr);
+    kms += D->stats.kernel_ms;
+    launches += D->stats.launches;
+    for (size_t k = 0; k < active.size(); ++k) {
+      const uint32_t i = active[k];
+      const wc_chain_problem& q = problems[i];
+      ProbRes& pr = R->probs[i];
+      const ProbRes& d = D->probs[k];
+      for (int s = 0; s < S_NSTAT; ++s)
+        pr.stats[s] = s == S_PEAKQ ? std::max(pr.stats[s], d.stats[s]) : pr.stats[s] + d.stats[s];
+      if (d.status != WC_OK) {
+        pr.status = d.status;
+        pr.error = d.error;
+        alive[i] = false;
+        continue;
+      }
+      PWork& w = items[k];
+      const DualRec& ch = d.dual[0];
+      if (ch.has_c2) {
+        std::vector<uint8_t> a1(q.n_chains, 0), a2(q.n_chains, 0);
+        size_t idx = 0;
+        for (uint32_t c = 0; c < q.n_chains; ++c) {
+          if (!w.inc[c]) continue;
+          if (ch.is_c1[idx]) a1[c] = 1;
+          else a2[c] = 1;
+          idx++;
+        }
+        stacks[i].push_back(PWork{a1, w.level, w.chain});
+        stacks[i].push_back(PWork{a2, w.level, w.chain});
+      } else {
+        w.chain.push_back(ch.c1);
+        if (w.level + 1 == q.levels) {
+          cons[i].push_back(w.chain);
+          assigns[i].push_back(w.inc);
+        } else {
+          stacks[i].push_back(PWork{w.inc, w.level + 1, w.chain});
+        }
+      }
+    }
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    ProbRes& pr = R->probs[i];
+    if (pr.status != WC_OK) continue;
+    const uint32_t M = problems[i].n_chains;
+    auto& C = cons[i];
+    if (C.size() > 1) {
+      std::vector<size_t> ord(C.size());
+      std::iota(ord.begin(), ord.end(), 0);
+      std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+        size_t m = std::min(C[a].size(), C[b].size());
+        for (size_t l = 0; l < m; ++l)
+          if (C[a][l].seq != C[b][l].seq) return C[a][l].seq < C[b][l].seq;
+        return C[a].size() < C[b].size();
+      });
+      pr.indices.assign(M, UINT64_MAX);
+      for (size_t ci = 0; ci < ord.size(); ++ci) {
+        for (uint32_t c = 0; c < M; ++c)
+          if (assigns[i][ord[ci]][c]) pr.indices[c] = ci;
+        pr.chains.push_back(C[ord[ci]]);
+      }
+    } else {
+      pr.chains = C;
+      pr.indices.assign(M, 0);
+    }
   }
   double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   fill_stats(R.get(), kms, launches, wall);
@@ -579,6 +991,88 @@ int wc_results_problem_stats(const wc_results* r, uint32_t p, wc_stats* o) {
   return WC_OK;
 }
 
+// ---- standalone DWFALite batch (dynamic_wfa.rs:48-265) ----
+int wc_dwfa_batch(wc_ctx* ctx, uint32_t n, wc_dwfa_job* jobs) {
+  if (n == 0) return WC_OK;
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
+  // one arena: per job baseline | other | wavefront (u32, cap)
+  std::vector<uint64_t> boff(n), ooff(n), woff(n);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (jobs[i].wf_cap < jobs[i].wf_len || jobs[i].wf_len != 2 * jobs[i].e + 1)
+      return set_err(ctx, WC_E_BAD_INPUT, "wavefront length must be 2e+1 and fit wf_cap");
+    boff[i] = total;
+    total += (jobs[i].baseline_len + 15) & ~15ull;
+    ooff[i] = total;
+    total += (jobs[i].other_len + 15) & ~15ull;
+    woff[i] = total;
+    total += (jobs[i].wf_cap * 4 + 15) & ~15ull;
+  }
+  std::vector<uint8_t> h(std::max<uint64_t>(total, 16));
+  std::vector<DwfaDevJob> dj(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const wc_dwfa_job& j = jobs[i];
+    if (j.baseline_len) memcpy(h.data() + boff[i], j.baseline, j.baseline_len);
+    if (j.other_len) memcpy(h.data() + ooff[i], j.other, j.other_len);
+    uint32_t* wf = (uint32_t*)(h.data() + woff[i]);
+    for (uint64_t k = 0; k < j.wf_len; ++k) wf[k] = (uint32_t)j.wavefront[k];
+  }
+  DevBuf arena;
+  if (!arena.ensure(h.size()) || !ctx->jobs.ensure(n * sizeof(DwfaDevJob)))
+    return set_err(ctx, WC_E_HIP, "device allocation failed (dwfa)");
+  uint8_t* base = (uint8_t*)arena.p;
+  for (uint32_t i = 0; i < n; ++i) {
+    const wc_dwfa_job& j = jobs[i];
+    DwfaDevJob& d = dj[i];
+    memset(&d, 0, sizeof(d));
+    d.baseline = base + boff[i];
+    d.blen = (uint32_t)j.baseline_len;
+    d.other = base + ooff[i];
+    d.olen = (uint32_t)j.other_len;
+    d.offset = (uint32_t)j.offset;
+    d.wildcard = j.wildcard;
+    d.early = j.early;
+    d.op = j.op;
+    d.e = (uint32_t)j.e;
+    d.wf = (uint32_t*)(base + woff[i]);
+    d.wf_cap = (uint32_t)j.wf_cap;
+  }
+  int rc = WC_OK;
+  do {
+    if (hipMemcpyAsync(arena.p, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(ctx->jobs.p, dj.data(), n * sizeof(DwfaDevJob), hipMemcpyHostToDevice, ctx->stream) !=
+            hipSuccess) {
+      rc = set_err(ctx, WC_E_HIP, "copy to device failed (dwfa)");
+      break;
+    }
+    launch_dwfa_jobs((DwfaDevJob*)ctx->jobs.p, n, ctx->stream);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess ||
+        hipMemcpy(dj.data(), ctx->jobs.p, n * sizeof(DwfaDevJob), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(h.data(), arena.p, h.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = set_err(ctx, WC_E_HIP, "dwfa kernel failed");
+      break;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+      wc_dwfa_job& j = jobs[i];
+      const DwfaDevJob& d = dj[i];
+      j.status = (int32_t)d.status;
+      if (d.status != 0) continue;
+      j.e = d.e;
+      const uint32_t W = 2 * d.e + 1;
+      j.wf_len = W;
+      const uint32_t* wf = (const uint32_t*)(h.data() + woff[i]);
+      for (uint32_t k = 0; k < W && k < j.wf_cap; ++k) j.wavefront[k] = wf[k];
+      j.n_cand = d.n_cand;
+      for (uint32_t k = 0; k < d.n_cand && k < 16; ++k) {
+        j.cand_syms[k] = d.cand_syms[k];
+        j.cand_counts[k] = d.cand_counts[k];
+      }
+    }
+  } while (0);
+  arena.release();
+  return rc;
+}
+
 // ---- generator ----
 struct wc_gen {
   std::vector<uint8_t> consensus;
@@ -608,16 +1102,3 @@ const uint8_t* wc_gen_sample(const wc_gen* g, uint64_t i, uint64_t* len) {
 void wc_gen_free(wc_gen* g) { delete g; }
 
 }  // extern "C"
-
-// ---- temporary entry points (implemented in the next milestone) ----
-extern "C" {
-int wc_dual_consensus_batch(wc_ctx* ctx, const wc_config*, uint32_t, const wc_problem*, wc_results** out) {
-  *out = nullptr;
-  return set_err(ctx, WC_E_LIMIT, "dual engine not built yet");
-}
-int wc_priority_consensus_batch(wc_ctx* ctx, const wc_config*, uint32_t, const wc_chain_problem*, wc_results** out) {
-  *out = nullptr;
-  return set_err(ctx, WC_E_LIMIT, "priority engine not built yet");
-}
-int wc_dwfa_batch(wc_ctx* ctx, uint32_t, wc_dwfa_job*) { return set_err(ctx, WC_E_LIMIT, "dwfa batch not built yet"); }
-}
