@@ -9,7 +9,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwaffle_con.so")
+# WAFFLE_CON_LIB may name another in-tree build variant (A/B benchmarking)
+LIB_PATH = os.environ.get("WAFFLE_CON_LIB") or os.path.join(_HERE, "libwaffle_con.so")
 
 _lib = None
 _lock = threading.Lock()

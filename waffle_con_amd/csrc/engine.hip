@@ -6,14 +6,15 @@
 // global work counter and executes the reference's least-cost-first search
 // with the reference's exact pop order (priority-queue 1.x heap, SURVEY
 // Appendix A), candidate order (hashbrown/FxHash iteration, Appendix B) and
-// f64 vote summation order. Node DWFA state lives in a per-workgroup node pool
-// in HBM (clone on branch, in place for the last child); the heap, node
-// metadata and per-read nomination summaries live in LDS.
+// f64 vote summation order.
 //
-// Per pop: ANALYZE (per-read tips + end flags), optional FINALIZE of the
-// popped node on scratch, VOTES (ordered f64 sums), then PUSH of every child
-// (the per-read DWFA update, dynamic_wfa.rs:75-99) followed by a prune + cost
-// reduction pass.
+// Node state lives in a per-workgroup node pool in HBM: per read a 64-byte
+// frontier cache (RState) plus the authoritative wavefront row. A push is one
+// thread per read on its RState (O(frontier) work, no full scan); only reads
+// whose edit distance must grow (or whose frontier is wide) take the
+// wave-cooperative path over the full wavefront. The heap, node metadata,
+// per-read nominations and the pushed child's analysis live in LDS, so the
+// common linear search step (one child, popped next) never re-reads node state.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -21,9 +22,16 @@
 
 namespace wc {
 
+// minimum waves per SIMD the engine kernels are register-allocated for
+// (4 = 4 workgroups of 4 waves per CU, 128 VGPRs)
+#ifndef WC_WAVES_PER_EU
+#define WC_WAVES_PER_EU 4
+#endif
+
 constexpr int kMaxChild = 64;
 constexpr uint32_t WC_E_INVARIANT_CODE = 10;  // include/waffle_con.h
 constexpr uint32_t WC_E_LIMIT_CODE = 11;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 struct Ctl {
   uint32_t prob;
@@ -34,10 +42,12 @@ struct Ctl {
   uint32_t top_dual;
   uint64_t top_cost;
   uint32_t n_end[2];
+  uint32_t multi[2];
   uint32_t n_either;
   uint32_t ovf;
   uint32_t reached;
   uint32_t fin[2];
+  uint32_t nheavy;
   uint64_t cost_acc;
   uint32_t some_acc[2];
   uint64_t max_err;
@@ -46,9 +56,14 @@ struct Ctl {
   uint32_t am_len;
   uint32_t n_ret;
   int32_t store_idx;
+  uint32_t cache_slot, cache_hit, cache_nend, cache_multi;
   uint32_t nkeys[2];
   uint8_t keys[2][kKout];
   double vals[2][kKout];
+  // thread-0 scratch for child enumeration (kept in LDS, not private memory)
+  int16_t opt[2][kKout + 1];
+  double srt_v[kKout];
+  uint8_t srt_s[kKout];
   uint32_t nchild;
   int16_t ch_s[kMaxChild][2];  // symbol per side, -1 = none (lock for dual children)
   uint8_t ch_kind[kMaxChild];  // 0 dual child, 1 stay-single, 2 split (activate_dual)
@@ -63,8 +78,9 @@ struct Lds {
   HeapEntry* heap;
   uint32_t* freestack;
   SlotMeta* meta;
-  RInfo* rinfo;  // [sides][nmax]
-  uint32_t* fe;  // [sides][nmax]
+  RInfo* rinfo;    // [sides][nmax]
+  uint32_t* fe;    // [sides][nmax]
+  uint32_t* list;  // [2*nmax] work list (heavy reads / wide analyses)
 };
 
 __device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32_t nmax) {
@@ -79,6 +95,8 @@ __device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32
   l.rinfo = (RInfo*)p;
   p += (uint64_t)sides * nmax * sizeof(RInfo);
   l.fe = (uint32_t*)p;
+  p += align16((uint64_t)sides * nmax * 4);
+  l.list = (uint32_t*)p;
   return l;
 }
 
@@ -153,6 +171,17 @@ __device__ inline uint64_t ceil_u64(double x) {
   return (uint64_t)c;
 }
 
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
+    uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
+    v += ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+// wave-uniform counters (lane 0 holds them)
 __device__ inline void flush_counters(Ctl& ctl, const WaveCounters& wc) {
   if (lane_id() == 0) {
     if (wc.updates) atomicAdd((unsigned long long*)&ctl.cnt[S_UPDATES], (unsigned long long)wc.updates);
@@ -162,6 +191,13 @@ __device__ inline void flush_counters(Ctl& ctl, const WaveCounters& wc) {
     if (wc.finalizes) atomicAdd((unsigned long long*)&ctl.cnt[S_FINALIZES], (unsigned long long)wc.finalizes);
   }
 }
+// per-thread counters (every lane its own): wave-reduce, then lane 0 adds
+__device__ inline void flush_thread_counters(Ctl& ctl, WaveCounters c) {
+  c.updates = wave_sum_u32(c.updates);
+  c.w_out = wave_sum_u32(c.w_out);
+  c.compares = wave_sum_u32(c.compares);
+  flush_counters(ctl, c);
+}
 
 // per-workgroup engine context (registers)
 struct Eng {
@@ -169,8 +205,7 @@ struct Eng {
   uint8_t* ws;
   uint64_t sbytes;
   uint32_t nmax, wcap, lcap, pcap, sides, n;
-  uint32_t* trk_lc[2];
-  uint32_t* trk_pc[2];
+  uint32_t* trk;  // [lc0 | pc0 | lc1 | pc1], each lcap+2 u32
   uint32_t* total_active;
   uint32_t* active_min;
   uint32_t* scratch;
@@ -182,7 +217,9 @@ struct Eng {
   __device__ const uint8_t* read(uint32_t r) const { return A->rbytes + A->roff[P.read_begin + r]; }
   __device__ uint32_t rlen(uint32_t r) const { return A->rlen[P.read_begin + r]; }
   __device__ TrackerRef tracker(Ctl& ctl, int k) const {
-    return TrackerRef{trk_lc[k], trk_pc[k], &ctl.trk_total[k], &ctl.trk_thr[k], A->cfg.max_capacity_per_size};
+    const uint64_t L2 = lcap + 2;
+    return TrackerRef{trk + 2 * k * L2, trk + (2 * k + 1) * L2, &ctl.trk_total[k], &ctl.trk_thr[k],
+                      A->cfg.max_capacity_per_size};
   }
 };
 
@@ -198,10 +235,7 @@ __device__ inline Eng make_eng(const EngineArgs& A, uint8_t* smem) {
   E.sbytes = slot_bytes(A.sides, A.nmax, A.wcap, A.lcap);
   uint32_t* t = (uint32_t*)(E.ws + (uint64_t)A.pcap * E.sbytes);
   const uint32_t L2 = A.lcap + 2;
-  E.trk_lc[0] = t;
-  E.trk_pc[0] = t + L2;
-  E.trk_lc[1] = t + 2 * L2;
-  E.trk_pc[1] = t + 3 * L2;
+  E.trk = t;
   uint8_t* q = E.ws + (uint64_t)A.pcap * E.sbytes + align16((uint64_t)4 * L2 * 4);
   E.total_active = (uint32_t*)q;
   E.active_min = E.total_active + L2;
@@ -211,13 +245,13 @@ __device__ inline Eng make_eng(const EngineArgs& A, uint8_t* smem) {
   return E;
 }
 
-// ---- per-problem init: free stack, trackers, root node ----
+// ---- per-problem init: free stack, trackers, root node (consensus.rs:384-403) ----
 __device__ inline void init_problem(Eng& E, Ctl& ctl) {
   const int tid = threadIdx.x;
   const DevConfig& cfg = E.A->cfg;
   if (tid == 0) {
     ctl.heap_n = 0;
-    ctl.nfree = E.pcap - 1;  // slot 0 (stack top) becomes the root
+    ctl.nfree = E.pcap - 1;  // slot 0 (the stack top) becomes the root
     ctl.status = ST_OK;
     ctl.max_err = ~0ull;
     for (int k = 0; k < 2; ++k) {
@@ -228,15 +262,18 @@ __device__ inline void init_problem(Eng& E, Ctl& ctl) {
     }
     ctl.n_ret = 0;
     ctl.am_len = 1;
+    ctl.cache_slot = kNoSlot;
     for (int s = 0; s < S_NSTAT; ++s) ctl.cnt[s] = 0;
   }
   for (uint32_t i = tid; i < E.pcap; i += kBlock) E.L.freestack[i] = E.pcap - 1 - i;
-  for (uint32_t i = tid; i < 4 * (E.lcap + 2); i += kBlock) E.trk_lc[0][i] = 0;
+  for (uint32_t i = tid; i < 4 * (E.lcap + 2); i += kBlock) E.trk[i] = 0;
   SideView v = E.sv(0, 0);
   for (uint32_t r = tid; r < E.n; r += kBlock) {
-    const bool act = E.A->ractivate[E.P.read_begin + r] < 0;
-    v.e[r] = act ? 0u : kInactive;
-    v.off[r] = 0;
+    // e = 0 (or None), off = 0, maxb = 0, nscmp = 0, nf = 1: the single
+    // diagonal d=0 sits at the (empty) consensus end
+    const uint32_t e = E.A->ractivate[E.P.read_begin + r] < 0 ? 0u : kInactive;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    rstate_store(&v.rs[r], RRaw{make_uint4(e, 0, 0, 1u << 16), z, z, z});
     v.wf[(uint64_t)r * E.wcap] = 0;
   }
   __syncthreads();
@@ -254,26 +291,49 @@ __device__ inline void init_problem(Eng& E, Ctl& ctl) {
   __syncthreads();
 }
 
-// ---- ANALYZE one side of a node: per-read tips / end flags into rinfo ----
+// ---- ANALYZE one node side (block-level, contains barriers) ----
+// Thread per read from the RState; reads with a wide frontier are nominated by
+// a wave over their full wavefront. Counts n_end / multi of the side.
 __device__ inline void analyze_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t side, uint32_t len, RInfo* out) {
-  const int lane = lane_id();
+  const int tid = threadIdx.x, lane = lane_id();
   SideView v = E.sv(slot, side);
-  for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
-    const uint32_t e = v.e[r];
-    if (e == kInactive) {
-      if (lane == 0) {
-        out[r].e = kInactive;
-        out[r].n = 0;
-        out[r].end = 0;
-      }
+  if (tid == 0) ctl.nheavy = 0;
+  __syncthreads();
+  uint32_t ends = 0, multi = 0;
+  for (uint32_t r = tid; r < E.n; r += kBlock) {
+    const RRaw s = rstate_load(&v.rs[r]);
+    if (rraw_e(s) == kInactive) {
+      out[r].e = kInactive;
+      out[r].n = 0;
+      out[r].end = 0;
       continue;
     }
-    bool ok = wave_analyze_read(v.wf + (uint64_t)r * E.wcap, e, v.off[r], E.read(r), E.rlen(r), len, &out[r]);
+    if (rraw_flags(s) & kWide) {
+      E.L.list[atomicAdd(&ctl.nheavy, 1u)] = r;
+      continue;
+    }
+    Front f;
+    front_load(s, f);
+    bool m;
+    thread_analyze(f, E.read(r), E.rlen(r), len, &out[r], m);
+    ends += out[r].end;
+    multi |= m;
+  }
+  if (ends) atomicAdd(&ctl.n_end[side], ends);
+  if (multi) atomicOr(&ctl.multi[side], 1u);
+  __syncthreads();
+  const uint32_t nh = ctl.nheavy;
+  for (uint32_t k = wave_id(); k < nh; k += kWaves) {
+    const uint32_t r = E.L.list[k];
+    const uint32_t e = v.rs[r].e, off = v.rs[r].off;
+    const bool ok = wave_analyze_read(v.wf + (uint64_t)r * E.wcap, e, off, E.read(r), E.rlen(r), len, &out[r]);
     if (lane == 0) {
       if (!ok) atomicOr(&ctl.ovf, 1u);
       if (out[r].end) atomicAdd(&ctl.n_end[side], 1u);
+      if (out[r].n > 1) atomicOr(&ctl.multi[side], 1u);
     }
   }
+  __syncthreads();
 }
 
 // ---- FINALIZE one side on scratch (the node is not modified) ----
@@ -282,14 +342,14 @@ __device__ inline void finalize_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t s
   const int lane = lane_id();
   SideView v = E.sv(slot, side);
   for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
-    const uint32_t e = v.e[r];
+    const uint32_t e = v.rs[r].e;
     if (e == kInactive) {
       if (lane == 0) fe[r] = kInactive;
       continue;
     }
     uint32_t f = 0;
-    bool ok = wave_finalize_read(v.wf + (uint64_t)r * E.wcap, e, v.off[r], E.read(r), E.rlen(r), v.con, len,
-                                 E.A->cfg.wildcard, E.scratch, E.wcap, f, cnt);
+    const bool ok = wave_finalize_read(v.wf + (uint64_t)r * E.wcap, e, v.rs[r].off, E.read(r), E.rlen(r), v.con,
+                                       len, E.A->cfg.wildcard, E.scratch, E.wcap, f, cnt);
     if (lane == 0) {
       if (!ok) atomicOr(&ctl.ovf, 4u);
       fe[r] = ok ? f : kInactive;
@@ -298,62 +358,126 @@ __device__ inline void finalize_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t s
   }
 }
 
-// ---- PUSH symbols onto up to two sides of one node (sym < 0 = untouched) ----
-// Work items are (side, read) pairs spread over the waves. The new symbol is
-// already written at con[len-1] of each pushed side. Optional single-side
-// cost accumulation (ConsensusNode::priority, consensus.rs:480-510).
+// ---- PUSH symbols onto up to two sides of one node (block-level, barriers) ----
+// The new symbol is already written at con[len-1] of each pushed side.
+// Work items are (side, read) pairs: thread step on the RState, then the wave
+// path for reads that must grow their edit distance. When `info` is set, the
+// pushed side-0 child's nominations are written there (the next pop's
+// analysis). When `want_cost`, accumulates the single-side priority cost.
 __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
-                                  bool want_cost, WaveCounters& cnt) {
-  const int lane = lane_id();
+                                  bool want_cost, RInfo* info) {
+  const int tid = threadIdx.x, lane = lane_id();
   const DevConfig& cfg = E.A->cfg;
+  const bool early = cfg.early != 0;
+  if (tid == 0) ctl.nheavy = 0;
+  __syncthreads();
+  WaveCounters tc = {0, 0, 0, 0, 0};
   uint64_t cost = 0;
-  const uint32_t items = 2 * E.n;
-  for (uint32_t it = wave_id(); it < items; it += kWaves) {
-    const uint32_t side = it / E.n, r = it % E.n;
+  uint32_t ends = 0, multi = 0;
+  // work items over the pushed sides only: (side, read) with side >= first
+  const uint32_t first = s0 >= 0 ? 0u : 1u;
+  const uint32_t items = ((s0 >= 0 ? 1u : 0u) + (s1 >= 0 ? 1u : 0u)) * E.n;
+  for (uint32_t it = tid; it < items; it += kBlock) {
+    const uint32_t hi = it >= E.n ? 1u : 0u, r = it - hi * E.n, side = first + hi;
     const int sym = side == 0 ? s0 : s1;
-    if (sym < 0) continue;
     SideView v = E.sv(slot, side);
-    uint32_t e = v.e[r];
-    if (e == kInactive) continue;
+    const RRaw s = rstate_load(&v.rs[r]);
+    RInfo* out = (info && side == 0) ? &info[r] : nullptr;
+    if (rraw_e(s) == kInactive) {
+      if (out) {
+        out->e = kInactive;
+        out->n = 0;
+        out->end = 0;
+      }
+      continue;
+    }
     const uint32_t olen = side == 0 ? len0 : len1;
-    bool ok = wave_push_read(v.wf + (uint64_t)r * E.wcap, e, v.off[r], E.read(r), E.rlen(r), v.con, olen,
-                             (uint8_t)sym, cfg.wildcard, cfg.early != 0, E.wcap, cnt);
-    if (!ok) {
+    const uint8_t* rd = E.read(r);
+    const uint32_t blen = E.rlen(r);
+    if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
+      E.L.list[atomicAdd(&ctl.nheavy, 1u)] = side * E.n + r;
+      continue;
+    }
+    Front f;
+    front_load(s, f);
+    uint32_t cmp = 0;
+    const bool heavy =
+        thread_push(f, rd, blen, olen - 1, (uint8_t)sym, cfg.wildcard, early, v.wf + (uint64_t)r * E.wcap, cmp);
+    tc.compares += cmp;
+    front_store(&v.rs[r], f);
+    if (heavy) {
+      E.L.list[atomicAdd(&ctl.nheavy, 1u)] = side * E.n + r;
+      continue;
+    }
+    tc.updates++;
+    tc.w_out += 2 * f.e + 1;
+    cost += cost_of(f.e, cfg.cost_mode);
+    if (out) {
+      bool m;
+      thread_analyze(f, rd, blen, olen, out, m);
+      ends += out->end;
+      multi |= m;
+    }
+  }
+  flush_thread_counters(ctl, tc);
+  if (ends) atomicAdd(&ctl.n_end[0], ends);
+  if (multi) atomicOr(&ctl.multi[0], 1u);
+  if (want_cost && cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);
+  __syncthreads();
+  const uint32_t nh = ctl.nheavy;
+  WaveCounters cnt = {0, 0, 0, 0, 0};
+  for (uint32_t k = wave_id(); k < nh; k += kWaves) {
+    const uint32_t it = E.L.list[k];
+    const uint32_t side = it >= E.n ? 1u : 0u, r = it - side * E.n;
+    SideView v = E.sv(slot, side);
+    const uint32_t olen = side == 0 ? len0 : len1;
+    const int sym = side == 0 ? s0 : s1;
+    uint32_t e = 0;
+    uint32_t* wf = v.wf + (uint64_t)r * E.wcap;
+    if (!wave_heavy(&v.rs[r], wf, E.read(r), E.rlen(r), v.con, olen, (uint8_t)sym, cfg.wildcard, early, E.wcap, cnt,
+                    e)) {
       if (lane == 0) atomicOr(&ctl.ovf, 4u);
       continue;
     }
-    if (lane == 0) v.e[r] = e;
-    cost += cost_of(e, cfg.cost_mode);
+    if (info && side == 0) {
+      const bool ok = wave_analyze_read(wf, e, v.rs[r].off, E.read(r), E.rlen(r), olen, &info[r]);
+      if (lane == 0) {
+        if (!ok) atomicOr(&ctl.ovf, 1u);
+        if (info[r].end) atomicAdd(&ctl.n_end[0], 1u);
+        if (info[r].n > 1) atomicOr(&ctl.multi[0], 1u);
+      }
+    }
+    if (want_cost && lane == 0) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost_of(e, cfg.cost_mode));
   }
-  if (want_cost && lane == 0 && cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);
+  flush_counters(ctl, cnt);
+  __syncthreads();
 }
 
-// ---- clone a node (consensus bytes + live wavefront rows) ----
-__device__ inline void copy_node(Eng& E, uint32_t src, uint32_t dst, uint32_t nsides, const uint32_t* lens) {
+// ---- clone a node: RState records, live wavefront rows, consensus bytes ----
+__device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t dst, uint32_t sdst, uint32_t len) {
   const int tid = threadIdx.x, lane = lane_id();
-  for (uint32_t s = 0; s < nsides; ++s) {
-    SideView a = E.sv(src, s), b = E.sv(dst, s);
-    for (uint32_t i = tid; i < lens[s]; i += kBlock) b.con[i] = a.con[i];
-    for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
-      const uint32_t e = a.e[r];
-      if (lane == 0) {
-        b.e[r] = e;
-        b.off[r] = a.off[r];
-      }
-      if (e == kInactive) continue;
-      const uint32_t W = 2 * e + 1;
-      for (uint32_t i = lane; i < W; i += 64) b.wf[(uint64_t)r * E.wcap + i] = a.wf[(uint64_t)r * E.wcap + i];
-    }
+  SideView a = E.sv(src, ssrc), b = E.sv(dst, sdst);
+  for (uint32_t i = tid; i < len; i += kBlock) b.con[i] = a.con[i];
+  for (uint32_t r = tid; r < E.n; r += kBlock) {
+    rstate_store(&b.rs[r], rstate_load(&a.rs[r]));
+  }
+  for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
+    const uint32_t e = a.rs[r].e;
+    if (e == kInactive) continue;
+    const uint32_t W = 2 * e + 1;
+    const uint32_t* wa = a.wf + (uint64_t)r * E.wcap;
+    uint32_t* wb = b.wf + (uint64_t)r * E.wcap;
+    for (uint32_t i = lane; i < W; i += 64) wb[i] = wa[i];
   }
 }
 
 // ---- VOTES (consensus.rs:540-564 / dual_consensus.rs:1242-1290) ----
 // One wave. Outer-map insertion order = first appearance over (read index,
 // inner iteration position); values are summed per key strictly in read order
-// (the reference's f64 order), weight * occ / split. Weights follow
-// get_ed_weights (dual_consensus.rs:1299-1336) when `weighted`. Writes keys /
-// vals of `side` in iteration order with the wildcard removed when other keys
-// exist. Returns false on > kKout keys.
+// (the reference's f64 order), weight * occ / split. When no read has two
+// distinct symbols (and no weights), every contribution is exactly 1.0, so the
+// per-key sums are exact integer counts (order-independent) and are taken
+// with ballots. Weights follow get_ed_weights (dual_consensus.rs:1299-1336).
 __device__ inline double vote_weight(const RInfo* r0, const RInfo* r1, uint32_t r, bool is_dual, bool side1) {
   if (!is_dual) return 1.0;
   const bool h1 = r0[r].e != kInactive, h2 = r1[r].e != kInactive;
@@ -365,12 +489,13 @@ __device__ inline double vote_weight(const RInfo* r0, const RInfo* r1, uint32_t 
 }
 
 __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, const RInfo* r0, const RInfo* r1,
-                                  uint32_t n, bool weighted, bool is_dual, int wc) {
+                                  uint32_t n, bool weighted, bool is_dual, bool multi, int wc) {
   const int lane = lane_id();
   const bool side1 = side == 0;
-  uint32_t known[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint8_t ins[kKout];
+  // wave-uniform key lists packed as bytes in two u64 (no private arrays)
+  uint64_t ins_lo = 0, ins_hi = 0;
   uint32_t nk = 0;
+  auto ins_at = [&](uint32_t j) { return j < 8 ? byte_at(ins_lo, j) : byte_at(ins_hi, j - 8); };
   for (uint32_t base = 0; base < n; base += 64) {
     const uint32_t r = base + lane;
     bool voter = r < n && ri[r].e != kInactive;
@@ -379,35 +504,55 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
       uint32_t cand = 0xFFFF;
       if (voter) {
         const RInfo& x = ri[r];
-        for (uint32_t k = 0; k < x.n; ++k) {
-          const uint8_t s = x.sym[k];
-          if (!((known[s >> 5] >> (s & 31)) & 1u)) {
-            cand = s;
-            break;
-          }
+        for (uint32_t k = 0; k < x.n && cand == 0xFFFF; ++k) {
+          const uint32_t s = x.sym[k];
+          uint32_t j = 0;
+          while (j < nk && ins_at(j) != s) ++j;
+          if (j == nk) cand = s;
         }
       }
       const uint64_t m = ballot(cand != 0xFFFF);
       if (!m) break;
       const int first = __ffsll((unsigned long long)m) - 1;
       const uint32_t s = (uint32_t)__shfl((int)cand, first, 64);
-      if (nk == kKout) return false;
-      ins[nk++] = (uint8_t)s;
-      known[s >> 5] |= 1u << (s & 31);
+      if (nk == (uint32_t)kKout) return false;
+      if (nk < 8) ins_lo |= (uint64_t)s << (8 * nk);
+      else ins_hi |= (uint64_t)s << (8 * (nk - 8));
+      nk++;
     }
   }
-  uint8_t ord[kKout];
-  fx_order(ins, nk, ord);
-  uint8_t keys[kKout];
+  const uint64_t ord = fx_order_packed(nk, ins_at);
+  // iteration-order keys with the wildcard removed (consensus.rs:556-561)
+  uint64_t k_lo = 0, k_hi = 0;
   uint32_t m = 0;
   const bool drop_wc = wc >= 0 && nk > 1;
   for (uint32_t k = 0; k < nk; ++k) {
-    const uint8_t s = ins[ord[k]];
-    if (drop_wc && s == (uint8_t)wc) continue;
-    keys[m++] = s;
+    const uint32_t s = ins_at(nib(ord, k));
+    if (drop_wc && s == (uint32_t)(uint8_t)wc) continue;
+    if (m < 8) k_lo |= (uint64_t)s << (8 * m);
+    else k_hi |= (uint64_t)s << (8 * (m - 8));
+    m++;
   }
-  if ((uint32_t)lane < m) {
-    const uint8_t key = keys[lane];
+  auto key_at = [&](uint32_t j) { return j < 8 ? byte_at(k_lo, j) : byte_at(k_hi, j - 8); };
+  if (!weighted && !multi) {
+    // every voter has exactly one distinct symbol: contribution 1.0 each, so
+    // the ordered f64 sum is an exact integer count; lane j keeps key j's count
+    uint32_t c = 0;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t r = base + lane;
+      const bool voter = r < n && ri[r].e != kInactive && ri[r].n == 1;
+      const uint32_t s = voter ? ri[r].sym[0] : 0xFFFF;
+      for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t pc = (uint32_t)__popcll((unsigned long long)ballot(s == key_at(k)));
+        if (k == (uint32_t)lane) c += pc;
+      }
+    }
+    if ((uint32_t)lane < m) {
+      ctl.keys[side][lane] = (uint8_t)key_at(lane);
+      ctl.vals[side][lane] = (double)c;
+    }
+  } else if ((uint32_t)lane < m) {
+    const uint32_t key = key_at(lane);
     double acc = 0.0;
     for (uint32_t r = 0; r < n; ++r) {
       const RInfo& x = ri[r];
@@ -454,10 +599,33 @@ __device__ inline void store_record(Eng& E, Ctl& ctl, uint8_t* outp, uint32_t sl
   }
 }
 
+__device__ inline void trace_pop(const EngineArgs& A, uint32_t prob, const HeapEntry& top, uint32_t flags,
+                                 uint32_t extra) {
+  if (!A.trace || prob != 0) return;
+  const uint32_t k = A.trace[0];
+  if (k >= A.trace_cap) return;
+  uint32_t* rec = A.trace + 4 + 4 * k;
+  rec[0] = (uint32_t)top.cost;
+  rec[1] = top.len;
+  rec[2] = flags;
+  rec[3] = extra;
+  A.trace[0] = k + 1;
+}
+
+__device__ inline void finish_problem(const EngineArgs& A, Ctl& ctl, uint8_t* outp, uint32_t prob) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
+    A.status[prob] = ctl.status;
+    for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)prob * S_NSTAT + s] = ctl.cnt[s];
+  }
+  __syncthreads();
+}
+
 // =====================================================================
 // ConsensusDWFA engine (consensus.rs:139-351)
 // =====================================================================
-__global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) single_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl;
   const int tid = threadIdx.x;
@@ -480,6 +648,7 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
       // ---- pop (consensus.rs:224-251) ----
       if (tid == 0) {
         TrackerRef t = E.tracker(ctl, 0);
+        ctl.cache_hit = 0;
         if (ctl.heap_n == 0) {
           ctl.action = 2;
         } else {
@@ -505,9 +674,18 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
             ctl.last_constraint[0]++;
             if (!t.process(top.len)) ctl.status = 4;  // "Capacity is full"
             ctl.action = 0;
+            ctl.cache_hit = top.slot == ctl.cache_slot;
           }
+          trace_pop(A, prob, top, ctl.action << 1, 0);
         }
-        ctl.n_end[0] = 0;
+        if (ctl.cache_hit) {
+          ctl.n_end[0] = ctl.cache_nend;
+          ctl.multi[0] = ctl.cache_multi;
+        } else {
+          ctl.n_end[0] = 0;
+          ctl.multi[0] = 0;
+        }
+        ctl.cache_slot = kNoSlot;
         ctl.ovf = 0;
       }
       __syncthreads();
@@ -517,10 +695,7 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
 
       const uint32_t top = ctl.top_slot;
       const uint32_t len = ctl.top_len;
-      SideView tv = E.sv(top, 0);
-
-      analyze_side(E, ctl, top, 0, len, E.L.rinfo);
-      __syncthreads();
+      if (!ctl.cache_hit) analyze_side(E, ctl, top, 0, len, E.L.rinfo);
       if (tid == 0) {
         const uint32_t ne = ctl.n_end[0];
         ctl.reached = early ? (ne == E.n) : (ne > 0);  // consensus.rs:516-532
@@ -570,7 +745,8 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
 
       // ---- votes + child selection (consensus.rs:283-321) ----
       if (wave_id() == 0) {
-        const bool ok = wave_votes(ctl, 0, E.L.rinfo, E.L.rinfo, E.L.rinfo, E.n, false, false, cfg.wildcard);
+        const bool ok =
+            wave_votes(ctl, 0, E.L.rinfo, E.L.rinfo, E.L.rinfo, E.n, false, false, ctl.multi[0] != 0, cfg.wildcard);
         if (lane == 0) {
           if (!ok) {
             ctl.status = WC_E_LIMIT_CODE;
@@ -617,23 +793,19 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
           }
           ctl.cur_slot = slot;
           ctl.cost_acc = 0;
-          ctl.ovf = 0;
+          ctl.n_end[0] = 0;
+          ctl.multi[0] = 0;
         }
         __syncthreads();
         if (ctl.status != ST_OK) break;
         const uint32_t slot = ctl.cur_slot;
-        if (slot != top) {
-          const uint32_t lens[2] = {len, 0};
-          copy_node(E, top, slot, 1, lens);
-        }
+        if (slot != top) copy_side(E, top, 0, slot, 0, len);
         if (tid == 0) E.sv(slot, 0).con[len] = (uint8_t)ctl.ch_s[c][0];
         __syncthreads();
-        WaveCounters cnt = {0, 0, 0, 0, 0};
-        push_sides(E, ctl, slot, ctl.ch_s[c][0], -1, len + 1, 0, true, cnt);
-        flush_counters(ctl, cnt);
-        __syncthreads();
+        push_sides(E, ctl, slot, ctl.ch_s[c][0], -1, len + 1, 0, true, E.L.rinfo);
         if (tid == 0) {
           if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
+          else if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
           ctl.ch_cost[c] = ctl.cost_acc;
           ctl.ch_slot[c] = slot;
           E.L.meta[slot].len[0] = len + 1;
@@ -648,24 +820,21 @@ __global__ void __launch_bounds__(kBlock) single_engine_kernel(EngineArgs A) {
           t.insert(len + 1);
           heap_push(E.L.heap, ctl.heap_n, HeapEntry{ctl.ch_cost[c], len + 1, ctl.ch_slot[c]});
         }
+        // the last child's nominations are in LDS: reuse them if it is popped next
+        ctl.cache_slot = ctl.ch_slot[nc - 1];
+        ctl.cache_nend = ctl.n_end[0];
+        ctl.cache_multi = ctl.multi[0];
       }
       __syncthreads();
     }
-
-    __syncthreads();
-    if (tid == 0) {
-      ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
-      A.status[prob] = ctl.status;
-      for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)prob * S_NSTAT + s] = ctl.cnt[s];
-    }
-    __syncthreads();
+    finish_problem(A, ctl, outp, prob);
   }
 }
 
 // =====================================================================
 // DualConsensusDWFA engine (dual_consensus.rs:240-787)
 // =====================================================================
-__global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl;
   const int tid = threadIdx.x;
@@ -727,19 +896,10 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
             ctl.cnt[S_EXPLORED]++;
             ctl.action = 0;
           }
-          if (A.trace && prob == 0) {
-            uint32_t k = A.trace[0];
-            if (k < A.trace_cap) {
-              uint32_t* rec = A.trace + 4 + 4 * k;
-              rec[0] = (uint32_t)top.cost;
-              rec[1] = top.len;
-              rec[2] = dual | (ctl.action << 1) | (m.nsome[0] << 8) | (m.nsome[1] << 20);
-              rec[3] = (uint32_t)am;
-              A.trace[0] = k + 1;
-            }
-          }
+          trace_pop(A, prob, top, dual | (ctl.action << 1) | (m.nsome[0] << 8) | (m.nsome[1] << 20), (uint32_t)am);
         }
         ctl.n_end[0] = ctl.n_end[1] = 0;
+        ctl.multi[0] = ctl.multi[1] = 0;
         ctl.n_either = 0;
         ctl.ovf = 0;
       }
@@ -756,7 +916,6 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
 
       analyze_side(E, ctl, top, 0, tlens[0], R0);
       if (tdual) analyze_side(E, ctl, top, 1, tlens[1], R1);
-      __syncthreads();
       // reached_all_end (dual_consensus.rs:1174-1195): per read, either side at its end
       for (uint32_t r = tid; r < E.n; r += kBlock) {
         const bool v = (R0[r].e != kInactive && R0[r].end) || (tdual && R1[r].e != kInactive && R1[r].end);
@@ -838,14 +997,15 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
       // ---- votes on both sides (waves 0 and 1 in parallel) ----
       if (wave_id() < (tdual ? 2 : 1)) {
         const uint32_t side = wave_id();
-        const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, E.n, weighted, tdual, cfg.wildcard);
+        const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, E.n, weighted, tdual,
+                                   ctl.multi[side] != 0, cfg.wildcard);
         if (!ok && lane == 0) atomicOr(&ctl.ovf, 1u);
       }
       __syncthreads();
       if (tid == 0) {
         if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
-        double thr[2];
-        uint64_t mc[2];
+        double thr[2] = {0.0, 0.0};
+        uint64_t mc[2] = {0, 0};
         for (uint32_t s = 0; s < (tdual ? 2u : 1u); ++s) {
           double sum = -0.0, mx = 0.0;
           bool have = false;
@@ -862,9 +1022,10 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
         bool overflow = false;
         if (tdual) {
           // dual_consensus.rs:554-650: options per side, None first
-          int16_t o[2][kKout + 1];
+          auto& o = ctl.opt;
           uint32_t no[2] = {0, 0};
           const bool lock[2] = {(tm.flags & 2u) != 0, (tm.flags & 4u) != 0};
+#pragma unroll
           for (int s = 0; s < 2; ++s) {
             if (ctl.fin[s] || ctl.nkeys[s] == 0 || lock[s]) o[s][no[s]++] = -1;
             if (!lock[s])
@@ -893,13 +1054,13 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
             nc++;
           }
           // split children from every pair of sorted candidates (:682-734)
-          double cv[kKout];
-          uint8_t cs[kKout];
+          double* cv = ctl.srt_v;
+          uint8_t* cs = ctl.srt_s;
           uint32_t ns = 0, passing = 0;
           for (uint32_t k = 0; k < ctl.nkeys[0]; ++k) {
             if (cfg.wildcard >= 0 && ctl.keys[0][k] == (uint8_t)cfg.wildcard) continue;
             if (ctl.vals[0][k] >= (double)mc[0]) passing++;
-            // insertion sort by (Reverse(count), symbol), stable
+            // stable insertion sort by (Reverse(count), symbol)
             uint32_t p = ns;
             while (p > 0 && (cv[p - 1] < ctl.vals[0][k] || (cv[p - 1] == ctl.vals[0][k] && cs[p - 1] > ctl.keys[0][k]))) {
               cv[p] = cv[p - 1];
@@ -951,31 +1112,19 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
           ctl.cur_slot = slot;
           ctl.cost_acc = 0;
           ctl.some_acc[0] = ctl.some_acc[1] = 0;
-          ctl.ovf = 0;
         }
         __syncthreads();
         if (ctl.status != ST_OK) break;
         const uint32_t slot = ctl.cur_slot;
         const uint8_t kind = ctl.ch_kind[c];
         const int s0 = ctl.ch_s[c][0], s1 = ctl.ch_s[c][1];
-        if (slot != top) copy_node(E, top, slot, tdual ? 2 : 1, tlens);
-        __syncthreads();
-        if (kind == 2) {
-          // activate_dual (dual_consensus.rs:957-976): side 2 := side 1
-          SideView a = E.sv(slot, 0), b = E.sv(slot, 1);
-          for (uint32_t i = tid; i < tlens[0]; i += kBlock) b.con[i] = a.con[i];
-          for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
-            const uint32_t e = a.e[r];
-            if (lane == 0) {
-              b.e[r] = e;
-              b.off[r] = a.off[r];
-            }
-            if (e == kInactive) continue;
-            const uint32_t W = 2 * e + 1;
-            for (uint32_t i = lane; i < W; i += 64) b.wf[(uint64_t)r * E.wcap + i] = a.wf[(uint64_t)r * E.wcap + i];
-          }
+        if (slot != top) {
+          copy_side(E, top, 0, slot, 0, tlens[0]);
+          if (tdual) copy_side(E, top, 1, slot, 1, tlens[1]);
+          __syncthreads();
         }
-        uint32_t nl[2];
+        // activate_dual (dual_consensus.rs:957-976): side 2 := side 1
+        if (kind == 2) copy_side(E, slot, 0, slot, 1, tlens[0]);
         if (tid == 0) {
           SlotMeta m = tm;
           if (kind == 2) {
@@ -983,6 +1132,7 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
             m.len[1] = m.len[0];
             m.nsome[1] = m.nsome[0];
           }
+#pragma unroll
           for (int s = 0; s < 2; ++s) {
             const int sym = s == 0 ? s0 : s1;
             if (sym >= 0) {
@@ -995,12 +1145,8 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
           E.L.meta[slot] = m;
         }
         __syncthreads();
-        nl[0] = E.L.meta[slot].len[0];
-        nl[1] = E.L.meta[slot].len[1];
-        WaveCounters cnt = {0, 0, 0, 0, 0};
-        push_sides(E, ctl, slot, s0, s1, nl[0], nl[1], false, cnt);
-        flush_counters(ctl, cnt);
-        __syncthreads();
+        const uint32_t nl0 = E.L.meta[slot].len[0], nl1 = E.L.meta[slot].len[1];
+        push_sides(E, ctl, slot, s0, s1, nl0, nl1, false, nullptr);
         // prune (dual_consensus.rs:1030-1045) + priority (:1092-1168)
         const bool cdual = (E.L.meta[slot].flags & 1u) != 0;
         {
@@ -1008,13 +1154,13 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
           uint64_t cost = 0;
           uint32_t n0 = 0, n1 = 0;
           for (uint32_t r = tid; r < E.n; r += kBlock) {
-            uint32_t e1 = a.e[r], e2 = cdual ? b.e[r] : kInactive;
+            uint32_t e1 = a.rs[r].e, e2 = cdual ? b.rs[r].e : kInactive;
             if (cdual && e1 != kInactive && e2 != kInactive) {
               if ((uint64_t)e1 + cfg.dual_max_ed_delta < (uint64_t)e2) {
-                b.e[r] = kInactive;
+                b.rs[r].e = kInactive;
                 e2 = kInactive;
               } else if ((uint64_t)e2 + cfg.dual_max_ed_delta < (uint64_t)e1) {
-                a.e[r] = kInactive;
+                a.rs[r].e = kInactive;
                 e1 = kInactive;
               }
             }
@@ -1032,6 +1178,7 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
         __syncthreads();
         if (tid == 0) {
           if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
+          else if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
           SlotMeta& m = E.L.meta[slot];
           m.nsome[0] = ctl.some_acc[0];
           m.nsome[1] = ctl.some_acc[1];
@@ -1052,14 +1199,7 @@ __global__ void __launch_bounds__(kBlock) dual_engine_kernel(EngineArgs A) {
       }
       __syncthreads();
     }
-
-    __syncthreads();
-    if (tid == 0) {
-      ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
-      A.status[prob] = ctl.status;
-      for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)prob * S_NSTAT + s] = ctl.cnt[s];
-    }
-    __syncthreads();
+    finish_problem(A, ctl, outp, prob);
   }
 }
 

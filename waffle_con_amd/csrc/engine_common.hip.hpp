@@ -33,75 +33,92 @@ __device__ __forceinline__ uint64_t cost_of(uint32_t e, int mode) {
 }
 
 // --- FxHashMap<u8,_> iteration order (oracle rust_compat.hpp) ---
-// Given distinct keys in insertion order, produce the bucket-ascending order.
-// Supports up to 16 keys (tables of 4, 8, 16 or 32 buckets).
+// hashbrown with FxHasher over u8 keys: the table (4, 8 or 16 buckets for up
+// to 14 keys) is kept in one u64 of 4-bit bucket tags (key index + 1), so no
+// private array (and no scratch memory) is needed. Insertion is the first
+// empty bucket cyclically from h1 = (k * FxSEED) & (B - 1); growth rebuilds in
+// ascending bucket order; iteration is ascending bucket order.
 __device__ inline uint32_t fx_cap(uint32_t b) { return b == 0 ? 0 : (b < 8 ? b - 1 : b / 8 * 7); }
-__device__ inline uint32_t fx_buckets_for(uint32_t cap) {
-  if (cap < 8) return cap < 4 ? 4 : 8;
-  uint32_t adj = cap * 8 / 7, p = 1;
-  while (p < adj) p <<= 1;
-  return p;
-}
-__device__ inline uint32_t fx_slot(const int16_t* tab, uint32_t B, uint8_t k) {
-  uint64_t h = (uint64_t)k * 0x517cc1b727220a95ULL;
-  uint32_t mask = B - 1, pos = (uint32_t)h & mask;
-  if (B < 16) {
-    for (uint32_t i = pos; i < B; ++i)
-      if (tab[i] < 0) return i;
-    for (uint32_t i = 0; i < B; ++i)
-      if (tab[i] < 0) return i;
-    return 0;
+__device__ inline uint32_t fx_buckets_for(uint32_t cap) { return cap < 4 ? 4 : (cap < 8 ? 8 : 16); }
+__device__ inline uint64_t fx_put(uint64_t T, uint32_t B, uint32_t key, uint32_t tag) {
+  const uint64_t h = (uint64_t)(key & 0xFF) * 0x517cc1b727220a95ULL;
+  uint32_t pos = (uint32_t)h & (B - 1);
+  for (uint32_t t = 0; t < B; ++t) {
+    const uint32_t b = (pos + t) & (B - 1);
+    if (((T >> (4 * b)) & 15ull) == 0) return T | ((uint64_t)tag << (4 * b));
   }
-  uint32_t stride = 0;
-  for (;;) {
-    for (uint32_t j = 0; j < 16; ++j)
-      if (tab[(pos + j) & mask] < 0) return (pos + j) & mask;
-    stride += 16;
-    pos = (pos + stride) & mask;
-  }
+  return T;
 }
-// keys[0..n) distinct in insertion order -> out[0..n) iteration order (indices into keys)
-__device__ inline void fx_order(const uint8_t* keys, uint32_t n, uint8_t* out) {
-  int16_t tab[32];
+// keys: key(k) for k in [0, n) distinct, in insertion order (n <= 14).
+// Returns the iteration order as 4-bit key indices (nibble m = m-th key).
+template <class KeyFn>
+__device__ inline uint64_t fx_order_packed(uint32_t n, KeyFn key) {
+  uint64_t T = 0;
   uint32_t B = 0, items = 0, growth = 0;
   for (uint32_t k = 0; k < n; ++k) {
     if (growth == 0) {
-      uint32_t want = max(items + 1, fx_cap(B) + 1);
-      uint32_t nb = fx_buckets_for(want);
-      int16_t old[32];
-      for (uint32_t i = 0; i < B; ++i) old[i] = tab[i];
-      for (uint32_t i = 0; i < nb; ++i) tab[i] = -1;
-      for (uint32_t i = 0; i < B; ++i)
-        if (old[i] >= 0) tab[fx_slot(tab, nb, keys[old[i]])] = old[i];
+      const uint32_t nb = fx_buckets_for(max(items + 1, fx_cap(B) + 1));
+      const uint64_t old = T;
+      T = 0;
+      for (uint32_t b = 0; b < B; ++b) {
+        const uint32_t v = (uint32_t)(old >> (4 * b)) & 15u;
+        if (v) T = fx_put(T, nb, key(v - 1), v);
+      }
       B = nb;
       growth = fx_cap(nb) - items;
     }
-    tab[fx_slot(tab, B, keys[k])] = (int16_t)k;
+    T = fx_put(T, B, key(k), k + 1);
     items++;
     growth--;
   }
+  uint64_t out = 0;
   uint32_t m = 0;
-  for (uint32_t i = 0; i < B; ++i)
-    if (tab[i] >= 0) out[m++] = (uint8_t)tab[i];
+  for (uint32_t b = 0; b < B; ++b) {
+    const uint32_t v = (uint32_t)(T >> (4 * b)) & 15u;
+    if (v) {
+      out |= (uint64_t)(v - 1) << (4 * m);
+      m++;
+    }
+  }
+  return out;
 }
+__device__ __forceinline__ uint32_t nib(uint64_t x, uint32_t i) { return (uint32_t)(x >> (4 * i)) & 15u; }
+__device__ __forceinline__ uint32_t byte_at(uint64_t x, uint32_t i) { return (uint32_t)(x >> (8 * i)) & 0xFFu; }
 
 // --- per-read DWFA views ---
 struct SideView {
-  uint32_t* e;    // [nmax]
-  uint32_t* off;  // [nmax]
-  uint32_t* wf;   // [nmax * wcap]
-  uint8_t* con;   // [lcap]
+  RState* rs;    // [nmax]
+  uint32_t* wf;  // [nmax * wcap]
+  uint8_t* con;  // [lcap]
 };
 
 __device__ inline SideView side_view(uint8_t* slot_base, uint32_t side, uint32_t nmax, uint32_t wcap, uint32_t lcap) {
   uint8_t* b = slot_base + (uint64_t)side * side_bytes(nmax, wcap, lcap);
   SideView v;
-  v.e = (uint32_t*)b;
-  v.off = v.e + nmax;
-  v.wf = v.off + nmax;
-  v.con = b + align16((uint64_t)nmax * 8 + (uint64_t)nmax * wcap * 4);
+  v.rs = (RState*)b;
+  v.wf = (uint32_t*)(b + (uint64_t)nmax * sizeof(RState));
+  v.con = b + align16((uint64_t)nmax * sizeof(RState) + (uint64_t)nmax * wcap * 4);
   return v;
 }
+
+// A 64-byte RState moves as four 16-byte accesses held in named registers
+// (word 3 = nscmp | nf << 16 | flags << 24; words 4-7 = fi pairs; 8-15 = fd).
+struct RRaw {
+  uint4 a, b, c, d;
+};
+__device__ __forceinline__ RRaw rstate_load(const RState* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  return RRaw{q[0], q[1], q[2], q[3]};
+}
+__device__ __forceinline__ void rstate_store(RState* p, const RRaw& s) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = s.a;
+  q[1] = s.b;
+  q[2] = s.c;
+  q[3] = s.d;
+}
+__device__ __forceinline__ uint32_t rraw_e(const RRaw& s) { return s.a.x; }
+__device__ __forceinline__ uint32_t rraw_flags(const RRaw& s) { return s.a.w >> 24; }
 
 struct WaveCounters {
   uint32_t updates, w_out, compares, edinc, finalizes;
@@ -268,25 +285,25 @@ __device__ inline bool wave_finalize_read(const uint32_t* wf, uint32_t e, uint32
 }
 
 // Tip nomination of one read (dynamic_wfa.rs:241-255) plus reached_baseline_end
-// (:232-234). Distinct symbols are found in first-appearance order (ascending
-// diagonal), then permuted into FxHashMap iteration order. Returns false when
-// more than kKmax distinct symbols sit at the tips.
+// (:232-234), one wave over the full wavefront. Distinct symbols are found in
+// first-appearance order (ascending diagonal), then permuted into FxHashMap
+// iteration order. Keys/counts are wave-uniform packed registers. Returns
+// false when more than kKmax distinct symbols sit at the tips.
 __device__ inline bool wave_analyze_read(const uint32_t* wf, uint32_t e, uint32_t off, const uint8_t* rd,
                                          uint32_t blen, uint32_t olen, RInfo* out) {
   const int lane = lane_id();
   const uint32_t W = 2 * e + 1;
-  uint8_t keys[kKmax];
-  uint32_t cnts[kKmax];
+  uint64_t keys = 0, cnt_lo = 0, cnt_hi = 0;  // 8 keys (bytes), 8 x 16-bit counts
   uint32_t nk = 0;
   uint32_t mb = 0;
   bool ok = true;
   for (uint32_t base = 0; base < W; base += 64) {
-    uint32_t i = base + lane;
+    const uint32_t i = base + lane;
     bool tip = false;
     uint32_t s = 0;
     if (i < W) {
-      uint32_t d = wf[i];
-      uint32_t bo = d + e - i;
+      const uint32_t d = wf[i];
+      const uint32_t bo = d + e - i;
       mb = max(mb, bo);
       if (d + off == olen && bo < blen) {
         tip = true;
@@ -295,33 +312,35 @@ __device__ inline bool wave_analyze_read(const uint32_t* wf, uint32_t e, uint32_
     }
     uint64_t m = ballot(tip);
     while (m) {
-      int first = __ffsll((unsigned long long)m) - 1;
-      uint32_t sym = (uint32_t)__shfl((int)s, first, 64);
-      uint64_t ms = ballot(tip && s == sym);
+      const int first = __ffsll((unsigned long long)m) - 1;
+      const uint32_t sym = (uint32_t)__shfl((int)s, first, 64);
+      const uint64_t ms = ballot(tip && s == sym);
       uint32_t k = 0;
-      while (k < nk && keys[k] != (uint8_t)sym) ++k;
+      while (k < nk && byte_at(keys, k) != sym) ++k;
       if (k == nk) {
-        if (nk == kKmax) {
+        if (nk == (uint32_t)kKmax) {
           ok = false;
           break;
         }
-        keys[nk] = (uint8_t)sym;
-        cnts[nk] = 0;
+        keys |= (uint64_t)sym << (8 * nk);
         nk++;
       }
-      cnts[k] += (uint32_t)__popcll((unsigned long long)ms);
+      const uint64_t add = (uint64_t)__popcll((unsigned long long)ms);
+      if (k < 4) cnt_lo += add << (16 * k);
+      else cnt_hi += add << (16 * (k - 4));
       m &= ~ms;
     }
   }
   mb = wave_max_u32(mb);
   if (lane == 0) {
-    uint8_t ord[kKmax];
-    fx_order(keys, nk, ord);
+    const uint64_t ord = fx_order_packed(nk, [&](uint32_t j) { return byte_at(keys, j); });
     uint32_t split = 0;
     for (uint32_t k = 0; k < nk; ++k) {
-      out->sym[k] = keys[ord[k]];
-      out->occ[k] = (uint16_t)cnts[ord[k]];
-      split += cnts[ord[k]];
+      const uint32_t j = nib(ord, k);
+      const uint32_t c = (uint32_t)((j < 4 ? cnt_lo >> (16 * j) : cnt_hi >> (16 * (j - 4))) & 0xFFFFu);
+      out->sym[k] = (uint8_t)byte_at(keys, j);
+      out->occ[k] = (uint16_t)c;
+      split += c;
     }
     out->n = (uint8_t)nk;
     out->split = (uint16_t)split;
@@ -329,6 +348,219 @@ __device__ inline bool wave_analyze_read(const uint32_t* wf, uint32_t e, uint32_
     out->e = e;
   }
   return ok;
+}
+
+// =====================================================================
+// Frontier-cache (RState) operations. A push of one symbol only moves
+// frontier diagonals, so the common case is one thread per read touching
+// its 64-byte RState plus a few read bytes; the full wavefront is revisited
+// (one wave, lanes over diagonals) only when the edit distance must grow.
+// =====================================================================
+
+// Per-read frontier in registers: entries k < kF with a keep mask (order =
+// ascending diagonal index). Only static indices are used on it.
+struct Front {
+  uint32_t e, off, maxb, nscmp, mask;
+  uint32_t fi[kF], fd[kF];
+};
+__device__ __forceinline__ void front_load(const RRaw& s, Front& f) {
+  f.e = s.a.x;
+  f.off = s.a.y;
+  f.maxb = s.a.z;
+  f.nscmp = s.a.w & 0xFFFFu;
+  f.mask = (1u << ((s.a.w >> 16) & 0xFFu)) - 1u;
+  f.fi[0] = s.b.x & 0xFFFFu;
+  f.fi[1] = s.b.x >> 16;
+  f.fi[2] = s.b.y & 0xFFFFu;
+  f.fi[3] = s.b.y >> 16;
+  f.fi[4] = s.b.z & 0xFFFFu;
+  f.fi[5] = s.b.z >> 16;
+  f.fi[6] = s.b.w & 0xFFFFu;
+  f.fi[7] = s.b.w >> 16;
+  f.fd[0] = s.c.x;
+  f.fd[1] = s.c.y;
+  f.fd[2] = s.c.z;
+  f.fd[3] = s.c.w;
+  f.fd[4] = s.d.x;
+  f.fd[5] = s.d.y;
+  f.fd[6] = s.d.z;
+  f.fd[7] = s.d.w;
+}
+// write the compacted frontier back (memory stores at computed positions)
+__device__ __forceinline__ void front_store(RState* p, const Front& f) {
+  uint32_t n = 0;
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    if (f.mask & (1u << k)) {
+      p->fi[n] = (uint16_t)f.fi[k];
+      p->fd[n] = f.fd[k];
+      n++;
+    }
+  }
+  p->e = f.e;
+  p->off = f.off;
+  p->maxb = f.maxb;
+  p->nscmp = (uint16_t)f.nscmp;
+  p->nf = (uint8_t)n;
+  p->flags = 0;
+}
+
+// Nomination + end flag of one read from its frontier (thread-level),
+// dynamic_wfa.rs:232-234 and :241-255. `multi` = more than one distinct symbol.
+__device__ inline void thread_analyze(const Front& f, const uint8_t* rd, uint32_t blen, uint32_t len, RInfo* out,
+                                      bool& multi) {
+  uint32_t mb = f.maxb;
+  uint32_t tipsym[kF];
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    tipsym[k] = 0x100;
+    if (f.mask & (1u << k)) {
+      const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+      mb = max(mb, bo);
+      if (f.fd[k] + f.off == len && bo < blen) tipsym[k] = rd[bo];
+    }
+  }
+  uint64_t keys = 0;
+  uint32_t cnts = 0, nk = 0;  // counts: 4-bit nibbles (<= kF tips)
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    const uint32_t s = tipsym[k];
+    if (s == 0x100) continue;
+    uint32_t j = 0;
+    while (j < nk && byte_at(keys, j) != s) ++j;
+    if (j == nk) {
+      keys |= (uint64_t)s << (8 * nk);
+      nk++;
+    }
+    cnts += 1u << (4 * j);
+  }
+  const uint64_t ord = nk > 1 ? fx_order_packed(nk, [&](uint32_t j) { return byte_at(keys, j); }) : 0ull;
+  uint32_t split = 0;
+  for (uint32_t k = 0; k < nk; ++k) {
+    const uint32_t j = nib(ord, k);
+    const uint32_t c = (cnts >> (4 * j)) & 15u;
+    out->sym[k] = (uint8_t)byte_at(keys, j);
+    out->occ[k] = (uint16_t)c;
+    split += c;
+  }
+  out->n = (uint8_t)nk;
+  out->split = (uint16_t)split;
+  out->end = (mb == blen);
+  out->e = f.e;
+  multi = nk > 1;
+}
+
+// The extend step of DWFALite::update for one appended symbol on the frontier
+// (thread-level). Tips (d + off == old length) compare once and either advance
+// by one or become stuck; everything else is unchanged. Returns true when the
+// read needs the wave path: the ED-increase loop (dynamic_wfa.rs:84-91).
+// `cmp` receives the compares the reference extend makes.
+__device__ inline bool thread_push(Front& f, const uint8_t* rd, uint32_t blen, uint32_t old_len, uint8_t sym, int wc,
+                                   bool early, uint32_t* wf_row, uint32_t& cmp) {
+  uint32_t x[kF];
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    x[k] = 0x100;
+    if (f.mask & (1u << k)) {
+      const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+      if (f.fd[k] + f.off == old_len && bo < blen) x[k] = rd[bo];
+    }
+  }
+  uint32_t c = f.nscmp;
+  uint32_t mb = 0;
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    if (!(f.mask & (1u << k))) continue;
+    const uint32_t d = f.fd[k];
+    const uint32_t bo = d + f.e - f.fi[k];
+    if (d + f.off == old_len) {
+      if (bo < blen) {
+        c++;
+        if (x[k] == sym || (wc >= 0 && x[k] == (uint32_t)(uint8_t)wc)) {
+          f.fd[k] = d + 1;
+          wf_row[f.fi[k]] = d + 1;
+          mb = max(mb, bo + 1);
+          continue;
+        }
+        f.nscmp++;  // stuck on a mismatch: compared (and failing) on every later push
+      }
+      f.maxb = max(f.maxb, bo);
+      f.mask &= ~(1u << k);
+    } else {
+      mb = max(mb, bo);
+    }
+  }
+  mb = max(mb, f.maxb);
+  cmp = c;
+  return f.mask == 0 && !(early && mb == blen);
+}
+
+// Rebuild an RState from the authoritative wavefront (one wave).
+__device__ inline void wave_rebuild(const uint32_t* wf, uint32_t e, uint32_t off, uint32_t blen, uint32_t len,
+                                    RState* out) {
+  const int lane = lane_id();
+  const uint32_t W = 2 * e + 1;
+  uint32_t nf = 0, mb = 0, nsc = 0;
+  for (uint32_t base = 0; base < W; base += 64) {
+    const uint32_t i = base + lane;
+    const bool valid = i < W;
+    const uint32_t d = valid ? wf[i] : 0;
+    const uint32_t bo = d + e - i;
+    const bool inF = valid && d + off >= len;
+    const uint64_t m = ballot(inF);
+    const uint32_t pos = nf + (uint32_t)__popcll((unsigned long long)(m & ((1ull << lane) - 1ull)));
+    if (inF && pos < (uint32_t)kF) {
+      out->fi[pos] = (uint16_t)i;
+      out->fd[pos] = d;
+    }
+    nf += (uint32_t)__popcll((unsigned long long)m);
+    if (valid && !inF) {
+      mb = max(mb, bo);
+      nsc += bo < blen;
+    }
+  }
+  mb = wave_max_u32(mb);
+  nsc = wave_sum_u32(nsc);
+  if (lane == 0) {
+    out->e = e;
+    out->off = off;
+    out->maxb = mb;
+    out->nscmp = (uint16_t)min(nsc, 65535u);
+    out->nf = (uint8_t)min(nf, (uint32_t)kF);
+    out->flags = (nf > (uint32_t)kF || nsc > 65535u) ? kWide : 0;
+  }
+}
+
+// The wave part of a push for one read whose thread step returned true:
+// full-scan push for a wide frontier, otherwise the ED-increase loop from the
+// post-extend wavefront; then rebuild the RState. Returns false on wavefront
+// capacity overflow.
+__device__ inline bool wave_heavy(RState* rsp, uint32_t* wf, const uint8_t* rd, uint32_t blen, const uint8_t* con,
+                                  uint32_t olen, uint8_t sym, int wc, bool early, uint32_t wcap, WaveCounters& cnt,
+                                  uint32_t& e_out) {
+  const uint32_t flags = rsp->flags;
+  uint32_t e = rsp->e;
+  const uint32_t off = rsp->off;
+  if (flags & kWide) {
+    if (!wave_push_read(wf, e, off, rd, blen, con, olen, sym, wc, early, wcap, cnt)) return false;
+  } else {
+    uint32_t W = 2 * e + 1, mo, mb, cmp = 0;
+    do {
+      if (W + 2 > wcap) return false;
+      wave_grow(wf, W);
+      W += 2;
+      e += 1;
+      cnt.edinc++;
+      wave_extend_all(wf, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
+    } while (mo + off < olen && !(early && mb == blen));
+    cnt.updates++;
+    cnt.w_out += W;
+    cnt.compares += wave_sum_u32(cmp);
+  }
+  __builtin_amdgcn_wave_barrier();
+  wave_rebuild(wf, e, off, blen, olen, rsp);
+  e_out = e;
+  return true;
 }
 
 }  // namespace wc

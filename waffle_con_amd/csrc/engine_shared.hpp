@@ -8,7 +8,7 @@ namespace wc {
 constexpr int kBlock = 256;       // threads per engine workgroup (4 waves)
 constexpr int kWaves = kBlock / 64;
 constexpr int kKmax = 8;          // distinct symbols at one read's tips
-constexpr int kKout = 16;         // distinct symbols voted across a node side
+constexpr int kKout = 14;         // distinct symbols voted across a node side (16-bucket table)
 constexpr uint32_t kInactive = 0xFFFFFFFFu;  // Option<DWFALite>::None
 
 // per-problem status (device → host)
@@ -93,9 +93,27 @@ struct EngineArgs {
 // ---- byte layouts (host and device compute them identically) ----
 __host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
-// one node slot: per side: e[nmax] u32, off[nmax] u32, wf[nmax*wcap] u32, con[lcap]
+// Per-read DWFA state of one node side. The full wavefront (wf row, u32 per
+// diagonal) stays authoritative in HBM; RState caches what a push needs:
+// the frontier F = diagonals with d + off >= |consensus| (the only ones that
+// can move when a symbol is appended), plus summaries of the stuck rest.
+constexpr int kF = 8;
+constexpr uint8_t kWide = 1;  // frontier larger than kF: use the full-scan path
+struct RState {
+  uint32_t e;       // edit distance, kInactive = None
+  uint32_t off;     // DWFALite offset (activation)
+  uint32_t maxb;    // max baseline offset d+e-i over stuck diagonals
+  uint16_t nscmp;   // stuck diagonals with baseline offset < |read| (each push compares them once)
+  uint8_t nf;       // frontier size
+  uint8_t flags;    // kWide
+  uint16_t fi[kF];  // frontier diagonal indices, ascending
+  uint32_t fd[kF];  // frontier d values
+};
+static_assert(sizeof(RState) == 64, "RState must stay 64 bytes");
+
+// one node slot: per side: RState[nmax], wf[nmax*wcap] u32, con[lcap]
 __host__ __device__ inline uint64_t side_bytes(uint32_t nmax, uint32_t wcap, uint32_t lcap) {
-  return align16((uint64_t)nmax * 8 + (uint64_t)nmax * wcap * 4) + align16(lcap);
+  return align16((uint64_t)nmax * sizeof(RState) + (uint64_t)nmax * wcap * 4) + align16(lcap);
 }
 __host__ __device__ inline uint64_t slot_bytes(uint32_t sides, uint32_t nmax, uint32_t wcap, uint32_t lcap) {
   return sides * side_bytes(nmax, wcap, lcap);
@@ -136,12 +154,14 @@ struct RInfo {
   uint16_t occ[kKmax];
   uint32_t e;     // current edit distance (kInactive = None)
 };
+// LDS: heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] | heavy list[2*nmax] u32
 __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax) {
   uint64_t t = (uint64_t)pcap * sizeof(HeapEntry);
   t += align16((uint64_t)pcap * 4);
   t += (uint64_t)pcap * sizeof(SlotMeta);
   t += (uint64_t)sides * nmax * sizeof(RInfo);
   t += align16((uint64_t)sides * nmax * 4);
+  t += align16((uint64_t)2 * nmax * 4);
   return align16(t);
 }
 
