@@ -4,9 +4,15 @@ Workload (BASELINE.json configs[1], north-star throughput form): ConsensusDWFA
 over synthetic HiFi-like loci — generate_test(alphabet 4, 10 kb, 100 reads,
 0.5% error) with seed = locus id, min_count = 100/4 (consensus_bench.rs
 convention). One "step" = the whole batch of loci through the device-resident
-engine (one launch, inputs already resident in HBM is NOT assumed by the
-library: the per-step host->device copy of the reads is inside the step; the
-engine kernel time is reported separately via HIP events).
+engine: one engine launch over reads already resident in HBM (ResidentBatch,
+uploaded before the timed region), plus the read-back of the consensus
+records. The engine kernel time is measured separately with HIP events on the
+library's stream (kernel_ms_per_step) and drives the roofline figure.
+
+roofline.traffic is the HBM byte count per launch measured by the rocprofv3
+PMC passes committed under profiles/ (FETCH_SIZE and WRITE_SIZE in separate
+passes, FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 note); it is
+reported only when the recorded workload equals this run's.
 
 Multi-GPU: one process per GPU (torch.distributed.run); loci are sharded
 (weak scaling: every rank owns --loci loci), no collective on the data path.
@@ -34,7 +40,7 @@ def parse():
     ap.add_argument("--len", type=int, default=10000)
     ap.add_argument("--reads", type=int, default=100)
     ap.add_argument("--err", type=float, default=0.005)
-    ap.add_argument("--cpu-sample", type=int, default=32, help="loci timed on the CPU oracle (rank 0, N=1)")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="loci timed on the CPU oracle (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -57,6 +63,19 @@ def cpu_baseline(loci, min_count, threads):
     dt = time.perf_counter() - t0
     updates = sum(c["updates"] for _, c in outs)
     return dt, updates, outs
+
+
+def pmc_traffic(loci, reads, length, err):
+    """HBM bytes per engine launch from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f)
+    w = rec.get("workload", {})
+    if (w.get("loci_per_gpu"), w.get("reads"), w.get("len"), w.get("error_rate")) != (loci, reads, length, err):
+        return None
+    return rec.get("traffic_bytes_per_launch")
 
 
 def main():
@@ -154,7 +173,7 @@ def main():
                    "loci_per_gpu": a.loci, "reads": a.reads, "len": a.len, "error_rate": a.err,
                    "parallelism": "loci-sharded x%d (no collective)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(a.loci, a.reads, a.len, a.err),
                      "kernel": "wc::single_engine_kernel",
                      "algorithmic_bytes_per_launch": per_launch_bytes},
         "gen_s": gen_s,

@@ -57,6 +57,8 @@ struct Ctl {
   uint32_t n_ret;
   int32_t store_idx;
   uint32_t cache_slot, cache_hit, cache_nend, cache_multi;
+  uint32_t hot_slot;  // slot whose RStates are held in Lds::hot (authoritative), kNoSlot = none
+  uint32_t hot_prev, hot_load;
   uint32_t nkeys[2];
   uint8_t keys[2][kKout];
   double vals[2][kKout];
@@ -72,9 +74,31 @@ struct Ctl {
   uint32_t ch_len[kMaxChild];
   uint32_t cur_slot;
   uint64_t cnt[S_NSTAT];
+#ifdef WC_PHASE_PROF
+  uint64_t ph[kPhases];
+  uint64_t ph_t;
+#endif
 };
 
+// Phase timing (debug builds with -DWC_PHASE_PROF, read out via WC_PHASES):
+// thread 0 charges the shader cycles since the previous mark to phase k.
+#ifdef WC_PHASE_PROF
+#define PH_MARK(k)                                             \
+  do {                                                         \
+    if (threadIdx.x == 0) {                                    \
+      const uint64_t _t = __builtin_amdgcn_s_memtime();        \
+      ctl.ph[(k)] += _t - ctl.ph_t;                            \
+      ctl.ph_t = _t;                                           \
+    }                                                          \
+  } while (0)
+#else
+#define PH_MARK(k) \
+  do {             \
+  } while (0)
+#endif
+
 struct Lds {
+  RState* hot;     // [sides][nmax] RStates of the node being expanded (single engine)
   HeapEntry* heap;
   uint32_t* freestack;
   SlotMeta* meta;
@@ -86,6 +110,8 @@ struct Lds {
 __device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32_t nmax) {
   Lds l;
   uint8_t* p = smem;
+  l.hot = (RState*)p;
+  p += (uint64_t)hot_sides(sides) * nmax * sizeof(RState);
   l.heap = (HeapEntry*)p;
   p += (uint64_t)pcap * sizeof(HeapEntry);
   l.freestack = (uint32_t*)p;
@@ -199,6 +225,11 @@ __device__ inline void flush_thread_counters(Ctl& ctl, WaveCounters c) {
   flush_counters(ctl, c);
 }
 
+// A value read from LDS that is the same for the whole workgroup: moving it
+// to a scalar register lets loops, branches and addresses stay scalar.
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
 // per-workgroup engine context (registers)
 struct Eng {
   const EngineArgs* A;
@@ -263,7 +294,13 @@ __device__ inline void init_problem(Eng& E, Ctl& ctl) {
     ctl.n_ret = 0;
     ctl.am_len = 1;
     ctl.cache_slot = kNoSlot;
+    ctl.hot_slot = kNoSlot;
+    ctl.hot_load = 0;
     for (int s = 0; s < S_NSTAT; ++s) ctl.cnt[s] = 0;
+#ifdef WC_PHASE_PROF
+    for (int k = 0; k < kPhases; ++k) ctl.ph[k] = 0;
+    ctl.ph_t = __builtin_amdgcn_s_memtime();
+#endif
   }
   for (uint32_t i = tid; i < E.pcap; i += kBlock) E.L.freestack[i] = E.pcap - 1 - i;
   for (uint32_t i = tid; i < 4 * (E.lcap + 2); i += kBlock) E.trk[i] = 0;
@@ -294,14 +331,24 @@ __device__ inline void init_problem(Eng& E, Ctl& ctl) {
 // ---- ANALYZE one node side (block-level, contains barriers) ----
 // Thread per read from the RState; reads with a wide frontier are nominated by
 // a wave over their full wavefront. Counts n_end / multi of the side.
+// Where a node's per-read RStates live: in its HBM slot, or (kHot) in the
+// LDS copy of the node being expanded (single engine: the popped node).
+template <bool kHot>
+__device__ __forceinline__ RState* node_rs(Eng& E, uint32_t slot, uint32_t side) {
+  if constexpr (kHot) return E.L.hot + side * E.nmax;
+  else return E.sv(slot, side).rs;
+}
+
+template <bool kHot>
 __device__ inline void analyze_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t side, uint32_t len, RInfo* out) {
   const int tid = threadIdx.x, lane = lane_id();
   SideView v = E.sv(slot, side);
+  const RState* rs = node_rs<kHot>(E, slot, side);
   if (tid == 0) ctl.nheavy = 0;
   __syncthreads();
   uint32_t ends = 0, multi = 0;
   for (uint32_t r = tid; r < E.n; r += kBlock) {
-    const RRaw s = rstate_load(&v.rs[r]);
+    const RRaw s = rstate_load(&rs[r]);
     if (rraw_e(s) == kInactive) {
       out[r].e = kInactive;
       out[r].n = 0;
@@ -322,10 +369,10 @@ __device__ inline void analyze_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t si
   if (ends) atomicAdd(&ctl.n_end[side], ends);
   if (multi) atomicOr(&ctl.multi[side], 1u);
   __syncthreads();
-  const uint32_t nh = ctl.nheavy;
+  const uint32_t nh = uni(ctl.nheavy);
   for (uint32_t k = wave_id(); k < nh; k += kWaves) {
     const uint32_t r = E.L.list[k];
-    const uint32_t e = v.rs[r].e, off = v.rs[r].off;
+    const uint32_t e = rs[r].e, off = rs[r].off;
     const bool ok = wave_analyze_read(v.wf + (uint64_t)r * E.wcap, e, off, E.read(r), E.rlen(r), len, &out[r]);
     if (lane == 0) {
       if (!ok) atomicOr(&ctl.ovf, 1u);
@@ -337,18 +384,20 @@ __device__ inline void analyze_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t si
 }
 
 // ---- FINALIZE one side on scratch (the node is not modified) ----
+template <bool kHot>
 __device__ inline void finalize_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t side, uint32_t len, uint32_t* fe,
                                      WaveCounters& cnt) {
   const int lane = lane_id();
   SideView v = E.sv(slot, side);
+  const RState* rs = node_rs<kHot>(E, slot, side);
   for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
-    const uint32_t e = v.rs[r].e;
+    const uint32_t e = rs[r].e;
     if (e == kInactive) {
       if (lane == 0) fe[r] = kInactive;
       continue;
     }
     uint32_t f = 0;
-    const bool ok = wave_finalize_read(v.wf + (uint64_t)r * E.wcap, e, v.rs[r].off, E.read(r), E.rlen(r), v.con,
+    const bool ok = wave_finalize_read(v.wf + (uint64_t)r * E.wcap, e, rs[r].off, E.read(r), E.rlen(r), v.con,
                                        len, E.A->cfg.wildcard, E.scratch, E.wcap, f, cnt);
     if (lane == 0) {
       if (!ok) atomicOr(&ctl.ovf, 4u);
@@ -364,6 +413,9 @@ __device__ inline void finalize_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t s
 // path for reads that must grow their edit distance. When `info` is set, the
 // pushed side-0 child's nominations are written there (the next pop's
 // analysis). When `want_cost`, accumulates the single-side priority cost.
+// kSrcHot: the parent's RStates are the LDS copy (else the slot's own);
+// kDstHot: the child's RStates go to the LDS copy (else to the slot).
+template <bool kSrcHot, bool kDstHot>
 __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
                                   bool want_cost, RInfo* info) {
   const int tid = threadIdx.x, lane = lane_id();
@@ -381,9 +433,11 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
     const uint32_t hi = it >= E.n ? 1u : 0u, r = it - hi * E.n, side = first + hi;
     const int sym = side == 0 ? s0 : s1;
     SideView v = E.sv(slot, side);
-    const RRaw s = rstate_load(&v.rs[r]);
+    RState* dst = node_rs<kDstHot>(E, slot, side);
+    const RRaw s = rstate_load(&node_rs<kSrcHot>(E, slot, side)[r]);
     RInfo* out = (info && side == 0) ? &info[r] : nullptr;
     if (rraw_e(s) == kInactive) {
+      if (kSrcHot != kDstHot) rstate_store(&dst[r], s);
       if (out) {
         out->e = kInactive;
         out->n = 0;
@@ -395,6 +449,7 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
     const uint8_t* rd = E.read(r);
     const uint32_t blen = E.rlen(r);
     if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
+      if (kSrcHot != kDstHot) rstate_store(&dst[r], s);
       E.L.list[atomicAdd(&ctl.nheavy, 1u)] = side * E.n + r;
       continue;
     }
@@ -404,7 +459,7 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
     const bool heavy =
         thread_push(f, rd, blen, olen - 1, (uint8_t)sym, cfg.wildcard, early, v.wf + (uint64_t)r * E.wcap, cmp);
     tc.compares += cmp;
-    front_store(&v.rs[r], f);
+    front_store(&dst[r], f);
     if (heavy) {
       E.L.list[atomicAdd(&ctl.nheavy, 1u)] = side * E.n + r;
       continue;
@@ -419,12 +474,15 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
       multi |= m;
     }
   }
+  PH_MARK(8);
   flush_thread_counters(ctl, tc);
+  PH_MARK(9);
   if (ends) atomicAdd(&ctl.n_end[0], ends);
   if (multi) atomicOr(&ctl.multi[0], 1u);
   if (want_cost && cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);
   __syncthreads();
-  const uint32_t nh = ctl.nheavy;
+  PH_MARK(5);
+  const uint32_t nh = uni(ctl.nheavy);
   WaveCounters cnt = {0, 0, 0, 0, 0};
   for (uint32_t k = wave_id(); k < nh; k += kWaves) {
     const uint32_t it = E.L.list[k];
@@ -434,13 +492,14 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
     const int sym = side == 0 ? s0 : s1;
     uint32_t e = 0;
     uint32_t* wf = v.wf + (uint64_t)r * E.wcap;
-    if (!wave_heavy(&v.rs[r], wf, E.read(r), E.rlen(r), v.con, olen, (uint8_t)sym, cfg.wildcard, early, E.wcap, cnt,
+    RState* dst = node_rs<kDstHot>(E, slot, side);
+    if (!wave_heavy(&dst[r], wf, E.read(r), E.rlen(r), v.con, olen, (uint8_t)sym, cfg.wildcard, early, E.wcap, cnt,
                     e)) {
       if (lane == 0) atomicOr(&ctl.ovf, 4u);
       continue;
     }
     if (info && side == 0) {
-      const bool ok = wave_analyze_read(wf, e, v.rs[r].off, E.read(r), E.rlen(r), olen, &info[r]);
+      const bool ok = wave_analyze_read(wf, e, dst[r].off, E.read(r), E.rlen(r), olen, &info[r]);
       if (lane == 0) {
         if (!ok) atomicOr(&ctl.ovf, 1u);
         if (info[r].end) atomicAdd(&ctl.n_end[0], 1u);
@@ -451,18 +510,40 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
   }
   flush_counters(ctl, cnt);
   __syncthreads();
+  PH_MARK(6);
+}
+
+__device__ inline void copy_bytes(uint8_t* d, const uint8_t* s, uint32_t len) {
+  const uint32_t n16 = len >> 4;
+  for (uint32_t i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+  for (uint32_t i = (n16 << 4) + threadIdx.x; i < len; i += kBlock) d[i] = s[i];
+}
+
+// move the RStates of one node side between its slot and the LDS copy
+__device__ inline void hot_store(Eng& E, uint32_t slot, uint32_t side) {
+  RState* d = E.sv(slot, side).rs;
+  const RState* h = E.L.hot + side * E.nmax;
+  for (uint32_t r = threadIdx.x; r < E.n; r += kBlock) rstate_store(&d[r], rstate_load(&h[r]));
+}
+__device__ inline void hot_fetch(Eng& E, uint32_t slot, uint32_t side) {
+  const RState* d = E.sv(slot, side).rs;
+  RState* h = E.L.hot + side * E.nmax;
+  for (uint32_t r = threadIdx.x; r < E.n; r += kBlock) rstate_store(&h[r], rstate_load(&d[r]));
 }
 
 // ---- clone a node: RState records, live wavefront rows, consensus bytes ----
+// kSrcHot: the source's RStates are the LDS copy; they are then not copied
+// (the clone's push writes the child's RStates straight into its slot).
+template <bool kSrcHot>
 __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t dst, uint32_t sdst, uint32_t len) {
   const int tid = threadIdx.x, lane = lane_id();
   SideView a = E.sv(src, ssrc), b = E.sv(dst, sdst);
-  for (uint32_t i = tid; i < len; i += kBlock) b.con[i] = a.con[i];
-  for (uint32_t r = tid; r < E.n; r += kBlock) {
-    rstate_store(&b.rs[r], rstate_load(&a.rs[r]));
-  }
+  const RState* ars = node_rs<kSrcHot>(E, src, ssrc);
+  copy_bytes(b.con, a.con, len);
+  if (!kSrcHot)
+    for (uint32_t r = tid; r < E.n; r += kBlock) rstate_store(&b.rs[r], rstate_load(&ars[r]));
   for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
-    const uint32_t e = a.rs[r].e;
+    const uint32_t e = ars[r].e;
     if (e == kInactive) continue;
     const uint32_t W = 2 * e + 1;
     const uint32_t* wa = a.wf + (uint64_t)r * E.wcap;
@@ -488,41 +569,113 @@ __device__ inline double vote_weight(const RInfo* r0, const RInfo* r1, uint32_t 
   return 0.0;
 }
 
+// One read's nominations in registers (RInfo is 32 bytes: two 16-byte LDS reads)
+struct RInfoReg {
+  uint32_t n, split, e;
+  uint64_t sym;    // sym[k] = byte k
+  uint4 occ;       // occ[k] = 16-bit halves: k=0,1 in .x ... k=6,7 in .w
+};
+__device__ __forceinline__ RInfoReg rinfo_load(const RInfo* p) {
+  static_assert(sizeof(RInfo) == 32, "RInfo layout");
+  const uint4 a = reinterpret_cast<const uint4*>(p)[0];
+  const uint4 b = reinterpret_cast<const uint4*>(p)[1];
+  RInfoReg x;
+  x.n = a.x & 0xFFu;
+  x.split = a.x >> 16;
+  x.sym = (uint64_t)a.y | ((uint64_t)a.z << 32);
+  x.occ = make_uint4(a.w, b.x, b.y, b.z);
+  x.e = b.w;
+  return x;
+}
+__device__ __forceinline__ uint32_t occ_at(const uint4& o, uint32_t k) {
+  const uint32_t w = k < 2 ? o.x : (k < 4 ? o.y : (k < 6 ? o.z : o.w));
+  return (k & 1) ? (w >> 16) : (w & 0xFFFFu);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// acc + 1.0 + 1.0 + ... (t times) with IEEE round-to-nearest after every
+// add, in closed form. Within one binade [2^p, 2^(p+1)) (acc < 2^53) every
+// integer step is exact, so a run that stays below the next power of two is a
+// single exact add; the step that crosses it is done as a real f64 add (the
+// only step that can round). At most ~log2(t) crossings.
+__device__ inline double add_ones(double acc, uint32_t t) {
+  while (t) {
+    if (acc == trunc(acc)) return acc + (double)t;  // integer + integer: exact
+    int ex;
+    frexp(acc, &ex);                          // acc in [2^(ex-1), 2^ex)
+    const double room = ldexp(1.0, ex) - acc;  // exact (same ulp grid)
+    const uint32_t k = min(t, (uint32_t)ceil(room) - 1u);  // steps staying below 2^ex
+    acc += (double)k;
+    t -= k;
+    if (t) {
+      acc += 1.0;
+      t--;
+    }
+  }
+  return acc;
+}
+
+// wave-uniform 256-bit symbol set
+struct SymSet {
+  uint64_t w0, w1, w2, w3;
+  __device__ bool has(uint32_t s) const {
+    const uint64_t w = s < 64 ? w0 : (s < 128 ? w1 : (s < 192 ? w2 : w3));
+    return (w >> (s & 63)) & 1ull;
+  }
+  __device__ void add(uint32_t s) {
+    const uint64_t b = 1ull << (s & 63);
+    if (s < 64) w0 |= b;
+    else if (s < 128) w1 |= b;
+    else if (s < 192) w2 |= b;
+    else w3 |= b;
+  }
+};
+
 __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, const RInfo* r0, const RInfo* r1,
                                   uint32_t n, bool weighted, bool is_dual, bool multi, int wc) {
   const int lane = lane_id();
   const bool side1 = side == 0;
-  // wave-uniform key lists packed as bytes in two u64 (no private arrays)
+  // 1. outer-map insertion order: first appearance over (read, inner order)
   uint64_t ins_lo = 0, ins_hi = 0;
   uint32_t nk = 0;
+  SymSet known = {0, 0, 0, 0};
   auto ins_at = [&](uint32_t j) { return j < 8 ? byte_at(ins_lo, j) : byte_at(ins_hi, j - 8); };
   for (uint32_t base = 0; base < n; base += 64) {
     const uint32_t r = base + lane;
-    bool voter = r < n && ri[r].e != kInactive;
+    RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
+    if (r < n) x = rinfo_load(&ri[r]);
+    bool voter = x.e != kInactive;
     if (voter && weighted) voter = vote_weight(r0, r1, r, is_dual, side1) > 0.0;
+    const uint32_t xn = voter ? x.n : 0u;
     for (;;) {
       uint32_t cand = 0xFFFF;
-      if (voter) {
-        const RInfo& x = ri[r];
-        for (uint32_t k = 0; k < x.n && cand == 0xFFFF; ++k) {
-          const uint32_t s = x.sym[k];
-          uint32_t j = 0;
-          while (j < nk && ins_at(j) != s) ++j;
-          if (j == nk) cand = s;
+      for (uint32_t k = 0; k < xn; ++k) {
+        const uint32_t s = byte_at(x.sym, k);
+        if (!known.has(s)) {
+          cand = s;
+          break;
         }
       }
       const uint64_t m = ballot(cand != 0xFFFF);
       if (!m) break;
       const int first = __ffsll((unsigned long long)m) - 1;
-      const uint32_t s = (uint32_t)__shfl((int)cand, first, 64);
+      const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)cand, first);
       if (nk == (uint32_t)kKout) return false;
       if (nk < 8) ins_lo |= (uint64_t)s << (8 * nk);
       else ins_hi |= (uint64_t)s << (8 * (nk - 8));
       nk++;
+      known.add(s);
     }
   }
+  // 2. hashbrown iteration order, wildcard removed (consensus.rs:556-561)
+  PH_MARK(10);
   const uint64_t ord = fx_order_packed(nk, ins_at);
-  // iteration-order keys with the wildcard removed (consensus.rs:556-561)
   uint64_t k_lo = 0, k_hi = 0;
   uint32_t m = 0;
   const bool drop_wc = wc >= 0 && nk > 1;
@@ -534,45 +687,73 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
     m++;
   }
   auto key_at = [&](uint32_t j) { return j < 8 ? byte_at(k_lo, j) : byte_at(k_hi, j - 8); };
+  PH_MARK(11);
+  // 3. per-key sums; lane k keeps key k's running sum
+  double accv = 0.0;
   if (!weighted && !multi) {
-    // every voter has exactly one distinct symbol: contribution 1.0 each, so
-    // the ordered f64 sum is an exact integer count; lane j keeps key j's count
+    // every voter has exactly one distinct symbol: each contribution is exactly
+    // 1.0, so the ordered f64 sum is an exact integer count
     uint32_t c = 0;
     for (uint32_t base = 0; base < n; base += 64) {
       const uint32_t r = base + lane;
-      const bool voter = r < n && ri[r].e != kInactive && ri[r].n == 1;
-      const uint32_t s = voter ? ri[r].sym[0] : 0xFFFF;
+      uint32_t s = 0xFFFF;
+      if (r < n) {
+        const RInfoReg x = rinfo_load(&ri[r]);
+        if (x.e != kInactive && x.n == 1) s = byte_at(x.sym, 0);
+      }
       for (uint32_t k = 0; k < m; ++k) {
         const uint32_t pc = (uint32_t)__popcll((unsigned long long)ballot(s == key_at(k)));
         if (k == (uint32_t)lane) c += pc;
       }
     }
-    if ((uint32_t)lane < m) {
-      ctl.keys[side][lane] = (uint8_t)key_at(lane);
-      ctl.vals[side][lane] = (double)c;
-    }
-  } else if ((uint32_t)lane < m) {
-    const uint32_t key = key_at(lane);
-    double acc = 0.0;
-    for (uint32_t r = 0; r < n; ++r) {
-      const RInfo& x = ri[r];
-      if (x.e == kInactive) continue;
-      double w = 1.0;
-      if (weighted) {
-        w = vote_weight(r0, r1, r, is_dual, side1);
-        if (!(w > 0.0)) continue;
-      }
-      for (uint32_t k = 0; k < x.n; ++k) {
-        if (x.sym[k] == key) {
-          acc += w * (double)x.occ[k] / (double)x.split;
-          break;
+    accv = (double)c;
+  } else {
+    // contributions computed lane-parallel (one read per lane), then folded
+    // strictly in read order (the reference's f64 summation order); a read
+    // without the key adds nothing (x + 0.0 == x, so skipping it is exact)
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t r = base + lane;
+      RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
+      if (r < n) x = rinfo_load(&ri[r]);
+      double w = 0.0;
+      if (x.e != kInactive) w = weighted ? vote_weight(r0, r1, r, is_dual, side1) : 1.0;
+      const bool voter = w > 0.0;
+      const double dsplit = (double)x.split;
+      for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t key = key_at(k);
+        uint32_t occ = 0;
+        if (voter)
+          for (uint32_t j = 0; j < x.n; ++j)
+            if (byte_at(x.sym, j) == key) {
+              occ = occ_at(x.occ, j);
+              break;
+            }
+        const double c = occ ? w * (double)occ / dsplit : 0.0;
+        // runs of exact 1.0 contributions are added in closed form
+        // (add_ones); every other contribution is added one at a time
+        const uint64_t ones = ballot(occ != 0 && c == 1.0);
+        uint64_t frac = ballot(occ != 0 && c != 1.0);
+        double acc = readlane_f64(accv, (int)k);
+        uint64_t done = 0;
+        while (frac) {
+          const int l = __builtin_ctzll(frac);
+          frac &= frac - 1;
+          const uint64_t below = (1ull << l) - 1ull;
+          acc = add_ones(acc, (uint32_t)__popcll((unsigned long long)(ones & below & ~done)));
+          done = below | (1ull << l);
+          acc += readlane_f64(c, l);
         }
+        acc = add_ones(acc, (uint32_t)__popcll((unsigned long long)(ones & ~done)));
+        if ((uint32_t)lane == k) accv = acc;
       }
     }
-    ctl.keys[side][lane] = key;
-    ctl.vals[side][lane] = acc;
+  }
+  if ((uint32_t)lane < m) {
+    ctl.keys[side][lane] = (uint8_t)key_at(lane);
+    ctl.vals[side][lane] = accv;
   }
   if (lane == 0) ctl.nkeys[side] = m;
+  PH_MARK(12);
   return true;
 }
 
@@ -618,6 +799,10 @@ __device__ inline void finish_problem(const EngineArgs& A, Ctl& ctl, uint8_t* ou
     ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
     A.status[prob] = ctl.status;
     for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)prob * S_NSTAT + s] = ctl.cnt[s];
+#ifdef WC_PHASE_PROF
+    if (A.phases)
+      for (int k = 0; k < kPhases; ++k) atomicAdd(&A.phases[k], (unsigned long long)ctl.ph[k]);
+#endif
   }
   __syncthreads();
 }
@@ -637,7 +822,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
   for (;;) {
     if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
     __syncthreads();
-    const uint32_t prob = ctl.prob;
+    const uint32_t prob = uni(ctl.prob);
     if (prob >= A.n_problems) break;
     E.P = A.problems[prob];
     E.n = E.P.n_reads;
@@ -667,6 +852,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           if (top.cost > ctl.max_err || top.len < ctl.trk_thr[0] || t.at_capacity(top.len)) {
             ctl.cnt[S_IGNORED]++;
             E.L.freestack[ctl.nfree++] = top.slot;
+            if (top.slot == ctl.hot_slot) ctl.hot_slot = kNoSlot;
             ctl.action = 1;
           } else {
             ctl.farthest[0] = max(ctl.farthest[0], (uint64_t)top.len);
@@ -675,6 +861,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
             if (!t.process(top.len)) ctl.status = 4;  // "Capacity is full"
             ctl.action = 0;
             ctl.cache_hit = top.slot == ctl.cache_slot;
+            // the popped node's RStates move into LDS; the previous LDS
+            // node (still queued) is written back to its slot first
+            ctl.hot_prev = ctl.hot_slot;
+            ctl.hot_load = top.slot != ctl.hot_slot;
+            ctl.hot_slot = top.slot;
           }
           trace_pop(A, prob, top, ctl.action << 1, 0);
         }
@@ -688,26 +879,35 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         ctl.cache_slot = kNoSlot;
         ctl.ovf = 0;
       }
+      PH_MARK(13);
       __syncthreads();
-      if (ctl.action == 2) break;
-      if (ctl.action == 1) continue;
-      if (ctl.status != ST_OK) break;
+      PH_MARK(0);
+      if (uni(ctl.action) == 2) break;
+      if (uni(ctl.action) == 1) continue;
+      if (uni(ctl.status) != ST_OK) break;
 
-      const uint32_t top = ctl.top_slot;
-      const uint32_t len = ctl.top_len;
-      if (!ctl.cache_hit) analyze_side(E, ctl, top, 0, len, E.L.rinfo);
+      const uint32_t top = uni(ctl.top_slot);
+      const uint32_t len = uni(ctl.top_len);
+      if (uni(ctl.hot_load)) {
+        // per read r the same thread stores then fetches: no barrier needed
+        const uint32_t prev = uni(ctl.hot_prev);
+        if (prev != kNoSlot) hot_store(E, prev, 0);
+        hot_fetch(E, top, 0);
+      }
+      if (!uni(ctl.cache_hit)) analyze_side<true>(E, ctl, top, 0, len, E.L.rinfo);
+      PH_MARK(1);
       if (tid == 0) {
         const uint32_t ne = ctl.n_end[0];
         ctl.reached = early ? (ne == E.n) : (ne > 0);  // consensus.rs:516-532
         if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
       }
       __syncthreads();
-      if (ctl.status != ST_OK) break;
+      if (uni(ctl.status) != ST_OK) break;
 
       // ---- finalize a clone (consensus.rs:254-279) ----
-      if (ctl.reached) {
+      if (uni(ctl.reached)) {
         WaveCounters cnt = {0, 0, 0, 0, 0};
-        finalize_side(E, ctl, top, 0, len, E.L.fe, cnt);
+        finalize_side<true>(E, ctl, top, 0, len, E.L.fe, cnt);
         flush_counters(ctl, cnt);
         __syncthreads();
         if (tid == 0) {
@@ -736,11 +936,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           }
         }
         __syncthreads();
-        if (ctl.status != ST_OK) break;
-        if (ctl.store_idx >= 0) {
+        if (uni(ctl.status) != ST_OK) break;
+        if (uni(ctl.store_idx) >= 0) {
           const uint32_t lens[2] = {len, 0};
           store_record(E, ctl, outp, top, 1, lens, false);
         }
+        PH_MARK(2);
       }
 
       // ---- votes + child selection (consensus.rs:283-321) ----
@@ -771,10 +972,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         }
       }
       __syncthreads();
-      if (ctl.status != ST_OK) break;
-      const uint32_t nc = ctl.nchild;
+      PH_MARK(3);
+      if (uni(ctl.status) != ST_OK) break;
+      const uint32_t nc = uni(ctl.nchild);
       if (nc == 0) {
-        if (tid == 0) E.L.freestack[ctl.nfree++] = top;
+        if (tid == 0) {
+          E.L.freestack[ctl.nfree++] = top;
+          ctl.hot_slot = kNoSlot;
+        }
         __syncthreads();
         continue;
       }
@@ -797,12 +1002,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           ctl.multi[0] = 0;
         }
         __syncthreads();
-        if (ctl.status != ST_OK) break;
-        const uint32_t slot = ctl.cur_slot;
-        if (slot != top) copy_side(E, top, 0, slot, 0, len);
+        if (uni(ctl.status) != ST_OK) break;
+        const uint32_t slot = uni(ctl.cur_slot);
+        if (slot != top) copy_side<true>(E, top, 0, slot, 0, len);
         if (tid == 0) E.sv(slot, 0).con[len] = (uint8_t)ctl.ch_s[c][0];
         __syncthreads();
-        push_sides(E, ctl, slot, ctl.ch_s[c][0], -1, len + 1, 0, true, E.L.rinfo);
+        PH_MARK(4);
+        // clones read the parent from LDS and write their own slot; the last
+        // child is pushed in place on the LDS copy
+        const int sym = uni((int32_t)ctl.ch_s[c][0]);
+        if (slot != top) push_sides<true, false>(E, ctl, slot, sym, -1, len + 1, 0, true, E.L.rinfo);
+        else push_sides<true, true>(E, ctl, slot, sym, -1, len + 1, 0, true, E.L.rinfo);
         if (tid == 0) {
           if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
           else if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
@@ -811,9 +1021,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           E.L.meta[slot].len[0] = len + 1;
         }
         __syncthreads();
-        if (ctl.status != ST_OK) break;
+        if (uni(ctl.status) != ST_OK) break;
       }
-      if (ctl.status != ST_OK) break;
+      if (uni(ctl.status) != ST_OK) break;
       if (tid == 0) {
         TrackerRef t = E.tracker(ctl, 0);
         for (uint32_t c = 0; c < nc; ++c) {
@@ -826,6 +1036,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         ctl.cache_multi = ctl.multi[0];
       }
       __syncthreads();
+      PH_MARK(7);
     }
     finish_problem(A, ctl, outp, prob);
   }
@@ -849,7 +1060,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
   for (;;) {
     if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
     __syncthreads();
-    const uint32_t prob = ctl.prob;
+    const uint32_t prob = uni(ctl.prob);
     if (prob >= A.n_problems) break;
     E.P = A.problems[prob];
     E.n = E.P.n_reads;
@@ -904,18 +1115,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         ctl.ovf = 0;
       }
       __syncthreads();
-      if (ctl.action == 2) break;
-      if (ctl.action == 1) continue;
-      if (ctl.status != ST_OK) break;
+      if (uni(ctl.action) == 2) break;
+      if (uni(ctl.action) == 1) continue;
+      if (uni(ctl.status) != ST_OK) break;
 
-      const uint32_t top = ctl.top_slot;
-      const uint32_t tlen = ctl.top_len;
-      const bool tdual = ctl.top_dual != 0;
+      const uint32_t top = uni(ctl.top_slot);
+      const uint32_t tlen = uni(ctl.top_len);
+      const bool tdual = uni(ctl.top_dual) != 0;
       const SlotMeta tm = E.L.meta[top];
       const uint32_t tlens[2] = {tm.len[0], tm.len[1]};
 
-      analyze_side(E, ctl, top, 0, tlens[0], R0);
-      if (tdual) analyze_side(E, ctl, top, 1, tlens[1], R1);
+      analyze_side<false>(E, ctl, top, 0, tlens[0], R0);
+      if (tdual) analyze_side<false>(E, ctl, top, 1, tlens[1], R1);
       // reached_all_end (dual_consensus.rs:1174-1195): per read, either side at its end
       for (uint32_t r = tid; r < E.n; r += kBlock) {
         const bool v = (R0[r].e != kInactive && R0[r].end) || (tdual && R1[r].e != kInactive && R1[r].end);
@@ -930,13 +1141,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
       }
       __syncthreads();
-      if (ctl.status != ST_OK) break;
+      if (uni(ctl.status) != ST_OK) break;
 
       // ---- finalize a clone (dual_consensus.rs:438-492) ----
-      if (ctl.reached) {
+      if (uni(ctl.reached)) {
         WaveCounters cnt = {0, 0, 0, 0, 0};
-        finalize_side(E, ctl, top, 0, tlens[0], E.L.fe, cnt);
-        if (tdual) finalize_side(E, ctl, top, 1, tlens[1], E.L.fe + E.nmax, cnt);
+        finalize_side<false>(E, ctl, top, 0, tlens[0], E.L.fe, cnt);
+        if (tdual) finalize_side<false>(E, ctl, top, 1, tlens[1], E.L.fe + E.nmax, cnt);
         flush_counters(ctl, cnt);
         __syncthreads();
         if (tid == 0) {
@@ -982,8 +1193,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           }
         }
         __syncthreads();
-        if (ctl.status != ST_OK) break;
-        if (ctl.store_idx >= 0) store_record(E, ctl, outp, top, tdual ? 2 : 1, tlens, tdual);
+        if (uni(ctl.status) != ST_OK) break;
+        if (uni(ctl.store_idx) >= 0) store_record(E, ctl, outp, top, tdual ? 2 : 1, tlens, tdual);
       }
 
       // ---- active_min_count growth (dual_consensus.rs:497-513) ----
@@ -1088,8 +1299,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         ctl.nchild = nc;
       }
       __syncthreads();
-      if (ctl.status != ST_OK) break;
-      const uint32_t nc = ctl.nchild;
+      if (uni(ctl.status) != ST_OK) break;
+      const uint32_t nc = uni(ctl.nchild);
       if (nc == 0) {
         if (tid == 0) E.L.freestack[ctl.nfree++] = top;
         __syncthreads();
@@ -1114,17 +1325,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           ctl.some_acc[0] = ctl.some_acc[1] = 0;
         }
         __syncthreads();
-        if (ctl.status != ST_OK) break;
-        const uint32_t slot = ctl.cur_slot;
-        const uint8_t kind = ctl.ch_kind[c];
-        const int s0 = ctl.ch_s[c][0], s1 = ctl.ch_s[c][1];
+        if (uni(ctl.status) != ST_OK) break;
+        const uint32_t slot = uni(ctl.cur_slot);
+        const uint8_t kind = (uint8_t)uni((uint32_t)ctl.ch_kind[c]);
+        const int s0 = uni((int32_t)ctl.ch_s[c][0]), s1 = uni((int32_t)ctl.ch_s[c][1]);
         if (slot != top) {
-          copy_side(E, top, 0, slot, 0, tlens[0]);
-          if (tdual) copy_side(E, top, 1, slot, 1, tlens[1]);
+          copy_side<false>(E, top, 0, slot, 0, tlens[0]);
+          if (tdual) copy_side<false>(E, top, 1, slot, 1, tlens[1]);
           __syncthreads();
         }
         // activate_dual (dual_consensus.rs:957-976): side 2 := side 1
-        if (kind == 2) copy_side(E, slot, 0, slot, 1, tlens[0]);
+        if (kind == 2) copy_side<false>(E, slot, 0, slot, 1, tlens[0]);
         if (tid == 0) {
           SlotMeta m = tm;
           if (kind == 2) {
@@ -1146,7 +1357,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         }
         __syncthreads();
         const uint32_t nl0 = E.L.meta[slot].len[0], nl1 = E.L.meta[slot].len[1];
-        push_sides(E, ctl, slot, s0, s1, nl0, nl1, false, nullptr);
+        push_sides<false, false>(E, ctl, slot, s0, s1, nl0, nl1, false, nullptr);
         // prune (dual_consensus.rs:1030-1045) + priority (:1092-1168)
         const bool cdual = (E.L.meta[slot].flags & 1u) != 0;
         {
@@ -1187,9 +1398,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           ctl.ch_len[c] = max(m.len[0], m.len[1]);
         }
         __syncthreads();
-        if (ctl.status != ST_OK) break;
+        if (uni(ctl.status) != ST_OK) break;
       }
-      if (ctl.status != ST_OK) break;
+      if (uni(ctl.status) != ST_OK) break;
       if (tid == 0) {
         for (uint32_t c = 0; c < nc; ++c) {
           const uint32_t k = (E.L.meta[ctl.ch_slot[c]].flags & 1u) ? 1 : 0;

@@ -88,7 +88,9 @@ struct EngineArgs {
   uint32_t* trace;       // debug: per-pop records of problem 0 (nullptr = off)
   uint32_t trace_cap;    // records (4 u32 each); trace[0] = count
   uint32_t _pad2;
+  unsigned long long* phases;  // debug (WC_PHASE_PROF builds): shader cycles per phase, kPhases
 };
+constexpr int kPhases = 16;
 
 // ---- byte layouts (host and device compute them identically) ----
 __host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
@@ -154,9 +156,13 @@ struct RInfo {
   uint16_t occ[kKmax];
   uint32_t e;     // current edit distance (kInactive = None)
 };
-// LDS: heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] | heavy list[2*nmax] u32
+// sides whose expanded node's RStates are held in LDS (single engine only)
+__host__ __device__ inline uint32_t hot_sides(uint32_t sides) { return sides == 1 ? 1u : 0u; }
+// LDS: hot RStates[hot_sides][nmax] | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
+//      heavy list[2*nmax] u32
 __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax) {
-  uint64_t t = (uint64_t)pcap * sizeof(HeapEntry);
+  uint64_t t = (uint64_t)hot_sides(sides) * nmax * sizeof(RState);
+  t += (uint64_t)pcap * sizeof(HeapEntry);
   t += align16((uint64_t)pcap * 4);
   t += (uint64_t)pcap * sizeof(SlotMeta);
   t += (uint64_t)sides * nmax * sizeof(RInfo);

@@ -372,6 +372,14 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
       HIPCHK(hipMemsetAsync(tbuf.p, 0, 16, ctx->stream));
     }
 
+    // debug phase cycle counters (WC_PHASES=<file>, WC_PHASE_PROF builds only)
+    const char* phase_path = getenv("WC_PHASES");
+    DevBuf pbuf;
+    if (phase_path && pbuf.ensure(kPhases * 8)) {
+      a.phases = (unsigned long long*)pbuf.p;
+      HIPCHK(hipMemsetAsync(pbuf.p, 0, kPhases * 8, ctx->stream));
+    }
+
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (sides == 1) launch_single_engine(a, grid, lds, ctx->stream);
     else launch_dual_engine(a, grid, lds, ctx->stream);
@@ -382,6 +390,17 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     R.kernel_ms += ms;
     R.launches++;
+    if (a.phases) {
+      unsigned long long ph[kPhases];
+      HIPCHK(hipMemcpy(ph, pbuf.p, sizeof(ph), hipMemcpyDeviceToHost));
+      if (FILE* f = fopen(phase_path, "a")) {
+        fprintf(f, "sides=%u kernel_ms=%.3f", sides, ms);
+        for (int k = 0; k < kPhases; ++k) fprintf(f, " %llu", ph[k]);
+        fprintf(f, "\n");
+        fclose(f);
+      }
+      pbuf.release();
+    }
     if (a.trace) {
       uint32_t cnt = 0;
       HIPCHK(hipMemcpy(&cnt, tbuf.p, 4, hipMemcpyDeviceToHost));
