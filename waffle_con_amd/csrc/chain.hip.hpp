@@ -1,0 +1,398 @@
+// Linear-chain run-ahead for the ConsensusDWFA engine (included by engine.hip).
+//
+// The least-cost-first search of consensus.rs:139-351 is, almost everywhere, a
+// single chain: the popped node has exactly one passing candidate, the pushed
+// child is the only queued node and is popped next. Executed literally, every
+// consensus base costs a full pop: a block-wide push over all reads, the
+// votes, and a handful of barriers — latency, not bandwidth.
+//
+// run_chain executes up to K steps of such a chain speculatively and then
+// proves, step by step, that the reference search would have taken exactly
+// those steps:
+//   1. predict the next K-1 symbols (plurality of the reads' upcoming bases);
+//   2. every thread pushes the K symbols through its own read's DWFA
+//      (DWFALite::update, dynamic_wfa.rs:75-99; edit-distance increases are
+//      done by the thread's wave over the full wavefront) and records each
+//      step's nominations (dynamic_wfa.rs:241-255), cost and end flag;
+//   3. the votes of every step are evaluated exactly (consensus.rs:540-564,
+//      f64 order and hashbrown order as in the one-step path) and the pop
+//      sequence is replayed on the scalar search state: PQueueTracker
+//      threshold/capacity (consensus.rs:224-251), reached_end (:254), the
+//      candidate filter (:283-321). Step j is accepted only if the node would
+//      be popped next, explored, not reach an end, and have exactly one passing
+//      candidate equal to the predicted symbol j+1;
+//   4. the accepted prefix N_1..N_j* is committed: all counters, tracker and
+//      pool state are exactly those of j* literal iterations. If a step is
+//      rejected, the node's wavefront rows are restored from a backup slot and
+//      the accepted prefix is replayed.
+// The last accepted node is handed back to the literal path (pushed to the
+// queue with its nominations cached), which handles ends, branching and
+// everything else.
+
+// nomination record of one read at one chain step (u32)
+constexpr uint32_t kNomSymMask = 0xFFu;   // first symbol
+constexpr uint32_t kNomOne = 1u << 8;     // exactly one distinct symbol
+constexpr uint32_t kNomEnd = 1u << 12;    // reached_baseline_end
+constexpr uint32_t kNomActive = 1u << 13; // Some(dwfa)
+constexpr uint32_t kNomOvf = 1u << 14;    // >= 2 symbols: ChainOvf[code >> 16]
+
+__device__ __forceinline__ RInfoReg nom_load(const uint32_t* nom, const ChainOvf* ovf, uint32_t r) {
+  const uint32_t c = nom[r];
+  RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
+  if (!(c & kNomActive)) return x;
+  x.e = 0;
+  if (c & kNomOvf) {
+    const ChainOvf o = ovf[c >> 16];
+    x.n = o.n;
+    x.split = o.split;
+    x.sym = o.sym;
+    const uint64_t q = o.occ;
+    x.occ = make_uint4((uint32_t)(q & 0xFF) | (uint32_t)((q >> 8) & 0xFF) << 16,
+                       (uint32_t)((q >> 16) & 0xFF) | (uint32_t)((q >> 24) & 0xFF) << 16,
+                       (uint32_t)((q >> 32) & 0xFF) | (uint32_t)((q >> 40) & 0xFF) << 16,
+                       (uint32_t)((q >> 48) & 0xFF) | (uint32_t)((q >> 56) & 0xFF) << 16);
+  } else if (c & kNomOne) {
+    x.n = 1;
+    x.split = 1;  // occ / split = 1.0 exactly for a single symbol
+    x.sym = c & kNomSymMask;
+    x.occ = make_uint4(1, 0, 0, 0);
+  }
+  return x;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// (B) backup wavefront rows to slot S, prefetch capacities, predict symbols.
+__device__ inline void chain_prepare(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
+  const int tid = threadIdx.x, lane = lane_id();
+  SideView v = E.sv(top, 0), b = E.sv(S, 0);
+  for (uint32_t r = tid; r < E.n; r += kBlock) {
+    const RRaw h = rstate_load(&E.L.hot[r]);
+    if (rraw_e(h) == kInactive) continue;
+    if (rraw_flags(h) & kWide) atomicOr(&ctl.chain_nochain, 1u);
+    const uint32_t W = 2 * rraw_e(h) + 1;
+    const uint4* src = reinterpret_cast<const uint4*>(v.wf + (uint64_t)r * E.wcap);
+    uint4* dst = reinterpret_cast<uint4*>(b.wf + (uint64_t)r * E.wcap);
+    for (uint32_t i = 0; i < (W + 3) / 4; ++i) dst[i] = src[i];
+  }
+  const uint32_t* pc = E.trk + (E.lcap + 2);  // PQueueTracker processed counts
+  for (uint32_t j = tid; j <= K; j += kBlock) E.L.cpc[j] = (j >= 1) ? pc[L0 + j] : 0u;
+  if (wave_id() == 0) {
+    // upcoming bases of each read's first tip (reads 0..63)
+    uint32_t bo_tip = kInactive, blen = 0;
+    const uint8_t* rd = nullptr;
+    if ((uint32_t)lane < E.n) {
+      Front f;
+      front_load(rstate_load(&E.L.hot[lane]), f);
+      if (f.e != kInactive) {
+        rd = E.read(lane);
+        blen = E.rlen(lane);
+#pragma unroll
+        for (int k = kF - 1; k >= 0; --k)
+          if ((f.mask >> k) & 1u) {
+            const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+            if (f.fd[k] + f.off == L0 && bo < blen) bo_tip = bo;
+          }
+      }
+    }
+    for (uint32_t t = 1; t < K; ++t) {
+      const uint32_t p = bo_tip + t;
+      const uint32_t x = (bo_tip != kInactive && p < blen) ? (uint32_t)rd[p] : 0x100u;
+      // plurality of x over the wave (ties: the first-seen symbol)
+      uint64_t rem = ballot(x != 0x100u);
+      uint32_t best = 0x100u, bestc = 0;
+      while (rem) {
+        const int l = __builtin_ctzll(rem);
+        const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+        const uint64_t mm = ballot(x == s);
+        const uint32_t c = (uint32_t)__popcll((unsigned long long)mm);
+        if (c > bestc) {
+          bestc = c;
+          best = s;
+        }
+        rem &= ~mm;
+      }
+      if (best == 0x100u) {
+        if (lane == 0) atomicMin(&ctl.chain_stop, t);  // nothing to predict N_{t+1} from
+        break;
+      }
+      if (lane == 0) E.L.cpred[t + 1] = (uint8_t)best;
+    }
+    wave_lds_sync();
+    // the predicted symbols extend the node's own consensus buffer in place
+    // (positions >= L0 are not part of the node)
+    if ((uint32_t)lane >= 1 && (uint32_t)lane <= K) v.con[L0 + lane - 1] = E.L.cpred[lane];
+  }
+}
+
+// (C) push the K predicted symbols through every read, thread per read.
+// kFirst: speculative pass; stores nominations and step aggregates, leaves the
+// final RStates in slot S. Replay pass: writes the final RStates to the LDS
+// copy and the last step's nominations to rinfo (the analysis cache).
+template <bool kFirst>
+__device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
+  const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
+  if ((uint32_t)wave * 64 >= E.n) return;  // no reads in this wave (no barriers below)
+  const DevConfig& cfg = E.A->cfg;
+  const bool early = cfg.early != 0;
+  const int wc = cfg.wildcard;
+  SideView v = E.sv(top, 0);
+  const uint32_t r = (uint32_t)tid;
+  const bool has = r < E.n;
+  Front f;
+  f.e = kInactive;
+  f.off = f.maxb = f.nscmp = f.mask = 0;
+#pragma unroll
+  for (int k = 0; k < kF; ++k) f.fi[k] = f.fd[k] = 0;
+  const uint8_t* rd = nullptr;
+  uint32_t blen = 0;
+  if (has) {
+    front_load(rstate_load(&E.L.hot[r]), f);
+    rd = E.read(r);
+    blen = E.rlen(r);
+  }
+  const bool active = has && f.e != kInactive;
+  uint32_t* wf_row = v.wf + (uint64_t)r * E.wcap;
+  RState* tmp = &E.L.ctmp[wave];
+  for (uint32_t j = 1; j <= K; ++j) {
+    if (kFirst && j > uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
+    const uint32_t sym = uni((uint32_t)E.L.cpred[j]);
+    const uint32_t olen = L0 + j;
+    uint32_t cmp = 0;
+    bool heavy = false;
+    if (active) heavy = thread_push(f, rd, blen, olen - 1, (uint8_t)sym, wc, early, wf_row, cmp);
+    const uint32_t upd = (active && !heavy) ? 1u : 0u;
+    const uint32_t wout = upd ? 2 * f.e + 1 : 0u;
+    WaveCounters cnt = {0, 0, 0, 0, 0};
+    uint64_t hm = ballot(heavy);
+    while (hm) {  // edit-distance increase: the wave works on one read at a time
+      const int l = __builtin_ctzll(hm);
+      hm &= hm - 1;
+      if (lane == l) front_store(tmp, f);
+      wave_lds_sync();
+      const uint32_t rl = (uint32_t)wave * 64 + (uint32_t)l;
+      uint32_t e_out = 0;
+      const bool ok = wave_heavy(tmp, v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, olen,
+                                 (uint8_t)sym, wc, early, E.wcap, cnt, e_out);
+      wave_lds_sync();
+      if (!ok && lane == 0) atomicMin(&ctl.chain_stop, j - 1);
+      if (lane == l) {
+        const RRaw t = rstate_load(tmp);
+        if (rraw_flags(t) & kWide) atomicMin(&ctl.chain_stop, j - 1);  // not a thread-path state
+        front_load(t, f);
+      }
+      wave_lds_sync();
+    }
+    Nom o;
+    o.sym = o.occ = 0;
+    o.n = o.split = o.end = 0;
+    if (active) o = thread_nominate(f, rd, blen, olen);
+    if (kFirst) {
+      uint32_t code = 0;
+      if (active) {
+        code = kNomActive | (o.end ? kNomEnd : 0u) | (uint32_t)(o.sym & 0xFF) | (o.n == 1 ? kNomOne : 0u);
+        if (o.n > 1) {
+          const uint32_t idx = atomicAdd(&ctl.chain_novf, 1u);
+          if (idx < kChainOvf) {
+            ChainOvf& q = E.L.covf[idx];
+            q.sym = o.sym;
+            q.occ = o.occ;
+            q.split = o.split;
+            q.n = o.n;
+            code |= kNomOvf | (idx << 16);
+          } else {
+            atomicMin(&ctl.chain_stop, j - 1);
+          }
+        }
+      }
+      if (has) E.L.cnom[j * E.nmax + r] = code;
+      const uint64_t cost = active ? cost_of(f.e, cfg.cost_mode) : 0ull;
+      const uint64_t s_cost = wave_sum_u64(cost);
+      const uint32_t s_end = (uint32_t)__popcll((unsigned long long)ballot(active && o.end));
+      const bool s_multi = ballot(active && o.n > 1) != 0;
+      const uint32_t s_upd = (uint32_t)__popcll((unsigned long long)ballot(upd != 0)) + cnt.updates;
+      const uint32_t s_wout = wave_sum_u32(wout) + cnt.w_out;
+      const uint32_t s_cmp = wave_sum_u32(cmp) + cnt.compares;
+      if (lane == 0) {
+        ChainStep& st = E.L.cstep[j];
+        atomicAdd((unsigned long long*)&st.cost, (unsigned long long)s_cost);
+        if (s_end) atomicAdd(&st.n_end, s_end);
+        if (s_multi) atomicOr(&st.multi, 1u);
+        atomicAdd(&st.upd, s_upd);
+        atomicAdd(&st.wout, s_wout);
+        atomicAdd(&st.cmp, s_cmp);
+        if (cnt.edinc) atomicAdd(&st.edinc, cnt.edinc);
+      }
+    } else if (j == K && has) {
+      rinfo_store(&E.L.rinfo[r], o, f.e);
+    }
+  }
+  if (has) {
+    if (kFirst) front_store(&E.sv(S, 0).rs[r], f);
+    else front_store(&E.L.hot[r], f);
+  }
+}
+
+// (D) votes of the chain nodes N_1..N_{K-1}: ok[j] = exactly one passing
+// candidate and it is the predicted symbol j+1 (consensus.rs:283-321).
+__device__ inline void chain_votes(Eng& E, Ctl& ctl, uint32_t K) {
+  const int lane = lane_id();
+  const DevConfig& cfg = E.A->cfg;
+  for (uint32_t j = 1 + wave_id(); j < K; j += kWaves) {
+    const uint32_t* nom = E.L.cnom + j * E.nmax;
+    const bool multi = E.L.cstep[j].multi != 0;
+    uint32_t m = 0, key = 0;
+    double val = 0.0;
+    bool ok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r); },
+                              [&](uint32_t) { return 1.0; }, E.n, false, multi, cfg.wildcard, m, key, val);
+    if (ok) {
+      const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
+      const double thr = fmin((double)cfg.min_count, max_obs);
+      const uint64_t pass = ballot((uint32_t)lane < m && val >= thr);
+      ok = __popcll((unsigned long long)pass) == 1 &&
+           (uint32_t)__builtin_amdgcn_readlane((int)key, __builtin_ctzll(pass)) == (uint32_t)E.L.cpred[j + 1];
+    }
+    if (lane == 0) E.L.cstep[j].ok = ok ? 1u : 0u;
+  }
+}
+
+// (E) thread 0: replay the pops of N_1.. on the scalar search state
+// (consensus.rs:224-251 with the queue holding only the chain node) and
+// commit the accepted prefix. Returns j* = number of chain nodes generated.
+__device__ inline uint32_t chain_accept(Eng& E, Ctl& ctl, uint32_t L0, uint32_t Keff) {
+  const DevConfig& cfg = E.A->cfg;
+  const bool early = cfg.early != 0;
+  uint32_t* pc = E.trk + (E.lcap + 2);
+  uint32_t jstar = Keff >= 1 ? 1u : 0u;
+  uint64_t thr = ctl.trk_thr[0], farthest = ctl.farthest[0], lcnst = ctl.last_constraint[0];
+  for (uint32_t j = 1; j < Keff; ++j) {
+    const uint64_t L = L0 + j;
+    uint64_t t_thr = thr, t_l = lcnst;
+    uint64_t total = L >= t_thr ? 1u : 0u;  // the queue holds N_j only
+    while ((total > cfg.max_queue_size || t_l >= cfg.max_nodes_wo_constraint) && t_thr < farthest) {
+      if (t_thr == L) total--;
+      t_thr++;
+      t_l = 0;
+    }
+    const ChainStep& st = E.L.cstep[j];
+    if (st.cost > ctl.max_err || L < t_thr || (uint64_t)E.L.cpc[j] >= cfg.max_capacity_per_size) break;
+    const bool reached = early ? (st.n_end == E.n) : (st.n_end > 0);
+    if (reached || !st.ok) break;
+    thr = t_thr;
+    lcnst = t_l + 1;
+    farthest = max(farthest, L);
+    pc[L] = E.L.cpc[j] + 1;
+    ctl.cnt[S_POPS]++;
+    ctl.cnt[S_EXPLORED]++;
+    ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)1);
+    jstar = j + 1;
+  }
+  ctl.trk_thr[0] = thr;
+  ctl.farthest[0] = farthest;
+  ctl.last_constraint[0] = lcnst;
+  for (uint32_t j = 1; j <= jstar; ++j) {
+    const ChainStep& st = E.L.cstep[j];
+    ctl.cnt[S_UPDATES] += st.upd;
+    ctl.cnt[S_WOUT] += st.wout;
+    ctl.cnt[S_COMPARES] += st.cmp;
+    ctl.cnt[S_EDINC] += st.edinc;
+  }
+  return jstar;
+}
+
+// Run one chain from the popped node `top` (length L0, hot in LDS, queue
+// otherwise empty) whose single child symbol is s1. Returns j* (uniform); for
+// j* > 0 the chain node N_j* is in slot `top`/LDS, queued, with its
+// nominations cached; j* == 0 leaves everything as it was.
+__device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, int s1) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const uint32_t K = min(E.A->chain, E.lcap - L0);
+    ctl.chain_k = 0;
+    if (K >= 2 && ctl.nfree > 0) {
+      ctl.chain_k = K;
+      ctl.chain_slot = E.L.freestack[--ctl.nfree];
+      ctl.chain_stop = K;
+      ctl.chain_novf = 0;
+      ctl.chain_nochain = 0;
+      E.L.cpred[1] = (uint8_t)s1;
+    }
+  }
+  __syncthreads();
+  const uint32_t K = uni(ctl.chain_k);
+  if (K == 0) return 0;
+  const uint32_t S = uni(ctl.chain_slot);
+  for (uint32_t i = tid; i < (K + 1) * (uint32_t)(sizeof(ChainStep) / 4); i += kBlock)
+    reinterpret_cast<uint32_t*>(E.L.cstep)[i] = 0;
+  chain_prepare(E, ctl, top, L0, K, S);
+  __syncthreads();
+  if (uni(ctl.chain_nochain)) {
+    if (tid == 0) E.L.freestack[ctl.nfree++] = S;
+    __syncthreads();
+    return 0;
+  }
+  chain_walk<true>(E, ctl, top, L0, K, S);
+  __syncthreads();
+  const uint32_t Keff = uni(ctl.chain_stop);
+  chain_votes(E, ctl, Keff);
+  __syncthreads();
+  if (tid == 0) ctl.chain_len = chain_accept(E, ctl, L0, Keff);
+  __syncthreads();
+  const uint32_t jstar = uni(ctl.chain_len);
+  SideView v = E.sv(top, 0), b = E.sv(S, 0);
+  if (jstar == K && Keff == K) {
+    // every step accepted: the speculative final state is the node
+    for (uint32_t r = tid; r < E.n; r += kBlock) {
+      const RRaw t = rstate_load(&b.rs[r]);
+      rstate_store(&E.L.hot[r], t);
+      RInfoReg x = nom_load(E.L.cnom + K * E.nmax, E.L.covf, r);
+      Nom o;
+      o.n = x.n;
+      o.split = x.split;
+      o.sym = x.sym;
+      o.end = (E.L.cnom[K * E.nmax + r] & kNomEnd) ? 1u : 0u;
+      o.occ = (uint64_t)(x.occ.x & 0xFF) | (uint64_t)((x.occ.x >> 16) & 0xFF) << 8 |
+              (uint64_t)(x.occ.y & 0xFF) << 16 | (uint64_t)((x.occ.y >> 16) & 0xFF) << 24 |
+              (uint64_t)(x.occ.z & 0xFF) << 32 | (uint64_t)((x.occ.z >> 16) & 0xFF) << 40 |
+              (uint64_t)(x.occ.w & 0xFF) << 48 | (uint64_t)((x.occ.w >> 16) & 0xFF) << 56;
+      rinfo_store(&E.L.rinfo[r], o, rraw_e(t));
+    }
+  } else {
+    // restore the node's wavefront rows, then replay the accepted prefix
+    for (uint32_t r = tid; r < E.n; r += kBlock) {
+      const RRaw h = rstate_load(&E.L.hot[r]);
+      if (rraw_e(h) == kInactive) continue;
+      const uint32_t W = 2 * rraw_e(h) + 1;
+      const uint4* src = reinterpret_cast<const uint4*>(b.wf + (uint64_t)r * E.wcap);
+      uint4* dst = reinterpret_cast<uint4*>(v.wf + (uint64_t)r * E.wcap);
+      for (uint32_t i = 0; i < (W + 3) / 4; ++i) dst[i] = src[i];
+    }
+    __syncthreads();
+    if (jstar > 0) chain_walk<false>(E, ctl, top, L0, jstar, S);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    E.L.freestack[ctl.nfree++] = S;
+    if (jstar > 0) {
+      const ChainStep& st = E.L.cstep[jstar];
+      const uint32_t clen = L0 + jstar;
+      E.L.meta[top].len[0] = clen;
+      E.tracker(ctl, 0).insert(clen);
+      heap_push(E.L.heap, ctl.heap_n, HeapEntry{st.cost, clen, top});
+      ctl.cache_slot = top;
+      ctl.cache_nend = st.n_end;
+      ctl.cache_multi = st.multi;
+    }
+  }
+  __syncthreads();
+  return jstar;
+}

@@ -59,6 +59,8 @@ struct Ctl {
   uint32_t cache_slot, cache_hit, cache_nend, cache_multi;
   uint32_t hot_slot;  // slot whose RStates are held in Lds::hot (authoritative), kNoSlot = none
   uint32_t hot_prev, hot_load;
+  // linear-chain run-ahead (run_chain)
+  uint32_t chain_k, chain_slot, chain_stop, chain_novf, chain_nochain, chain_len;
   uint32_t nkeys[2];
   uint8_t keys[2][kKout];
   double vals[2][kKout];
@@ -99,6 +101,12 @@ struct Ctl {
 
 struct Lds {
   RState* hot;     // [sides][nmax] RStates of the node being expanded (single engine)
+  ChainStep* cstep;  // chain area (single engine with A.chain > 0)
+  ChainOvf* covf;
+  RState* ctmp;      // [kWaves]
+  uint32_t* cnom;    // [K+1][nmax]
+  uint32_t* cpc;     // [K+1]
+  uint8_t* cpred;    // [K+2]
   HeapEntry* heap;
   uint32_t* freestack;
   SlotMeta* meta;
@@ -107,11 +115,30 @@ struct Lds {
   uint32_t* list;  // [2*nmax] work list (heavy reads / wide analyses)
 };
 
-__device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32_t nmax) {
+__device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t K) {
   Lds l;
   uint8_t* p = smem;
   l.hot = (RState*)p;
   p += (uint64_t)hot_sides(sides) * nmax * sizeof(RState);
+  l.cstep = (ChainStep*)p;
+  l.covf = nullptr;
+  l.ctmp = nullptr;
+  l.cnom = nullptr;
+  l.cpc = nullptr;
+  l.cpred = nullptr;
+  if (K) {
+    p += align16((uint64_t)(K + 1) * sizeof(ChainStep));
+    l.covf = (ChainOvf*)p;
+    p += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
+    l.ctmp = (RState*)p;
+    p += (uint64_t)kWaves * 64;
+    l.cnom = (uint32_t*)p;
+    p += align16((uint64_t)(K + 1) * nmax * 4);
+    l.cpc = (uint32_t*)p;
+    p += align16((uint64_t)(K + 1) * 4);
+    l.cpred = p;
+    p += align16((uint64_t)(K + 2));
+  }
   l.heap = (HeapEntry*)p;
   p += (uint64_t)pcap * sizeof(HeapEntry);
   l.freestack = (uint32_t*)p;
@@ -272,7 +299,7 @@ __device__ inline Eng make_eng(const EngineArgs& A, uint8_t* smem) {
   E.active_min = E.total_active + L2;
   q += align16((uint64_t)2 * L2 * 4);
   E.scratch = (uint32_t*)q + (uint64_t)wave_id() * (A.wcap + 2);
-  E.L = carve(smem, A.sides, A.pcap, A.nmax);
+  E.L = carve(smem, A.sides, A.pcap, A.nmax, A.chain);
   return E;
 }
 
@@ -637,10 +664,14 @@ struct SymSet {
   }
 };
 
-__device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, const RInfo* r0, const RInfo* r1,
-                                  uint32_t n, bool weighted, bool is_dual, bool multi, int wc) {
+// Core of the votes over one node side (one wave). load(r) gives read r's
+// nominations (e = kInactive for None), weight(r) its vote weight (weighted
+// mode only). On return lane k < m holds the k-th key in iteration order and
+// its f64 vote. Returns false when more than kKout distinct symbols occur.
+template <class Load, class Weight>
+__device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, bool weighted, bool multi, int wc,
+                                       uint32_t& m_out, uint32_t& key_out, double& val_out) {
   const int lane = lane_id();
-  const bool side1 = side == 0;
   // 1. outer-map insertion order: first appearance over (read, inner order)
   uint64_t ins_lo = 0, ins_hi = 0;
   uint32_t nk = 0;
@@ -649,9 +680,9 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
   for (uint32_t base = 0; base < n; base += 64) {
     const uint32_t r = base + lane;
     RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
-    if (r < n) x = rinfo_load(&ri[r]);
+    if (r < n) x = load(r);
     bool voter = x.e != kInactive;
-    if (voter && weighted) voter = vote_weight(r0, r1, r, is_dual, side1) > 0.0;
+    if (voter && weighted) voter = weight(r) > 0.0;
     const uint32_t xn = voter ? x.n : 0u;
     for (;;) {
       uint32_t cand = 0xFFFF;
@@ -674,7 +705,6 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
     }
   }
   // 2. hashbrown iteration order, wildcard removed (consensus.rs:556-561)
-  PH_MARK(10);
   const uint64_t ord = fx_order_packed(nk, ins_at);
   uint64_t k_lo = 0, k_hi = 0;
   uint32_t m = 0;
@@ -687,7 +717,6 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
     m++;
   }
   auto key_at = [&](uint32_t j) { return j < 8 ? byte_at(k_lo, j) : byte_at(k_hi, j - 8); };
-  PH_MARK(11);
   // 3. per-key sums; lane k keeps key k's running sum
   double accv = 0.0;
   if (!weighted && !multi) {
@@ -698,7 +727,7 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
       const uint32_t r = base + lane;
       uint32_t s = 0xFFFF;
       if (r < n) {
-        const RInfoReg x = rinfo_load(&ri[r]);
+        const RInfoReg x = load(r);
         if (x.e != kInactive && x.n == 1) s = byte_at(x.sym, 0);
       }
       for (uint32_t k = 0; k < m; ++k) {
@@ -714,9 +743,9 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
     for (uint32_t base = 0; base < n; base += 64) {
       const uint32_t r = base + lane;
       RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
-      if (r < n) x = rinfo_load(&ri[r]);
+      if (r < n) x = load(r);
       double w = 0.0;
-      if (x.e != kInactive) w = weighted ? vote_weight(r0, r1, r, is_dual, side1) : 1.0;
+      if (x.e != kInactive) w = weighted ? weight(r) : 1.0;
       const bool voter = w > 0.0;
       const double dsplit = (double)x.split;
       for (uint32_t k = 0; k < m; ++k) {
@@ -748,14 +777,33 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
       }
     }
   }
+  m_out = m;
+  key_out = (uint32_t)lane < m ? key_at(lane) : 0u;
+  val_out = accv;
+  return true;
+}
+
+
+__device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, const RInfo* r0, const RInfo* r1,
+                                  uint32_t n, bool weighted, bool is_dual, bool multi, int wc) {
+  const int lane = lane_id();
+  const bool side1 = side == 0;
+  uint32_t m = 0, key = 0;
+  double val = 0.0;
+  const bool ok = wave_votes_core([&](uint32_t r) { return rinfo_load(&ri[r]); },
+                                  [&](uint32_t r) { return vote_weight(r0, r1, r, is_dual, side1); }, n, weighted,
+                                  multi, wc, m, key, val);
+  if (!ok) return false;
   if ((uint32_t)lane < m) {
-    ctl.keys[side][lane] = (uint8_t)key_at(lane);
-    ctl.vals[side][lane] = accv;
+    ctl.keys[side][lane] = (uint8_t)key;
+    ctl.vals[side][lane] = val;
   }
   if (lane == 0) ctl.nkeys[side] = m;
   PH_MARK(12);
   return true;
 }
+
+#include "chain.hip.hpp"
 
 // ---- write one result record (finalized node) ----
 __device__ inline void store_record(Eng& E, Ctl& ctl, uint8_t* outp, uint32_t slot, uint32_t nsides,
@@ -987,6 +1035,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (tid == 0) ctl.status = ST_RETRY | ST_RETRY_LCAP;
         __syncthreads();
         break;
+      }
+      // ---- one child and nothing else queued: linear-chain run-ahead ----
+      if (nc == 1 && A.chain && uni(ctl.heap_n) == 0 && E.P.n_active == E.n) {
+        const uint32_t jstar = run_chain(E, ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
+        PH_MARK(14);
+        if (jstar) continue;
       }
       // ---- push every child: clones first, the last child in place ----
       for (uint32_t c = 0; c < nc; ++c) {

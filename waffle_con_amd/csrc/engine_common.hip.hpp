@@ -406,9 +406,14 @@ __device__ __forceinline__ void front_store(RState* p, const Front& f) {
 }
 
 // Nomination + end flag of one read from its frontier (thread-level),
-// dynamic_wfa.rs:232-234 and :241-255. `multi` = more than one distinct symbol.
-__device__ inline void thread_analyze(const Front& f, const uint8_t* rd, uint32_t blen, uint32_t len, RInfo* out,
-                                      bool& multi) {
+// dynamic_wfa.rs:232-234 and :241-255: the distinct tip symbols in the
+// per-read FxHashMap iteration order with their occurrence counts.
+struct Nom {
+  uint64_t sym;  // byte k = k-th symbol in iteration order
+  uint64_t occ;  // byte k = its occurrences (<= kF tips)
+  uint32_t n, split, end;
+};
+__device__ inline Nom thread_nominate(const Front& f, const uint8_t* rd, uint32_t blen, uint32_t len) {
   uint32_t mb = f.maxb;
   uint32_t tipsym[kF];
 #pragma unroll
@@ -434,20 +439,47 @@ __device__ inline void thread_analyze(const Front& f, const uint8_t* rd, uint32_
     }
     cnts += 1u << (4 * j);
   }
-  const uint64_t ord = nk > 1 ? fx_order_packed(nk, [&](uint32_t j) { return byte_at(keys, j); }) : 0ull;
+  Nom o;
+  o.n = nk;
+  o.end = mb == blen;
+  if (nk <= 1) {
+    o.sym = keys;
+    o.occ = cnts;
+    o.split = cnts;
+    return o;
+  }
+  const uint64_t ord = fx_order_packed(nk, [&](uint32_t j) { return byte_at(keys, j); });
+  uint64_t sym = 0, occ = 0;
   uint32_t split = 0;
   for (uint32_t k = 0; k < nk; ++k) {
     const uint32_t j = nib(ord, k);
     const uint32_t c = (cnts >> (4 * j)) & 15u;
-    out->sym[k] = (uint8_t)byte_at(keys, j);
-    out->occ[k] = (uint16_t)c;
+    sym |= (uint64_t)byte_at(keys, j) << (8 * k);
+    occ |= (uint64_t)c << (8 * k);
     split += c;
   }
-  out->n = (uint8_t)nk;
-  out->split = (uint16_t)split;
-  out->end = (mb == blen);
-  out->e = f.e;
-  multi = nk > 1;
+  o.sym = sym;
+  o.occ = occ;
+  o.split = split;
+  return o;
+}
+// RInfo from a nomination: two 16-byte stores
+__device__ __forceinline__ void rinfo_store(RInfo* out, const Nom& o, uint32_t e) {
+  static_assert(sizeof(RInfo) == 32, "RInfo layout");
+  const uint32_t o16[4] = {
+      (uint32_t)(o.occ & 0xFF) | (uint32_t)((o.occ >> 8) & 0xFF) << 16,
+      (uint32_t)((o.occ >> 16) & 0xFF) | (uint32_t)((o.occ >> 24) & 0xFF) << 16,
+      (uint32_t)((o.occ >> 32) & 0xFF) | (uint32_t)((o.occ >> 40) & 0xFF) << 16,
+      (uint32_t)((o.occ >> 48) & 0xFF) | (uint32_t)((o.occ >> 56) & 0xFF) << 16};
+  uint4* q = reinterpret_cast<uint4*>(out);
+  q[0] = make_uint4(o.n | (o.end << 8) | (o.split << 16), (uint32_t)o.sym, (uint32_t)(o.sym >> 32), o16[0]);
+  q[1] = make_uint4(o16[1], o16[2], o16[3], e);
+}
+__device__ inline void thread_analyze(const Front& f, const uint8_t* rd, uint32_t blen, uint32_t len, RInfo* out,
+                                      bool& multi) {
+  const Nom o = thread_nominate(f, rd, blen, len);
+  rinfo_store(out, o, f.e);
+  multi = o.n > 1;
 }
 
 // The extend step of DWFALite::update for one appended symbol on the frontier

@@ -79,7 +79,7 @@ struct EngineArgs {
   uint32_t lcap;         // consensus capacity per side
   uint32_t nmax;         // max reads per problem in this batch
   uint32_t rmax;         // result records per problem
-  uint32_t _pad;
+  uint32_t chain;        // single engine: max linear-chain run-ahead steps (0 = off)
   uint8_t* out;
   uint64_t out_stride;
   uint32_t* status;      // per problem
@@ -156,12 +156,36 @@ struct RInfo {
   uint16_t occ[kKmax];
   uint32_t e;     // current edit distance (kInactive = None)
 };
+// ---- linear-chain run-ahead (single engine, engine.hip run_chain) ----
+constexpr uint32_t kChainMax = 16;   // steps per chain
+constexpr uint32_t kChainOvf = 192;  // multi-symbol nominations stored per chain
+struct ChainStep {                   // aggregates of one speculative step (node N_j)
+  uint64_t cost;
+  uint32_t n_end, multi, upd, wout, cmp, edinc, ok, pad;
+};
+struct ChainOvf {  // nominations of a read with >= 2 distinct tip symbols
+  uint64_t sym, occ;  // bytes in iteration order
+  uint32_t split, n;
+};
+// chain LDS: steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[K+1][nmax] u32 | pc[K+1] u32 | pred[K+2] u8
+__host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K) {
+  if (K == 0) return 0;
+  uint64_t t = align16((uint64_t)(K + 1) * sizeof(ChainStep));
+  t += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
+  t += (uint64_t)kWaves * 64;
+  t += align16((uint64_t)(K + 1) * nmax * 4);
+  t += align16((uint64_t)(K + 1) * 4);
+  t += align16((uint64_t)(K + 2));
+  return t;
+}
+
 // sides whose expanded node's RStates are held in LDS (single engine only)
 __host__ __device__ inline uint32_t hot_sides(uint32_t sides) { return sides == 1 ? 1u : 0u; }
-// LDS: hot RStates[hot_sides][nmax] | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
+// LDS: hot RStates[hot_sides][nmax] | chain area | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
 //      heavy list[2*nmax] u32
-__host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax) {
+__host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t chain) {
   uint64_t t = (uint64_t)hot_sides(sides) * nmax * sizeof(RState);
+  t += chain_lds_bytes(nmax, chain);
   t += (uint64_t)pcap * sizeof(HeapEntry);
   t += align16((uint64_t)pcap * 4);
   t += (uint64_t)pcap * sizeof(SlotMeta);

@@ -302,10 +302,15 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
   uint32_t lcap = ((maxlen + maxlen / 8 + 64 + 15) / 16) * 16;
   // node pool: as many slots as ~16 MiB of workspace per workgroup allows
   // (16..256), bounded by the LDS the heap/metadata need
+  // single engine: linear-chain run-ahead length (WC_CHAIN=<k> overrides, 0 = off)
+  uint32_t chain = (sides == 1 && nmax <= (uint32_t)kBlock) ? kChainMax : 0;
+  if (const char* ev = getenv("WC_CHAIN")) chain = std::min<uint32_t>((uint32_t)atoi(ev), kChainMax);
+  if (sides != 1 || nmax > (uint32_t)kBlock) chain = 0;
   uint32_t pcap = 16;
   {
     const uint64_t sb = slot_bytes(sides, nmax, wcap, lcap);
-    while (pcap < 256 && (uint64_t)(pcap * 2) * sb <= (16ull << 20) && lds_bytes(sides, pcap * 2, nmax) <= 40 * 1024)
+    while (pcap < 256 && (uint64_t)(pcap * 2) * sb <= (16ull << 20) &&
+           lds_bytes(sides, pcap * 2, nmax, chain) <= 40 * 1024)
       pcap *= 2;
   }
   const uint32_t rmax = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cfg.max_return_size, 1), 256);
@@ -322,7 +327,7 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
       dp[i].max_read_len = q.max_len;
       dp[i].n_active = n_active[ids[i]];
     }
-    size_t lds = (size_t)lds_bytes(sides, pcap, nmax);
+    size_t lds = (size_t)lds_bytes(sides, pcap, nmax, chain);
     if (lds > 60 * 1024) {
       for (uint32_t id : ids) {
         R.status[id] = WC_E_LIMIT;
@@ -357,6 +362,7 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
     a.lcap = lcap;
     a.nmax = nmax;
     a.rmax = rmax;
+    a.chain = chain;
     a.out = (uint8_t*)ctx->out.p;
     a.out_stride = ob;
     a.status = (uint32_t*)ctx->status.p;
