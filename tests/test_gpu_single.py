@@ -46,3 +46,18 @@ def test_batch_matches_individual():
     got = hip.consensus_batch(probs, **cfg)
     for p, g in zip(probs, got):
         assert g == orc.consensus(p, **cfg)
+
+
+@pytest.mark.parametrize("chain", ["0", "2", "5", "16"])
+@pytest.mark.parametrize("L,N,err,seed", [(1500, 20, 0.01, 11), (800, 12, 0.04, 12), (600, 9, 0.08, 13)])
+def test_chain_length_invariance(chain, L, N, err, seed, monkeypatch):
+    """The linear-chain run-ahead (WC_CHAIN = max steps, 0 = off) must not
+    change results or work counters: every length is bit-exact vs the oracle."""
+    monkeypatch.setenv("WC_CHAIN", chain)
+    seqs = _gen(L, N, err, seed)
+    cfg = dict(min_count=max(1, N // 4))
+    exp, ec = orc.consensus(seqs, counters=True, **cfg)
+    got, gc = hip.consensus(seqs, counters=True, **cfg)
+    assert got == exp
+    for k in COUNTER_KEYS:
+        assert gc[k] == ec[k], (k, gc[k], ec[k])

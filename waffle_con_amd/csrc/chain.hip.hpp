@@ -71,30 +71,48 @@ __device__ __forceinline__ double wave_max_f64(double v) {
   return v;
 }
 
-// (B) backup wavefront rows to slot S, prefetch capacities, predict symbols.
+// (B) backup wavefront rows to slot S, stage read windows in LDS, prefetch
+// capacities, predict symbols.
 __device__ inline void chain_prepare(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int tid = threadIdx.x, lane = lane_id();
-  SideView v = E.sv(top, 0), b = E.sv(S, 0);
+  SideView v = E.sv(top, 0);
+  // windows: 64 bytes from the lowest tip, 16-byte aligned (reads are
+  // 16-byte aligned and the read buffer has 64 bytes of tail padding)
   for (uint32_t r = tid; r < E.n; r += kBlock) {
     const RRaw h = rstate_load(&E.L.hot[r]);
-    if (rraw_e(h) == kInactive) continue;
-    if (rraw_flags(h) & kWide) atomicOr(&ctl.chain_nochain, 1u);
-    const uint32_t W = 2 * rraw_e(h) + 1;
-    const uint4* src = reinterpret_cast<const uint4*>(v.wf + (uint64_t)r * E.wcap);
-    uint4* dst = reinterpret_cast<uint4*>(b.wf + (uint64_t)r * E.wcap);
-    for (uint32_t i = 0; i < (W + 3) / 4; ++i) dst[i] = src[i];
+    if (rraw_e(h) != kInactive && (rraw_flags(h) & kWide)) atomicOr(&ctl.chain_nochain, 1u);
+    Front f;
+    front_load(h, f);
+    uint32_t lo = kInactive;
+    if (f.e != kInactive) {
+      const uint32_t blen = E.rlen(r);
+#pragma unroll
+      for (int k = 0; k < kF; ++k)
+        if ((f.mask >> k) & 1u) lo = min(lo, min(f.fd[k] + f.e - f.fi[k], blen));
+    }
+    if (lo == kInactive) lo = 0;
+    const uint32_t wb = lo & ~15u;
+    const uint4* g = reinterpret_cast<const uint4*>(E.read(r) + wb);
+    uint4* w = reinterpret_cast<uint4*>(E.L.cwin + (uint64_t)r * 64);
+    const uint4 a0 = g[0], a1 = g[1], a2 = g[2], a3 = g[3];
+    w[0] = a0;
+    w[1] = a1;
+    w[2] = a2;
+    w[3] = a3;
+    E.L.cwb[r] = wb;
   }
   const uint32_t* pc = E.trk + (E.lcap + 2);  // PQueueTracker processed counts
   for (uint32_t j = tid; j <= K; j += kBlock) E.L.cpc[j] = (j >= 1) ? pc[L0 + j] : 0u;
+  __syncthreads();
   if (wave_id() == 0) {
     // upcoming bases of each read's first tip (reads 0..63)
     uint32_t bo_tip = kInactive, blen = 0;
-    const uint8_t* rd = nullptr;
+    WindowBytes rb{nullptr, nullptr, 0};
     if ((uint32_t)lane < E.n) {
       Front f;
       front_load(rstate_load(&E.L.hot[lane]), f);
       if (f.e != kInactive) {
-        rd = E.read(lane);
+        rb = WindowBytes{E.read(lane), E.L.cwin + (uint64_t)lane * 64, E.L.cwb[lane]};
         blen = E.rlen(lane);
 #pragma unroll
         for (int k = kF - 1; k >= 0; --k)
@@ -106,7 +124,7 @@ __device__ inline void chain_prepare(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
     }
     for (uint32_t t = 1; t < K; ++t) {
       const uint32_t p = bo_tip + t;
-      const uint32_t x = (bo_tip != kInactive && p < blen) ? (uint32_t)rd[p] : 0x100u;
+      const uint32_t x = (bo_tip != kInactive && p < blen) ? rb(p) : 0x100u;
       // plurality of x over the wave (ties: the first-seen symbol)
       uint64_t rem = ballot(x != 0x100u);
       uint32_t best = 0x100u, bestc = 0;
@@ -135,9 +153,10 @@ __device__ inline void chain_prepare(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
 }
 
 // (C) push the K predicted symbols through every read, thread per read.
-// kFirst: speculative pass; stores nominations and step aggregates, leaves the
-// final RStates in slot S. Replay pass: writes the final RStates to the LDS
-// copy and the last step's nominations to rinfo (the analysis cache).
+// kFirst: speculative pass; stores each step's nominations and edit
+// distances, leaves the final RStates in slot S. Replay pass: writes the final
+// RStates to the LDS copy and the last step's nominations to rinfo (the
+// analysis cache). Both passes add their work counters to ctl.chain_tot.
 template <bool kFirst>
 __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
@@ -153,26 +172,31 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
   f.off = f.maxb = f.nscmp = f.mask = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) f.fi[k] = f.fd[k] = 0;
-  const uint8_t* rd = nullptr;
+  WindowBytes rb{nullptr, nullptr, 0};
   uint32_t blen = 0;
   if (has) {
     front_load(rstate_load(&E.L.hot[r]), f);
-    rd = E.read(r);
+    rb = WindowBytes{E.read(r), E.L.cwin + (uint64_t)r * 64, E.L.cwb[r]};
     blen = E.rlen(r);
   }
   const bool active = has && f.e != kInactive;
   uint32_t* wf_row = v.wf + (uint64_t)r * E.wcap;
   RState* tmp = &E.L.ctmp[wave];
+  uint32_t t_upd = 0, t_wout = 0, t_cmp = 0;
+  WaveCounters cnt = {0, 0, 0, 0, 0};
+  uint64_t bak = 0;  // lanes whose row was backed up (wave-uniform)
   for (uint32_t j = 1; j <= K; ++j) {
     if (kFirst && j > uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
     const uint32_t sym = uni((uint32_t)E.L.cpred[j]);
     const uint32_t olen = L0 + j;
     uint32_t cmp = 0;
     bool heavy = false;
-    if (active) heavy = thread_push(f, rd, blen, olen - 1, (uint8_t)sym, wc, early, wf_row, cmp);
-    const uint32_t upd = (active && !heavy) ? 1u : 0u;
-    const uint32_t wout = upd ? 2 * f.e + 1 : 0u;
-    WaveCounters cnt = {0, 0, 0, 0, 0};
+    if (active) heavy = thread_push(f, rb, blen, olen - 1, (uint8_t)sym, wc, early, wf_row, cmp);
+    t_cmp += cmp;
+    if (active && !heavy) {
+      t_upd++;
+      t_wout += 2 * f.e + 1;
+    }
     uint64_t hm = ballot(heavy);
     while (hm) {  // edit-distance increase: the wave works on one read at a time
       const int l = __builtin_ctzll(hm);
@@ -180,6 +204,22 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
       if (lane == l) front_store(tmp, f);
       wave_lds_sync();
       const uint32_t rl = (uint32_t)wave * 64 + (uint32_t)l;
+      if (kFirst && !((bak >> l) & 1ull)) {
+        // first rewrite of this row in the chain: keep a copy in slot S (the
+        // rows are otherwise only touched at frontier diagonals, which a
+        // rollback restores from the node's LDS RStates)
+        const uint32_t W0 = 2 * tmp->e + 1;
+        const uint32_t* src = v.wf + (uint64_t)rl * E.wcap;
+        uint32_t* dst = E.sv(S, 0).wf + (uint64_t)rl * E.wcap;
+        for (uint32_t i = lane; i < W0; i += 64) dst[i] = src[i];
+        if (lane == 0) {
+          const uint32_t k = atomicAdd(&ctl.chain_nbak, 1u);
+          E.L.list[2 * k] = rl;
+          E.L.list[2 * k + 1] = W0;
+        }
+        bak |= 1ull << l;
+        __threadfence_block();
+      }
       uint32_t e_out = 0;
       const bool ok = wave_heavy(tmp, v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, olen,
                                  (uint8_t)sym, wc, early, E.wcap, cnt, e_out);
@@ -187,7 +227,7 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
       if (!ok && lane == 0) atomicMin(&ctl.chain_stop, j - 1);
       if (lane == l) {
         const RRaw t = rstate_load(tmp);
-        if (rraw_flags(t) & kWide) atomicMin(&ctl.chain_stop, j - 1);  // not a thread-path state
+        if (kFirst && (rraw_flags(t) & kWide)) atomicMin(&ctl.chain_stop, j - 1);  // not a thread-path state
         front_load(t, f);
       }
       wave_lds_sync();
@@ -195,42 +235,29 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
     Nom o;
     o.sym = o.occ = 0;
     o.n = o.split = o.end = 0;
-    if (active) o = thread_nominate(f, rd, blen, olen);
+    if (active) o = thread_nominate(f, rb, blen, olen);
     if (kFirst) {
-      uint32_t code = 0;
-      if (active) {
-        code = kNomActive | (o.end ? kNomEnd : 0u) | (uint32_t)(o.sym & 0xFF) | (o.n == 1 ? kNomOne : 0u);
-        if (o.n > 1) {
-          const uint32_t idx = atomicAdd(&ctl.chain_novf, 1u);
-          if (idx < kChainOvf) {
-            ChainOvf& q = E.L.covf[idx];
-            q.sym = o.sym;
-            q.occ = o.occ;
-            q.split = o.split;
-            q.n = o.n;
-            code |= kNomOvf | (idx << 16);
-          } else {
-            atomicMin(&ctl.chain_stop, j - 1);
+      if (has) {
+        uint32_t code = 0;
+        if (active) {
+          code = kNomActive | (o.end ? kNomEnd : 0u) | (uint32_t)(o.sym & 0xFF) | (o.n == 1 ? kNomOne : 0u);
+          if (o.n > 1) {
+            const uint32_t idx = atomicAdd(&ctl.chain_novf, 1u);
+            if (idx < kChainOvf) {
+              ChainOvf& q = E.L.covf[idx];
+              q.sym = o.sym;
+              q.occ = o.occ;
+              q.split = o.split;
+              q.n = o.n;
+              code |= kNomOvf | (idx << 16);
+            } else {
+              atomicMin(&ctl.chain_stop, j - 1);
+            }
           }
+          if (f.e >= 0xFFFFu) atomicMin(&ctl.chain_stop, j - 1);
         }
-      }
-      if (has) E.L.cnom[j * E.nmax + r] = code;
-      const uint64_t cost = active ? cost_of(f.e, cfg.cost_mode) : 0ull;
-      const uint64_t s_cost = wave_sum_u64(cost);
-      const uint32_t s_end = (uint32_t)__popcll((unsigned long long)ballot(active && o.end));
-      const bool s_multi = ballot(active && o.n > 1) != 0;
-      const uint32_t s_upd = (uint32_t)__popcll((unsigned long long)ballot(upd != 0)) + cnt.updates;
-      const uint32_t s_wout = wave_sum_u32(wout) + cnt.w_out;
-      const uint32_t s_cmp = wave_sum_u32(cmp) + cnt.compares;
-      if (lane == 0) {
-        ChainStep& st = E.L.cstep[j];
-        atomicAdd((unsigned long long*)&st.cost, (unsigned long long)s_cost);
-        if (s_end) atomicAdd(&st.n_end, s_end);
-        if (s_multi) atomicOr(&st.multi, 1u);
-        atomicAdd(&st.upd, s_upd);
-        atomicAdd(&st.wout, s_wout);
-        atomicAdd(&st.cmp, s_cmp);
-        if (cnt.edinc) atomicAdd(&st.edinc, cnt.edinc);
+        E.L.cnom[j * E.nmax + r] = code;
+        E.L.ce[j * E.nmax + r] = (uint16_t)min(f.e, 0xFFFFu);
       }
     } else if (j == K && has) {
       rinfo_store(&E.L.rinfo[r], o, f.e);
@@ -240,28 +267,58 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
     if (kFirst) front_store(&E.sv(S, 0).rs[r], f);
     else front_store(&E.L.hot[r], f);
   }
+  const uint32_t s_upd = wave_sum_u32(t_upd) + cnt.updates;
+  const uint32_t s_wout = wave_sum_u32(t_wout) + cnt.w_out;
+  const uint32_t s_cmp = wave_sum_u32(t_cmp) + cnt.compares;
+  if (lane == 0) {
+    atomicAdd((unsigned long long*)&ctl.chain_tot[0], (unsigned long long)s_upd);
+    atomicAdd((unsigned long long*)&ctl.chain_tot[1], (unsigned long long)s_wout);
+    atomicAdd((unsigned long long*)&ctl.chain_tot[2], (unsigned long long)s_cmp);
+    atomicAdd((unsigned long long*)&ctl.chain_tot[3], (unsigned long long)cnt.edinc);
+  }
 }
 
-// (D) votes of the chain nodes N_1..N_{K-1}: ok[j] = exactly one passing
-// candidate and it is the predicted symbol j+1 (consensus.rs:283-321).
+// (D) per chain node N_j (j <= K): cost, end count and multi flag; for
+// j < K also the votes: ok[j] = exactly one passing candidate and it is the
+// predicted symbol j+1 (consensus.rs:283-321).
 __device__ inline void chain_votes(Eng& E, Ctl& ctl, uint32_t K) {
   const int lane = lane_id();
   const DevConfig& cfg = E.A->cfg;
-  for (uint32_t j = 1 + wave_id(); j < K; j += kWaves) {
+  for (uint32_t j = 1 + wave_id(); j <= K; j += kWaves) {
     const uint32_t* nom = E.L.cnom + j * E.nmax;
-    const bool multi = E.L.cstep[j].multi != 0;
-    uint32_t m = 0, key = 0;
-    double val = 0.0;
-    bool ok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r); },
-                              [&](uint32_t) { return 1.0; }, E.n, false, multi, cfg.wildcard, m, key, val);
-    if (ok) {
-      const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
-      const double thr = fmin((double)cfg.min_count, max_obs);
-      const uint64_t pass = ballot((uint32_t)lane < m && val >= thr);
-      ok = __popcll((unsigned long long)pass) == 1 &&
-           (uint32_t)__builtin_amdgcn_readlane((int)key, __builtin_ctzll(pass)) == (uint32_t)E.L.cpred[j + 1];
+    const uint16_t* ce = E.L.ce + j * E.nmax;
+    uint64_t cost = 0;
+    uint32_t ends = 0;
+    bool multi = false;
+    for (uint32_t base = 0; base < E.n; base += 64) {
+      const uint32_t r = base + lane;
+      const uint32_t c = r < E.n ? nom[r] : 0u;
+      if (c & kNomActive) cost += cost_of(ce[r], cfg.cost_mode);
+      ends += (uint32_t)__popcll((unsigned long long)ballot((c & kNomEnd) != 0));
+      multi |= ballot((c & kNomOvf) != 0) != 0;
     }
-    if (lane == 0) E.L.cstep[j].ok = ok ? 1u : 0u;
+    cost = wave_sum_u64(cost);
+    bool ok = false;
+    if (j < K) {
+      uint32_t m = 0, key = 0;
+      double val = 0.0;
+      ok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r); }, [&](uint32_t) { return 1.0; },
+                           E.n, false, multi, cfg.wildcard, m, key, val);
+      if (ok) {
+        const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
+        const double thr = fmin((double)cfg.min_count, max_obs);
+        const uint64_t pass = ballot((uint32_t)lane < m && val >= thr);
+        ok = __popcll((unsigned long long)pass) == 1 &&
+             (uint32_t)__builtin_amdgcn_readlane((int)key, __builtin_ctzll(pass)) == (uint32_t)E.L.cpred[j + 1];
+      }
+    }
+    if (lane == 0) {
+      ChainStep& st = E.L.cstep[j];
+      st.cost = cost;
+      st.n_end = ends;
+      st.multi = multi ? 1u : 0u;
+      st.ok = ok ? 1u : 0u;
+    }
   }
 }
 
@@ -299,13 +356,6 @@ __device__ inline uint32_t chain_accept(Eng& E, Ctl& ctl, uint32_t L0, uint32_t 
   ctl.trk_thr[0] = thr;
   ctl.farthest[0] = farthest;
   ctl.last_constraint[0] = lcnst;
-  for (uint32_t j = 1; j <= jstar; ++j) {
-    const ChainStep& st = E.L.cstep[j];
-    ctl.cnt[S_UPDATES] += st.upd;
-    ctl.cnt[S_WOUT] += st.wout;
-    ctl.cnt[S_COMPARES] += st.cmp;
-    ctl.cnt[S_EDINC] += st.edinc;
-  }
   return jstar;
 }
 
@@ -324,6 +374,8 @@ __device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
       ctl.chain_stop = K;
       ctl.chain_novf = 0;
       ctl.chain_nochain = 0;
+      ctl.chain_nbak = 0;
+      for (int k = 0; k < 4; ++k) ctl.chain_tot[k] = 0;
       E.L.cpred[1] = (uint8_t)s1;
     }
   }
@@ -335,6 +387,7 @@ __device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
     reinterpret_cast<uint32_t*>(E.L.cstep)[i] = 0;
   chain_prepare(E, ctl, top, L0, K, S);
   __syncthreads();
+  PH_MARK(8);
   if (uni(ctl.chain_nochain)) {
     if (tid == 0) E.L.freestack[ctl.nfree++] = S;
     __syncthreads();
@@ -342,11 +395,24 @@ __device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
   }
   chain_walk<true>(E, ctl, top, L0, K, S);
   __syncthreads();
+  PH_MARK(9);
   const uint32_t Keff = uni(ctl.chain_stop);
   chain_votes(E, ctl, Keff);
   __syncthreads();
-  if (tid == 0) ctl.chain_len = chain_accept(E, ctl, L0, Keff);
+  PH_MARK(10);
+  if (tid == 0) {
+    const uint32_t js = chain_accept(E, ctl, L0, Keff);
+    ctl.chain_len = js;
+    if (js == K && Keff == K) {  // the speculative pass is the committed work
+      ctl.cnt[S_UPDATES] += ctl.chain_tot[0];
+      ctl.cnt[S_WOUT] += ctl.chain_tot[1];
+      ctl.cnt[S_COMPARES] += ctl.chain_tot[2];
+      ctl.cnt[S_EDINC] += ctl.chain_tot[3];
+    }
+    for (int k = 0; k < 4; ++k) ctl.chain_tot[k] = 0;
+  }
   __syncthreads();
+  PH_MARK(11);
   const uint32_t jstar = uni(ctl.chain_len);
   SideView v = E.sv(top, 0), b = E.sv(S, 0);
   if (jstar == K && Keff == K) {
@@ -367,20 +433,42 @@ __device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
       rinfo_store(&E.L.rinfo[r], o, rraw_e(t));
     }
   } else {
-    // restore the node's wavefront rows, then replay the accepted prefix
+    // roll the node's wavefront rows back: rows rewritten by an edit-distance
+    // increase come back from their copies, then every frontier diagonal of
+    // the node gets its value from the node's RState (the only entries the
+    // thread path writes)
+    const int lane = lane_id();
+    const uint32_t nb = uni(ctl.chain_nbak);
+    for (uint32_t k = wave_id(); k < nb; k += kWaves) {
+      const uint32_t r = E.L.list[2 * k], W = E.L.list[2 * k + 1];
+      const uint32_t* src = b.wf + (uint64_t)r * E.wcap;
+      uint32_t* dst = v.wf + (uint64_t)r * E.wcap;
+      for (uint32_t i = lane; i < W; i += 64) dst[i] = src[i];
+    }
+    __syncthreads();
     for (uint32_t r = tid; r < E.n; r += kBlock) {
-      const RRaw h = rstate_load(&E.L.hot[r]);
-      if (rraw_e(h) == kInactive) continue;
-      const uint32_t W = 2 * rraw_e(h) + 1;
-      const uint4* src = reinterpret_cast<const uint4*>(b.wf + (uint64_t)r * E.wcap);
-      uint4* dst = reinterpret_cast<uint4*>(v.wf + (uint64_t)r * E.wcap);
-      for (uint32_t i = 0; i < (W + 3) / 4; ++i) dst[i] = src[i];
+      Front f;
+      front_load(rstate_load(&E.L.hot[r]), f);
+      if (f.e == kInactive) continue;
+      uint32_t* row = v.wf + (uint64_t)r * E.wcap;
+#pragma unroll
+      for (int k = 0; k < kF; ++k)
+        if ((f.mask >> k) & 1u) row[f.fi[k]] = f.fd[k];
     }
     __syncthreads();
     if (jstar > 0) chain_walk<false>(E, ctl, top, L0, jstar, S);
   }
   __syncthreads();
   if (tid == 0) {
+    if (!(jstar == K && Keff == K)) {  // the replay pass is the committed work
+      ctl.cnt[S_UPDATES] += ctl.chain_tot[0];
+      ctl.cnt[S_WOUT] += ctl.chain_tot[1];
+      ctl.cnt[S_COMPARES] += ctl.chain_tot[2];
+      ctl.cnt[S_EDINC] += ctl.chain_tot[3];
+    }
+#ifdef WC_PHASE_PROF
+    ctl.ph[15] += 1ull + ((jstar == K && Keff == K) ? (1ull << 20) : 0ull) + ((uint64_t)jstar << 40);
+#endif
     E.L.freestack[ctl.nfree++] = S;
     if (jstar > 0) {
       const ChainStep& st = E.L.cstep[jstar];

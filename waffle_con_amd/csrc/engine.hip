@@ -60,7 +60,8 @@ struct Ctl {
   uint32_t hot_slot;  // slot whose RStates are held in Lds::hot (authoritative), kNoSlot = none
   uint32_t hot_prev, hot_load;
   // linear-chain run-ahead (run_chain)
-  uint32_t chain_k, chain_slot, chain_stop, chain_novf, chain_nochain, chain_len;
+  uint32_t chain_k, chain_slot, chain_stop, chain_novf, chain_nochain, chain_len, chain_nbak;
+  uint64_t chain_tot[4];  // updates, w_out, compares, ed increases of one chain pass
   uint32_t nkeys[2];
   uint8_t keys[2][kKout];
   double vals[2][kKout];
@@ -105,6 +106,9 @@ struct Lds {
   ChainOvf* covf;
   RState* ctmp;      // [kWaves]
   uint32_t* cnom;    // [K+1][nmax]
+  uint16_t* ce;      // [K+1][nmax]
+  uint8_t* cwin;     // [nmax][64]
+  uint32_t* cwb;     // [nmax]
   uint32_t* cpc;     // [K+1]
   uint8_t* cpred;    // [K+2]
   HeapEntry* heap;
@@ -124,6 +128,9 @@ __device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32
   l.covf = nullptr;
   l.ctmp = nullptr;
   l.cnom = nullptr;
+  l.ce = nullptr;
+  l.cwin = nullptr;
+  l.cwb = nullptr;
   l.cpc = nullptr;
   l.cpred = nullptr;
   if (K) {
@@ -134,6 +141,12 @@ __device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32
     p += (uint64_t)kWaves * 64;
     l.cnom = (uint32_t*)p;
     p += align16((uint64_t)(K + 1) * nmax * 4);
+    l.ce = (uint16_t*)p;
+    p += align16((uint64_t)(K + 1) * nmax * 2);
+    l.cwin = p;
+    p += (uint64_t)nmax * 64;
+    l.cwb = (uint32_t*)p;
+    p += align16((uint64_t)nmax * 4);
     l.cpc = (uint32_t*)p;
     p += align16((uint64_t)(K + 1) * 4);
     l.cpred = p;
@@ -484,7 +497,7 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
     front_load(s, f);
     uint32_t cmp = 0;
     const bool heavy =
-        thread_push(f, rd, blen, olen - 1, (uint8_t)sym, cfg.wildcard, early, v.wf + (uint64_t)r * E.wcap, cmp);
+        thread_push(f, GlobalBytes{rd}, blen, olen - 1, (uint8_t)sym, cfg.wildcard, early, v.wf + (uint64_t)r * E.wcap, cmp);
     tc.compares += cmp;
     front_store(&dst[r], f);
     if (heavy) {
@@ -501,9 +514,9 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
       multi |= m;
     }
   }
-  PH_MARK(8);
+
   flush_thread_counters(ctl, tc);
-  PH_MARK(9);
+
   if (ends) atomicAdd(&ctl.n_end[0], ends);
   if (multi) atomicOr(&ctl.multi[0], 1u);
   if (want_cost && cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);

@@ -413,7 +413,24 @@ struct Nom {
   uint64_t occ;  // byte k = its occurrences (<= kF tips)
   uint32_t n, split, end;
 };
-__device__ inline Nom thread_nominate(const Front& f, const uint8_t* rd, uint32_t blen, uint32_t len) {
+// read byte sources for the thread-level steps
+struct GlobalBytes {
+  const uint8_t* rd;
+  __device__ __forceinline__ uint32_t operator()(uint32_t p) const { return rd[p]; }
+};
+// a 64-byte window of the read staged in LDS ([wb, wb+64)), global beyond it
+struct WindowBytes {
+  const uint8_t* rd;
+  const uint8_t* win;
+  uint32_t wb;
+  __device__ __forceinline__ uint32_t operator()(uint32_t p) const {
+    const uint32_t q = p - wb;
+    return q < 64u ? (uint32_t)win[q] : (uint32_t)rd[p];
+  }
+};
+
+template <class RB>
+__device__ inline Nom thread_nominate(const Front& f, RB rd, uint32_t blen, uint32_t len) {
   uint32_t mb = f.maxb;
   uint32_t tipsym[kF];
 #pragma unroll
@@ -422,7 +439,7 @@ __device__ inline Nom thread_nominate(const Front& f, const uint8_t* rd, uint32_
     if (f.mask & (1u << k)) {
       const uint32_t bo = f.fd[k] + f.e - f.fi[k];
       mb = max(mb, bo);
-      if (f.fd[k] + f.off == len && bo < blen) tipsym[k] = rd[bo];
+      if (f.fd[k] + f.off == len && bo < blen) tipsym[k] = rd(bo);
     }
   }
   uint64_t keys = 0;
@@ -477,7 +494,7 @@ __device__ __forceinline__ void rinfo_store(RInfo* out, const Nom& o, uint32_t e
 }
 __device__ inline void thread_analyze(const Front& f, const uint8_t* rd, uint32_t blen, uint32_t len, RInfo* out,
                                       bool& multi) {
-  const Nom o = thread_nominate(f, rd, blen, len);
+  const Nom o = thread_nominate(f, GlobalBytes{rd}, blen, len);
   rinfo_store(out, o, f.e);
   multi = o.n > 1;
 }
@@ -487,7 +504,8 @@ __device__ inline void thread_analyze(const Front& f, const uint8_t* rd, uint32_
 // by one or become stuck; everything else is unchanged. Returns true when the
 // read needs the wave path: the ED-increase loop (dynamic_wfa.rs:84-91).
 // `cmp` receives the compares the reference extend makes.
-__device__ inline bool thread_push(Front& f, const uint8_t* rd, uint32_t blen, uint32_t old_len, uint8_t sym, int wc,
+template <class RB>
+__device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_len, uint8_t sym, int wc,
                                    bool early, uint32_t* wf_row, uint32_t& cmp) {
   uint32_t x[kF];
 #pragma unroll
@@ -495,7 +513,7 @@ __device__ inline bool thread_push(Front& f, const uint8_t* rd, uint32_t blen, u
     x[k] = 0x100;
     if (f.mask & (1u << k)) {
       const uint32_t bo = f.fd[k] + f.e - f.fi[k];
-      if (f.fd[k] + f.off == old_len && bo < blen) x[k] = rd[bo];
+      if (f.fd[k] + f.off == old_len && bo < blen) x[k] = rd(bo);
     }
   }
   uint32_t c = f.nscmp;

@@ -167,13 +167,18 @@ struct ChainOvf {  // nominations of a read with >= 2 distinct tip symbols
   uint64_t sym, occ;  // bytes in iteration order
   uint32_t split, n;
 };
-// chain LDS: steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[K+1][nmax] u32 | pc[K+1] u32 | pred[K+2] u8
+// chain LDS: steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[K+1][nmax] u32 |
+//            ce[K+1][nmax] u16 (edit distances) | win[nmax][64] (read windows) | wb[nmax] u32 |
+//            pc[K+1] u32 | pred[K+2] u8
 __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K) {
   if (K == 0) return 0;
   uint64_t t = align16((uint64_t)(K + 1) * sizeof(ChainStep));
   t += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
   t += (uint64_t)kWaves * 64;
   t += align16((uint64_t)(K + 1) * nmax * 4);
+  t += align16((uint64_t)(K + 1) * nmax * 2);
+  t += (uint64_t)nmax * 64;
+  t += align16((uint64_t)nmax * 4);
   t += align16((uint64_t)(K + 1) * 4);
   t += align16((uint64_t)(K + 2));
   return t;

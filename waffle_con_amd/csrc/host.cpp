@@ -186,7 +186,9 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; ++i)
     for (uint32_t r = 0; r < problems[i].n_reads; ++r) total += (problems[i].lens[r] + 15) & ~15ull;
-  std::vector<uint8_t> h(std::max<uint64_t>(total, 16));
+  // reads start 16-byte aligned; 64 bytes of tail padding let the engine load
+  // 64-byte windows with 16-byte accesses anywhere inside a read
+  std::vector<uint8_t> h(total + 64);
   uint64_t pos = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const wc_problem& p = problems[i];
@@ -1033,7 +1035,9 @@ int wc_dwfa_batch(wc_ctx* ctx, uint32_t n, wc_dwfa_job* jobs) {
     woff[i] = total;
     total += (jobs[i].wf_cap * 4 + 15) & ~15ull;
   }
-  std::vector<uint8_t> h(std::max<uint64_t>(total, 16));
+  // reads start 16-byte aligned; 64 bytes of tail padding let the engine load
+  // 64-byte windows with 16-byte accesses anywhere inside a read
+  std::vector<uint8_t> h(total + 64);
   std::vector<DwfaDevJob> dj(n);
   for (uint32_t i = 0; i < n; ++i) {
     const wc_dwfa_job& j = jobs[i];
