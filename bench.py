@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--len", type=int, default=10000)
     ap.add_argument("--reads", type=int, default=100)
     ap.add_argument("--err", type=float, default=0.005)
-    ap.add_argument("--cpu-sample", type=int, default=256, help="loci timed on the CPU oracle (rank 0, N=1)")
+    ap.add_argument("--cpu-sample", type=int, default=1000, help="loci timed on the CPU oracle (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -95,7 +95,8 @@ def main():
 
     ctx = w.Context(local_rank)
     cfg = CdwfaConfig(min_count=a.reads // 4)
-    seeds = list(range(rank * a.loci, (rank + 1) * a.loci))
+    from waffle_con_amd.shard import shard_seeds
+    seeds = shard_seeds(a.loci, rank)
     t0 = time.perf_counter()
     loci = gen_loci(seeds, a.len, a.reads, a.err)
     gen_s = time.perf_counter() - t0
@@ -111,35 +112,25 @@ def main():
             raise RuntimeError("engine error: %s" % bad[0])
         return res, stats
 
-    def sync_barrier():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+    import torch
+    from waffle_con_amd import shard
+
+    def sync():
+        torch.cuda.synchronize()
 
     for _ in range(a.warmup):
         step()
-    sync_barrier()
-    t0 = time.perf_counter()
     kernel_ms, upd, wout, cmp = 0.0, 0, 0, 0
     last = None
-    for _ in range(a.steps):
-        last, st = step()
-        kernel_ms += st["kernel_ms"]
-        upd += st["updates"]
-        wout += st["w_out"]
-        cmp += st["compares"]
-    sync_barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed, float(upd), float(a.loci * a.steps)], dtype=torch.float64, device="cuda")
-        tmax = t.clone()
-        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:3], op=dist.ReduceOp.SUM)
-        elapsed, total_upd, total_loci = tmax[0].item(), t[1].item(), t[2].item()
-    else:
-        total_upd, total_loci = float(upd), float(a.loci * a.steps)
+    with shard.Timer(dist, sync) as tm:
+        for _ in range(a.steps):
+            last, st = step()
+            kernel_ms += st["kernel_ms"]
+            upd += st["updates"]
+            wout += st["w_out"]
+            cmp += st["compares"]
+    elapsed, total_upd, total_loci = shard.reduce_run(
+        dist, tm.elapsed, upd, a.loci * a.steps, device="cuda" if dist is not None else None)
 
     if rank != 0:
         if dist is not None:

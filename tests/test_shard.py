@@ -1,0 +1,85 @@
+"""Multi-GPU path on CPU: the loci sharding and timing reduction bench.py uses
+(waffle_con_amd/shard.py) with torch.distributed over gloo, world size 2.
+Each rank also runs the CPU oracle on its shard, which stands in for the
+per-GPU engine. The union of the rank results must equal the single-process
+run over all loci."""
+import os
+import socket
+
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from waffle_con_amd import shard  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, loci_per_rank, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import oracle_ffi as orc
+        import waffle_con_amd as w
+        seeds = shard.shard_seeds(loci_per_rank, rank)
+        with shard.Timer(dist) as tm:
+            res = {}
+            upd = 0
+            for s in seeds:
+                r, c = orc.consensus(w.generate_test(4, 200, 6, 0.02, s)[1], counters=True, min_count=2)
+                res[s] = [x["sequence"] for x in r]
+                upd += c["updates"]
+        el, tot_upd, tot_loci = shard.reduce_run(dist, tm.elapsed + rank, upd, len(seeds))
+        gathered = [None] * world
+        dist.all_gather_object(gathered, res)
+        q.put((rank, el, tm.elapsed, tot_upd, tot_loci, upd, gathered))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_helpers():
+    assert shard.shard_seeds(3, 0) == [0, 1, 2]
+    assert shard.shard_seeds(3, 2) == [6, 7, 8]
+    items = list(range(10))
+    parts = [shard.shard_items(items, r, 3) for r in range(3)]
+    assert sum(parts, []) == items and max(map(len, parts)) - min(map(len, parts)) <= 1
+    assert shard.reduce_run(None, 1.5, 10, 2) == (1.5, 10.0, 2.0)
+
+
+def test_gloo_world2_sharded_loci():
+    world, per = 2, 3
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, per, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    # every rank sees the max over ranks of its (elapsed + rank)
+    expect = max(o[2] + o[0] for o in out)
+    assert all(abs(o[1] - expect) < 1e-9 for o in out)
+    total_upd = sum(o[5] for o in out)
+    assert all(o[3] == total_upd and o[4] == world * per for o in out)
+    # disjoint shards covering seeds 0..world*per-1, equal to a single-process run
+    merged = {}
+    for d in out[0][6]:
+        assert not set(d) & set(merged)
+        merged.update(d)
+    assert sorted(merged) == list(range(world * per))
+    import oracle_ffi as orc
+    import waffle_con_amd as w
+    for s, seqs in merged.items():
+        exp = [x["sequence"] for x in orc.consensus(w.generate_test(4, 200, 6, 0.02, s)[1], min_count=2)]
+        assert seqs == exp

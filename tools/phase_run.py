@@ -1,0 +1,73 @@
+"""Where does the single engine spend its time? (run on the GPU box)
+
+Loads a phase-profiling build of the library (WAFFLE_CON_LIB, built with
+`make -C waffle_con_amd/csrc EXTRA=-DWC_PHASE_PROF OUT=../libwaffle_con_prof.so`)
+and writes, for the bench workload:
+  - shader cycles per engine phase summed over workgroups (WC_PHASES file),
+  - the per-locus work distribution (pops, updates, ED increases),
+  - the latency of the single heaviest locus run alone vs the whole batch.
+Usage: python tools/phase_run.py [--loci N] [--out gpurun_out/phases]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PHASES = {0: "pop-broadcast", 1: "analyze", 2: "finalize", 3: "votes+select", 4: "clone-copy", 5: "push-thread",
+          6: "push-heavy", 7: "heap-insert", 8: "chain-prepare", 9: "chain-walk", 10: "chain-votes",
+          11: "chain-accept", 12: "votes-wave", 13: "pop-logic", 14: "chain-total"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--loci", type=int, default=1000)
+    ap.add_argument("--len", type=int, default=10000)
+    ap.add_argument("--reads", type=int, default=100)
+    ap.add_argument("--err", type=float, default=0.005)
+    ap.add_argument("--out", default="gpurun_out/phases")
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    ph_file = os.path.join(a.out, "phases.txt")
+    if os.path.exists(ph_file):
+        os.remove(ph_file)
+    import waffle_con_amd as w
+    from waffle_con_amd.cdwfa_config import CdwfaConfig
+    cfg = CdwfaConfig(min_count=a.reads // 4)
+    loci = [w.generate_test(4, a.len, a.reads, a.err, s)[1] for s in range(a.loci)]
+    batch = w.ResidentBatch(loci)
+    batch.consensus(cfg)  # warm-up (no phase file yet)
+    os.environ["WC_PHASES"] = ph_file
+    t0 = time.perf_counter()
+    res, st = batch.consensus(cfg, per_problem=True)
+    wall = time.perf_counter() - t0
+    del os.environ["WC_PHASES"]
+    rep = {"loci": a.loci, "kernel_ms": st["kernel_ms"], "wall_s": wall, "updates": st["updates"],
+           "pops": st["pops"], "ed_increases": st["ed_increases"]}
+    with open(ph_file) as f:
+        line = f.read().strip().splitlines()[-1].split()
+    cyc = [int(x) for x in line[2:]]
+    tot = sum(cyc[k] for k in PHASES if k not in (12, 14)) or 1
+    rep["phase_share"] = {PHASES[k]: round(cyc[k] / tot, 4) for k in PHASES}
+    c15 = cyc[15]
+    rep["chains"] = {"count": c15 & 0xFFFFF, "full": (c15 >> 20) & 0xFFFFF, "accepted_steps": c15 >> 40}
+    pp = st.get("per_problem")
+    if pp:
+        pops = sorted(p["pops"] for p in pp)
+        rep["pops_min_med_max"] = [pops[0], pops[len(pops) // 2], pops[-1]]
+        heavy = max(range(len(pp)), key=lambda i: pp[i]["pops"] + pp[i]["ed_increases"])
+        one = w.ResidentBatch([loci[heavy]])
+        one.consensus(cfg)
+        _, s1 = one.consensus(cfg)
+        rep["heaviest_alone_kernel_ms"] = s1["kernel_ms"]
+        rep["heaviest_id"] = heavy
+    print(json.dumps(rep, indent=1))
+    with open(os.path.join(a.out, "report.json"), "w") as f:
+        json.dump(rep, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -25,7 +25,7 @@ class ResidentBatch:
     def __len__(self):
         return len(self._batch)
 
-    def consensus(self, config=None, return_errors=True):
+    def consensus(self, config=None, return_errors=True, per_problem=False):
         config = config or CdwfaConfig()
         L = _lib.lib()
         cfg = _lib.make_config(config)
@@ -52,7 +52,7 @@ class ResidentBatch:
                     items.append(Consensus(_lib.u8_bytes(sp, sl.value), config.consensus_cost,
                                            _lib.u64_list(cp, cl.value)))
                 out.append(items)
-            return out, _stats(res, L)
+            return out, _stats(res, L, per_problem)
         finally:
             L.wc_results_free(res)
 

@@ -43,10 +43,18 @@ def _raise_for(results, p, L):
         raise _lib.WaffleConError(L.wc_results_error(results, p).decode(), st)
 
 
-def _stats(results, L):
+def _stats(results, L, per_problem=False):
     s = _lib.WcStats()
     L.wc_results_stats(results, ctypes.byref(s))
-    return s.as_dict()
+    out = s.as_dict()
+    if per_problem:
+        pp = []
+        for p in range(L.wc_results_problems(results)):
+            q = _lib.WcStats()
+            L.wc_results_problem_stats(results, p, ctypes.byref(q))
+            pp.append(q.as_dict())
+        out["per_problem"] = pp
+    return out
 
 
 def _problems(batch):
