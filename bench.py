@@ -83,11 +83,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # torch ships its own HIP runtime next to the one the library links: torch
+    # must initialise the device first, or its later init finds no GPU
+    import torch
+    torch.cuda.init()
+    torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     import waffle_con_amd as w
@@ -112,7 +115,6 @@ def main():
             raise RuntimeError("engine error: %s" % bad[0])
         return res, stats
 
-    import torch
     from waffle_con_amd import shard
 
     def sync():

@@ -54,6 +54,12 @@ def main():
     rep["phase_share"] = {PHASES[k]: round(cyc[k] / tot, 4) for k in PHASES}
     c15 = cyc[15]
     rep["chains"] = {"count": c15 & 0xFFFFF, "full": (c15 >> 20) & 0xFFFFF, "accepted_steps": c15 >> 40}
+    # wave-0 sub-phases (cycles per chain, summed over workgroups / chains)
+    SUB = {16: "walk-push", 17: "walk-heavy", 18: "walk-nominate", 19: "walk-heavy-count(w0)", 20: "votes-fast",
+           21: "votes-exact", 23: "prepare-windows", 24: "prepare-predict", 25: "votes-exact-count(w0)"}
+    nch = max(1, rep["chains"]["count"])
+    rep["sub_cycles_per_chain"] = {SUB[k]: round(cyc[k] / nch, 1) for k in SUB if k < len(cyc)}
+    rep["block_cycles_per_chain"] = {PHASES[k]: round(cyc[k] / nch, 1) for k in (8, 9, 10, 11, 14)}
     pp = st.get("per_problem")
     if pp:
         pops = sorted(p["pops"] for p in pp)

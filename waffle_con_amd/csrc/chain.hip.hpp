@@ -36,7 +36,7 @@ constexpr uint32_t kNomEnd = 1u << 12;    // reached_baseline_end
 constexpr uint32_t kNomActive = 1u << 13; // Some(dwfa)
 constexpr uint32_t kNomOvf = 1u << 14;    // >= 2 symbols: ChainOvf[code >> 16]
 
-__device__ __forceinline__ RInfoReg nom_load(const uint32_t* nom, const ChainOvf* ovf, uint32_t r) {
+__device__ __forceinline__ RInfoReg nom_load(const Sh<uint32_t>* nom, const Sh<ChainOvf>* ovf, uint32_t r) {
   const uint32_t c = nom[r];
   RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
   if (!(c & kNomActive)) return x;
@@ -73,9 +73,10 @@ __device__ __forceinline__ double wave_max_f64(double v) {
 
 // (B) backup wavefront rows to slot S, stage read windows in LDS, prefetch
 // capacities, predict symbols.
-__device__ inline void chain_prepare(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
+__device__ inline void chain_prepare(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int tid = threadIdx.x, lane = lane_id();
   SideView v = E.sv(top, 0);
+  SUB_T0(ta);
   // windows: 64 bytes from the lowest tip, 16-byte aligned (reads are
   // 16-byte aligned and the read buffer has 64 bytes of tail padding)
   for (uint32_t r = tid; r < E.n; r += kBlock) {
@@ -92,8 +93,8 @@ __device__ inline void chain_prepare(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
     }
     if (lo == kInactive) lo = 0;
     const uint32_t wb = lo & ~15u;
-    const uint4* g = reinterpret_cast<const uint4*>(E.read(r) + wb);
-    uint4* w = reinterpret_cast<uint4*>(E.L.cwin + (uint64_t)r * 64);
+    const Gm<uint4>* g = (const Gm<uint4>*)(E.read(r) + wb);
+    Sh<uint4>* w = (Sh<uint4>*)(E.L.cwin + (uint64_t)r * 64);
     const uint4 a0 = g[0], a1 = g[1], a2 = g[2], a3 = g[3];
     w[0] = a0;
     w[1] = a1;
@@ -101,9 +102,11 @@ __device__ inline void chain_prepare(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
     w[3] = a3;
     E.L.cwb[r] = wb;
   }
-  const uint32_t* pc = E.trk + (E.lcap + 2);  // PQueueTracker processed counts
+  const Gm<uint32_t>* pc = E.trk + (E.lcap + 2);  // PQueueTracker processed counts
   for (uint32_t j = tid; j <= K; j += kBlock) E.L.cpc[j] = (j >= 1) ? pc[L0 + j] : 0u;
   __syncthreads();
+  SUB_T1(23, ta);
+  SUB_T0(tb);
   if (wave_id() == 0) {
     // upcoming bases of each read's first tip (reads 0..63)
     uint32_t bo_tip = kInactive, blen = 0;
@@ -150,67 +153,187 @@ __device__ inline void chain_prepare(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
     // (positions >= L0 are not part of the node)
     if ((uint32_t)lane >= 1 && (uint32_t)lane <= K) v.con[L0 + lane - 1] = E.L.cpred[lane];
   }
+  SUB_T1(24, tb);
 }
 
+// ---- thread-level step primitives over the LDS read window ----
+// A thread's read window: 64 bytes of its read staged in LDS from wb.
+struct Win {
+  const Sh<uint8_t>* w;
+  uint32_t wb;
+};
+// Bytes at the tip positions bo_k = d_k + e - i_k of all frontier entries.
+// The loads are unconditional (clamped into the window) so the eight LDS reads
+// issue back to back under one wait. Returns whether a tip inside the read lies
+// outside the window (the chain then stops before this step's node).
+__device__ __forceinline__ bool win_tip_bytes(const Win& W, const Front& f, uint32_t blen, uint32_t (&x)[kF]) {
+  bool oob = false;
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+    const uint32_t q = bo - W.wb;
+    const bool in = q < 64u;
+    x[k] = W.w[in ? q : 0u];
+    oob |= ((f.mask >> k) & 1u) && !in && bo < blen;
+  }
+  return oob;
+}
+// DWFALite::update's extend for one appended symbol on the frontier
+// (thread_push<kLazy> semantics), comparing against the preloaded tip bytes.
+__device__ __forceinline__ bool chain_push(Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t old_len,
+                                           uint32_t sym, int wc, bool early, Gm<uint32_t>* row, uint32_t& cmp) {
+  uint32_t c = f.nscmp, mb = 0;
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    if (!(f.mask & (1u << k))) continue;
+    const uint32_t d = f.fd[k];
+    const uint32_t bo = d + f.e - f.fi[k];
+    if (d + f.off == old_len) {
+      if (bo < blen) {
+        c++;
+        if (x[k] == sym || (wc >= 0 && x[k] == (uint32_t)(uint8_t)wc)) {
+          f.fd[k] = d + 1;
+          mb = max(mb, bo + 1);
+          continue;
+        }
+        f.nscmp++;  // stuck on a mismatch: compared (and failing) on every later push
+      }
+      row[f.fi[k]] = d;  // leaves the frontier: the row gets its final value
+      f.maxb = max(f.maxb, bo);
+      f.mask &= ~(1u << k);
+    } else {
+      mb = max(mb, bo);
+    }
+  }
+  mb = max(mb, f.maxb);
+  cmp = c;
+  return f.mask == 0 && !(early && mb == blen);
+}
+// get_extension_candidates + reached_baseline_end of one read from its
+// frontier and the bytes at its tips (thread_nominate semantics).
+__device__ __forceinline__ Nom chain_nominate(const Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t len) {
+  uint32_t mb = f.maxb;
+  uint64_t keys = 0;
+  uint32_t cnts = 0, nk = 0;
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    if (!(f.mask & (1u << k))) continue;
+    const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+    mb = max(mb, bo);
+    if (!(f.fd[k] + f.off == len && bo < blen)) continue;
+    const uint32_t s = x[k];
+    uint32_t j = 0;
+    while (j < nk && byte_at(keys, j) != s) ++j;
+    if (j == nk) {
+      keys |= (uint64_t)s << (8 * nk);
+      nk++;
+    }
+    cnts += 1u << (4 * j);
+  }
+  Nom o;
+  o.n = nk;
+  o.end = mb == blen;
+  if (nk <= 1) {
+    o.sym = keys;
+    o.occ = cnts;
+    o.split = cnts;
+    return o;
+  }
+  const uint64_t ord = fx_order_packed(nk, [&](uint32_t j) { return byte_at(keys, j); });
+  uint64_t sym = 0, occ = 0;
+  uint32_t split = 0;
+  for (uint32_t k = 0; k < nk; ++k) {
+    const uint32_t j = nib(ord, k);
+    const uint32_t c = (cnts >> (4 * j)) & 15u;
+    sym |= (uint64_t)byte_at(keys, j) << (8 * k);
+    occ |= (uint64_t)c << (8 * k);
+    split += c;
+  }
+  o.sym = sym;
+  o.occ = occ;
+  o.split = split;
+  return o;
+}
+
+// Votes in exact rational form: a read's contribution occ/split to a symbol
+// (split <= kF = 8) is an integer number of 1/840ths (840 = lcm(1..8)).
+constexpr uint32_t kVoteDen = 840;
+
 // (C) push the K predicted symbols through every read, thread per read.
-// kFirst: speculative pass; stores each step's nominations and edit
-// distances, leaves the final RStates in slot S. Replay pass: writes the final
-// RStates to the LDS copy and the last step's nominations to rinfo (the
-// analysis cache). Both passes add their work counters to ctl.chain_tot.
+// kFirst: speculative pass; stores each step's nominations and aggregates,
+// leaves the final RStates in slot S. Replay pass: writes the final RStates to
+// the LDS copy and the last step's nominations to rinfo (the analysis cache).
+// Both passes add their work counters to ctl.chain_tot. Wavefront rows are
+// written lazily (thread_push<kLazy>): only when a diagonal leaves the
+// frontier, plus one flush of the final frontier.
 template <bool kFirst>
-__device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
-  const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
-  if ((uint32_t)wave * 64 >= E.n) return;  // no reads in this wave (no barriers below)
-  const DevConfig& cfg = E.A->cfg;
+__device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
+  const int lane = lane_id(), wave = wave_id();
+  // reads are dealt round-robin over the waves (read = lane * kWaves + wave):
+  // every wave walks a quarter of the reads, so the edit-distance increases,
+  // which a wave handles one read at a time, are spread over all four
+  if ((uint32_t)wave >= E.n) return;  // no reads in this wave (no barriers below)
+  const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
   const int wc = cfg.wildcard;
   SideView v = E.sv(top, 0);
-  const uint32_t r = (uint32_t)tid;
+  const uint32_t r = (uint32_t)lane * kWaves + (uint32_t)wave;
   const bool has = r < E.n;
   Front f;
   f.e = kInactive;
   f.off = f.maxb = f.nscmp = f.mask = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) f.fi[k] = f.fd[k] = 0;
-  WindowBytes rb{nullptr, nullptr, 0};
+  Win W{E.L.cwin + (uint64_t)min(r, E.n - 1) * 64, 0};
   uint32_t blen = 0;
   if (has) {
     front_load(rstate_load(&E.L.hot[r]), f);
-    rb = WindowBytes{E.read(r), E.L.cwin + (uint64_t)r * 64, E.L.cwb[r]};
+    W.wb = E.L.cwb[r];
     blen = E.rlen(r);
   }
   const bool active = has && f.e != kInactive;
-  uint32_t* wf_row = v.wf + (uint64_t)r * E.wcap;
-  RState* tmp = &E.L.ctmp[wave];
+  Gm<uint32_t>* wf_row = v.wf + (uint64_t)r * E.wcap;
+  Sh<RState>* tmp = &E.L.ctmp[wave];
   uint32_t t_upd = 0, t_wout = 0, t_cmp = 0;
   WaveCounters cnt = {0, 0, 0, 0, 0};
   uint64_t bak = 0;  // lanes whose row was backed up (wave-uniform)
+  // this wave's share of the node cost; changes only when an edit distance grows
+  uint64_t wcost = kFirst ? wave_sum_u64(active ? cost_of(f.e, cfg.cost_mode) : 0ull) : 0ull;
+  uint32_t x[kF];  // bytes at the current tips
+  {
+    const bool oob = win_tip_bytes(W, f, blen, x) && active;
+    if (kFirst && ballot(oob) && lane == 0) atomicMin(&ctl.chain_stop, 0u);
+  }
   for (uint32_t j = 1; j <= K; ++j) {
     if (kFirst && j > uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
     const uint32_t sym = uni((uint32_t)E.L.cpred[j]);
     const uint32_t olen = L0 + j;
     uint32_t cmp = 0;
     bool heavy = false;
-    if (active) heavy = thread_push(f, rb, blen, olen - 1, (uint8_t)sym, wc, early, wf_row, cmp);
+    SUB_T0(ta);
+    if (active) heavy = chain_push(f, x, blen, olen - 1, sym, wc, early, wf_row, cmp);
     t_cmp += cmp;
     if (active && !heavy) {
       t_upd++;
       t_wout += 2 * f.e + 1;
     }
     uint64_t hm = ballot(heavy);
+    SUB_T1(16, ta);
+    SUB_CNT(19, __popcll(hm));
+    SUB_T0(tb);
     while (hm) {  // edit-distance increase: the wave works on one read at a time
       const int l = __builtin_ctzll(hm);
       hm &= hm - 1;
       if (lane == l) front_store(tmp, f);
       wave_lds_sync();
-      const uint32_t rl = (uint32_t)wave * 64 + (uint32_t)l;
+      const uint32_t rl = (uint32_t)l * kWaves + (uint32_t)wave;
       if (kFirst && !((bak >> l) & 1ull)) {
         // first rewrite of this row in the chain: keep a copy in slot S (the
         // rows are otherwise only touched at frontier diagonals, which a
         // rollback restores from the node's LDS RStates)
         const uint32_t W0 = 2 * tmp->e + 1;
-        const uint32_t* src = v.wf + (uint64_t)rl * E.wcap;
-        uint32_t* dst = E.sv(S, 0).wf + (uint64_t)rl * E.wcap;
+        const Gm<uint32_t>* src = v.wf + (uint64_t)rl * E.wcap;
+        Gm<uint32_t>* dst = E.sv(S, 0).wf + (uint64_t)rl * E.wcap;
         for (uint32_t i = lane; i < W0; i += 64) dst[i] = src[i];
         if (lane == 0) {
           const uint32_t k = atomicAdd(&ctl.chain_nbak, 1u);
@@ -221,10 +344,12 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
         __threadfence_block();
       }
       uint32_t e_out = 0;
+      const uint32_t e_in = uni(tmp->e);
       const bool ok = wave_heavy(tmp, v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, olen,
                                  (uint8_t)sym, wc, early, E.wcap, cnt, e_out);
       wave_lds_sync();
       if (!ok && lane == 0) atomicMin(&ctl.chain_stop, j - 1);
+      if (ok) wcost += cost_of(uni(e_out), cfg.cost_mode) - cost_of(e_in, cfg.cost_mode);
       if (lane == l) {
         const RRaw t = rstate_load(tmp);
         if (kFirst && (rraw_flags(t) & kWide)) atomicMin(&ctl.chain_stop, j - 1);  // not a thread-path state
@@ -232,11 +357,16 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
       }
       wave_lds_sync();
     }
+    SUB_T1(17, tb);
+    SUB_T0(tc);
+    // bytes at the new tips: this node's nominations and the next push
+    const bool oob = win_tip_bytes(W, f, blen, x) && active;
     Nom o;
     o.sym = o.occ = 0;
     o.n = o.split = o.end = 0;
-    if (active) o = thread_nominate(f, rb, blen, olen);
+    if (active) o = chain_nominate(f, x, blen, olen);
     if (kFirst) {
+      bool stop = oob;
       if (has) {
         uint32_t code = 0;
         if (active) {
@@ -244,25 +374,65 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
           if (o.n > 1) {
             const uint32_t idx = atomicAdd(&ctl.chain_novf, 1u);
             if (idx < kChainOvf) {
-              ChainOvf& q = E.L.covf[idx];
+              auto& q = E.L.covf[idx];
               q.sym = o.sym;
               q.occ = o.occ;
               q.split = o.split;
               q.n = o.n;
               code |= kNomOvf | (idx << 16);
             } else {
-              atomicMin(&ctl.chain_stop, j - 1);
+              stop = true;
             }
           }
-          if (f.e >= 0xFFFFu) atomicMin(&ctl.chain_stop, j - 1);
         }
         E.L.cnom[j * E.nmax + r] = code;
-        E.L.ce[j * E.nmax + r] = (uint16_t)min(f.e, 0xFFFFu);
+      }
+      // step aggregates: cost; reads at their end; votes for the predicted
+      // next symbol (P) and for all other symbols (O) in 1/840ths; counts of
+      // multi-symbol reads and of fractional votes for the prediction
+      const uint32_t pred = j < K ? (uint32_t)E.L.cpred[j + 1] : 0x100u;
+      uint32_t vp = 0, vo = 0;
+      bool frac = false;
+      if (active && o.n > 0) {
+        if (o.n == 1) {
+          if ((uint32_t)(o.sym & 0xFF) == pred) vp = kVoteDen;
+          else vo = kVoteDen;
+        } else {
+          const uint32_t unit = kVoteDen / o.split;
+          for (uint32_t k = 0; k < o.n; ++k) {
+            const uint32_t c = unit * (uint32_t)((o.occ >> (8 * k)) & 0xFF);
+            if ((uint32_t)((o.sym >> (8 * k)) & 0xFF) == pred) {
+              vp += c;
+              frac = true;
+            } else {
+              vo += c;
+            }
+          }
+        }
+      }
+      const uint64_t nend = (uint64_t)__popcll((unsigned long long)ballot(active && o.end));
+      const uint64_t mm = ballot(active && o.n > 1);
+      const uint64_t nmul = (uint64_t)__popcll((unsigned long long)mm);
+      const uint64_t nfrac = (uint64_t)__popcll((unsigned long long)ballot(frac));
+      uint64_t po;
+      if (mm == 0)  // every vote is 0 or one whole read: count with ballots
+        po = (uint64_t)kVoteDen * (uint64_t)__popcll((unsigned long long)ballot(vp != 0)) |
+             ((uint64_t)kVoteDen * (uint64_t)__popcll((unsigned long long)ballot(vo != 0)) << 32);
+      else
+        po = (uint64_t)wave_sum_u32(vp) | ((uint64_t)wave_sum_u32(vo) << 32);
+      if (ballot(stop) && lane == 0) atomicMin(&ctl.chain_stop, j - 1);
+      if (lane == 0) {
+        auto& st = E.L.cstep[j];
+        atomicAdd((unsigned long long*)&st.cost, (unsigned long long)wcost);
+        atomicAdd((unsigned long long*)&st.po, (unsigned long long)po);
+        atomicAdd((unsigned long long*)&st.ef, (unsigned long long)(nend | nmul << 16 | nfrac << 32));
       }
     } else if (j == K && has) {
       rinfo_store(&E.L.rinfo[r], o, f.e);
     }
+    SUB_T1(18, tc);
   }
+  if (active) front_flush(f, wf_row);  // lazy rows: write the final frontier
   if (has) {
     if (kFirst) front_store(&E.sv(S, 0).rs[r], f);
     else front_store(&E.L.hot[r], f);
@@ -278,32 +448,42 @@ __device__ inline void chain_walk(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, u
   }
 }
 
-// (D) per chain node N_j (j <= K): cost, end count and multi flag; for
-// j < K also the votes: ok[j] = exactly one passing candidate and it is the
-// predicted symbol j+1 (consensus.rs:283-321).
-__device__ inline void chain_votes(Eng& E, Ctl& ctl, uint32_t K) {
+// (D) per chain node N_j, j < K: ok[j] = exactly one passing candidate and it
+// is the predicted symbol j+1 (consensus.rs:283-321). Without a wildcard the
+// walk's exact rational vote totals (prediction vs everything else) decide
+// almost every step; the rest take the exact path (per-key f64 sums in read
+// order, hashbrown key order).
+__device__ inline void chain_votes(Eng& E, Sh<Ctl>& ctl, uint32_t K) {
   const int lane = lane_id();
-  const DevConfig& cfg = E.A->cfg;
-  for (uint32_t j = 1 + wave_id(); j <= K; j += kWaves) {
-    const uint32_t* nom = E.L.cnom + j * E.nmax;
-    const uint16_t* ce = E.L.ce + j * E.nmax;
-    uint64_t cost = 0;
-    uint32_t ends = 0;
-    bool multi = false;
-    for (uint32_t base = 0; base < E.n; base += 64) {
-      const uint32_t r = base + lane;
-      const uint32_t c = r < E.n ? nom[r] : 0u;
-      if (c & kNomActive) cost += cost_of(ce[r], cfg.cost_mode);
-      ends += (uint32_t)__popcll((unsigned long long)ballot((c & kNomEnd) != 0));
-      multi |= ballot((c & kNomOvf) != 0) != 0;
+  const DevConfig& cfg = E.cfg;
+  for (uint32_t j = 1 + wave_id(); j < K; j += kWaves) {
+    SUB_T0(ta);
+    auto& st = E.L.cstep[j];
+    const uint64_t po = st.po, ef = st.ef;
+    const uint64_t P = po & 0xFFFFFFFFull, O = po >> 32;
+    const uint32_t multi = step_nmulti(ef) ? 1u : 0u;
+    const uint64_t M = (uint64_t)kVoteDen * cfg.min_count;
+    // Exact rational votes (P, O in 1/840ths); the f64 sums of the reference
+    // differ from them by far less than 1/840, so strict inequalities carry
+    // over. Only exact ties with fractional terms need the f64 path.
+    int dec = -1;  // 1 ok, 0 not ok, -1 undecided
+    if (cfg.wildcard < 0) {
+      if (P == 0) dec = 0;  // the prediction is not a candidate
+      else if (O < P && O < M) {
+        // thr = min(min_count, max) and max = P when P < M: the prediction
+        // passes, every other key stays below the threshold
+        if (P != M || step_nfrac(ef) == 0) dec = 1;
+      }
     }
-    cost = wave_sum_u64(cost);
-    bool ok = false;
-    if (j < K) {
+    SUB_T1(20, ta);
+    SUB_T0(tb);
+    bool ok = dec == 1;
+    if (dec < 0) {
+      const Sh<uint32_t>* nom = E.L.cnom + j * E.nmax;
       uint32_t m = 0, key = 0;
       double val = 0.0;
       ok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r); }, [&](uint32_t) { return 1.0; },
-                           E.n, false, multi, cfg.wildcard, m, key, val);
+                           E.n, false, multi != 0, cfg.wildcard, m, key, val);
       if (ok) {
         const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
         const double thr = fmin((double)cfg.min_count, max_obs);
@@ -311,24 +491,20 @@ __device__ inline void chain_votes(Eng& E, Ctl& ctl, uint32_t K) {
         ok = __popcll((unsigned long long)pass) == 1 &&
              (uint32_t)__builtin_amdgcn_readlane((int)key, __builtin_ctzll(pass)) == (uint32_t)E.L.cpred[j + 1];
       }
+      SUB_CNT(25, 1);
     }
-    if (lane == 0) {
-      ChainStep& st = E.L.cstep[j];
-      st.cost = cost;
-      st.n_end = ends;
-      st.multi = multi ? 1u : 0u;
-      st.ok = ok ? 1u : 0u;
-    }
+    SUB_T1(21, tb);
+    if (lane == 0) st.ok = ok ? 1u : 0u;
   }
 }
 
 // (E) thread 0: replay the pops of N_1.. on the scalar search state
 // (consensus.rs:224-251 with the queue holding only the chain node) and
 // commit the accepted prefix. Returns j* = number of chain nodes generated.
-__device__ inline uint32_t chain_accept(Eng& E, Ctl& ctl, uint32_t L0, uint32_t Keff) {
-  const DevConfig& cfg = E.A->cfg;
+__device__ inline uint32_t chain_accept(Eng& E, Sh<Ctl>& ctl, uint32_t L0, uint32_t Keff) {
+  const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
-  uint32_t* pc = E.trk + (E.lcap + 2);
+  Gm<uint32_t>* pc = E.trk + (E.lcap + 2);
   uint32_t jstar = Keff >= 1 ? 1u : 0u;
   uint64_t thr = ctl.trk_thr[0], farthest = ctl.farthest[0], lcnst = ctl.last_constraint[0];
   for (uint32_t j = 1; j < Keff; ++j) {
@@ -340,9 +516,10 @@ __device__ inline uint32_t chain_accept(Eng& E, Ctl& ctl, uint32_t L0, uint32_t 
       t_thr++;
       t_l = 0;
     }
-    const ChainStep& st = E.L.cstep[j];
+    const auto& st = E.L.cstep[j];
     if (st.cost > ctl.max_err || L < t_thr || (uint64_t)E.L.cpc[j] >= cfg.max_capacity_per_size) break;
-    const bool reached = early ? (st.n_end == E.n) : (st.n_end > 0);
+    const uint32_t n_end = step_nend(st.ef);
+    const bool reached = early ? (n_end == E.n) : (n_end > 0);
     if (reached || !st.ok) break;
     thr = t_thr;
     lcnst = t_l + 1;
@@ -359,14 +536,17 @@ __device__ inline uint32_t chain_accept(Eng& E, Ctl& ctl, uint32_t L0, uint32_t 
   return jstar;
 }
 
+// Not inlined: the chain has its own register allocation (no spills in the
+// walk); the caller saves its live registers once per chain.
 // Run one chain from the popped node `top` (length L0, hot in LDS, queue
 // otherwise empty) whose single child symbol is s1. Returns j* (uniform); for
 // j* > 0 the chain node N_j* is in slot `top`/LDS, queued, with its
 // nominations cached; j* == 0 leaves everything as it was.
-__device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0, int s1) {
+__device__ __noinline__ uint32_t run_chain(Eng& Eref, Sh<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
+  Eng E = eng_uniform(Eref);  // scalar-register copy of the caller's context
   const int tid = threadIdx.x;
   if (tid == 0) {
-    const uint32_t K = min(E.A->chain, E.lcap - L0);
+    const uint32_t K = min(E.chain, E.lcap - L0);
     ctl.chain_k = 0;
     if (K >= 2 && ctl.nfree > 0) {
       ctl.chain_k = K;
@@ -384,7 +564,7 @@ __device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
   if (K == 0) return 0;
   const uint32_t S = uni(ctl.chain_slot);
   for (uint32_t i = tid; i < (K + 1) * (uint32_t)(sizeof(ChainStep) / 4); i += kBlock)
-    reinterpret_cast<uint32_t*>(E.L.cstep)[i] = 0;
+    ((Sh<uint32_t>*)E.L.cstep)[i] = 0;
   chain_prepare(E, ctl, top, L0, K, S);
   __syncthreads();
   PH_MARK(8);
@@ -441,8 +621,8 @@ __device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
     const uint32_t nb = uni(ctl.chain_nbak);
     for (uint32_t k = wave_id(); k < nb; k += kWaves) {
       const uint32_t r = E.L.list[2 * k], W = E.L.list[2 * k + 1];
-      const uint32_t* src = b.wf + (uint64_t)r * E.wcap;
-      uint32_t* dst = v.wf + (uint64_t)r * E.wcap;
+      const Gm<uint32_t>* src = b.wf + (uint64_t)r * E.wcap;
+      Gm<uint32_t>* dst = v.wf + (uint64_t)r * E.wcap;
       for (uint32_t i = lane; i < W; i += 64) dst[i] = src[i];
     }
     __syncthreads();
@@ -450,7 +630,7 @@ __device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
       Front f;
       front_load(rstate_load(&E.L.hot[r]), f);
       if (f.e == kInactive) continue;
-      uint32_t* row = v.wf + (uint64_t)r * E.wcap;
+      Gm<uint32_t>* row = v.wf + (uint64_t)r * E.wcap;
 #pragma unroll
       for (int k = 0; k < kF; ++k)
         if ((f.mask >> k) & 1u) row[f.fi[k]] = f.fd[k];
@@ -471,14 +651,14 @@ __device__ inline uint32_t run_chain(Eng& E, Ctl& ctl, uint32_t top, uint32_t L0
 #endif
     E.L.freestack[ctl.nfree++] = S;
     if (jstar > 0) {
-      const ChainStep& st = E.L.cstep[jstar];
+      const auto& st = E.L.cstep[jstar];
       const uint32_t clen = L0 + jstar;
       E.L.meta[top].len[0] = clen;
       E.tracker(ctl, 0).insert(clen);
       heap_push(E.L.heap, ctl.heap_n, HeapEntry{st.cost, clen, top});
       ctl.cache_slot = top;
-      ctl.cache_nend = st.n_end;
-      ctl.cache_multi = st.multi;
+      ctl.cache_nend = step_nend(st.ef);
+      ctl.cache_multi = step_nmulti(st.ef) ? 1u : 0u;
     }
   }
   __syncthreads();

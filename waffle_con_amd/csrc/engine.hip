@@ -94,84 +94,100 @@ struct Ctl {
       ctl.ph_t = _t;                                           \
     }                                                          \
   } while (0)
+// wave-0 sub-phase timers (thread 0 charges the cycles of a code span to k)
+#define SUB_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define SUB_T1(k, v)                                                          \
+  do {                                                                        \
+    if (threadIdx.x == 0) ctl.ph[(k)] += __builtin_amdgcn_s_memtime() - (v);  \
+  } while (0)
+#define SUB_CNT(k, n)                     \
+  do {                                    \
+    if (threadIdx.x == 0) ctl.ph[(k)] += (n); \
+  } while (0)
 #else
 #define PH_MARK(k) \
   do {             \
   } while (0)
+#define SUB_T0(v) \
+  do {            \
+  } while (0)
+#define SUB_T1(k, v) \
+  do {               \
+  } while (0)
+#define SUB_CNT(k, n) \
+  do {                \
+  } while (0)
 #endif
 
 struct Lds {
-  RState* hot;     // [sides][nmax] RStates of the node being expanded (single engine)
-  ChainStep* cstep;  // chain area (single engine with A.chain > 0)
-  ChainOvf* covf;
-  RState* ctmp;      // [kWaves]
-  uint32_t* cnom;    // [K+1][nmax]
-  uint16_t* ce;      // [K+1][nmax]
-  uint8_t* cwin;     // [nmax][64]
-  uint32_t* cwb;     // [nmax]
-  uint32_t* cpc;     // [K+1]
-  uint8_t* cpred;    // [K+2]
-  HeapEntry* heap;
-  uint32_t* freestack;
-  SlotMeta* meta;
-  RInfo* rinfo;    // [sides][nmax]
-  uint32_t* fe;    // [sides][nmax]
-  uint32_t* list;  // [2*nmax] work list (heavy reads / wide analyses)
+  Sh<RState>* hot;       // [sides][nmax] RStates of the node being expanded (single engine)
+  Sh<ChainStep>* cstep;  // chain area (single engine with A.chain > 0)
+  Sh<ChainOvf>* covf;
+  Sh<RState>* ctmp;      // [kWaves]
+  Sh<uint32_t>* cnom;    // [K+1][nmax]
+  Sh<uint8_t>* cwin;     // [nmax][64]
+  Sh<uint32_t>* cwb;     // [nmax]
+  Sh<uint32_t>* cpc;     // [K+1]
+  Sh<uint8_t>* cpred;    // [K+2]
+  Sh<HeapEntry>* heap;
+  Sh<uint32_t>* freestack;
+  Sh<SlotMeta>* meta;
+  Sh<RInfo>* rinfo;    // [sides][nmax]
+  Sh<uint32_t>* fe;    // [sides][nmax]
+  Sh<uint32_t>* list;  // [2*nmax] work list (heavy reads / wide analyses)
 };
 
-__device__ inline Lds carve(uint8_t* smem, uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t K) {
+__device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t K) {
   Lds l;
-  uint8_t* p = smem;
-  l.hot = (RState*)p;
+  Sh<uint8_t>* p = smem;
+  l.hot = (Sh<RState>*)p;
   p += (uint64_t)hot_sides(sides) * nmax * sizeof(RState);
-  l.cstep = (ChainStep*)p;
+  l.cstep = (Sh<ChainStep>*)p;
   l.covf = nullptr;
   l.ctmp = nullptr;
   l.cnom = nullptr;
-  l.ce = nullptr;
   l.cwin = nullptr;
   l.cwb = nullptr;
   l.cpc = nullptr;
   l.cpred = nullptr;
   if (K) {
     p += align16((uint64_t)(K + 1) * sizeof(ChainStep));
-    l.covf = (ChainOvf*)p;
+    l.covf = (Sh<ChainOvf>*)p;
     p += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
-    l.ctmp = (RState*)p;
+    l.ctmp = (Sh<RState>*)p;
     p += (uint64_t)kWaves * 64;
-    l.cnom = (uint32_t*)p;
+    l.cnom = (Sh<uint32_t>*)p;
     p += align16((uint64_t)(K + 1) * nmax * 4);
-    l.ce = (uint16_t*)p;
-    p += align16((uint64_t)(K + 1) * nmax * 2);
     l.cwin = p;
     p += (uint64_t)nmax * 64;
-    l.cwb = (uint32_t*)p;
+    l.cwb = (Sh<uint32_t>*)p;
     p += align16((uint64_t)nmax * 4);
-    l.cpc = (uint32_t*)p;
+    l.cpc = (Sh<uint32_t>*)p;
     p += align16((uint64_t)(K + 1) * 4);
     l.cpred = p;
     p += align16((uint64_t)(K + 2));
   }
-  l.heap = (HeapEntry*)p;
+  l.heap = (Sh<HeapEntry>*)p;
   p += (uint64_t)pcap * sizeof(HeapEntry);
-  l.freestack = (uint32_t*)p;
+  l.freestack = (Sh<uint32_t>*)p;
   p += align16((uint64_t)pcap * 4);
-  l.meta = (SlotMeta*)p;
+  l.meta = (Sh<SlotMeta>*)p;
   p += (uint64_t)pcap * sizeof(SlotMeta);
-  l.rinfo = (RInfo*)p;
+  l.rinfo = (Sh<RInfo>*)p;
   p += (uint64_t)sides * nmax * sizeof(RInfo);
-  l.fe = (uint32_t*)p;
+  l.fe = (Sh<uint32_t>*)p;
   p += align16((uint64_t)sides * nmax * 4);
-  l.list = (uint32_t*)p;
+  l.list = (Sh<uint32_t>*)p;
   return l;
 }
 
 // ---- priority-queue 1.x emulation (thread 0 only) ----
-__device__ inline bool prio_less(const HeapEntry& a, const HeapEntry& b) {
+template <class A, class B>
+__device__ inline bool prio_less(const A& a, const B& b) {
   if (a.cost != b.cost) return a.cost > b.cost;  // Reverse(cost)
   return a.len < b.len;
 }
-__device__ inline void heap_push(HeapEntry* h, uint32_t& n, HeapEntry e) {
+__device__ inline void heap_push(Sh<HeapEntry>* h, Sh<uint32_t>& n, HeapEntry e) {
   uint32_t pos = n++;
   while (pos > 0) {
     uint32_t parent = (pos - 1) / 2;
@@ -181,7 +197,7 @@ __device__ inline void heap_push(HeapEntry* h, uint32_t& n, HeapEntry e) {
   }
   h[pos] = e;
 }
-__device__ inline HeapEntry heap_pop(HeapEntry* h, uint32_t& n) {
+__device__ inline HeapEntry heap_pop(Sh<HeapEntry>* h, Sh<uint32_t>& n) {
   HeapEntry top = h[0];
   n--;
   h[0] = h[n];
@@ -205,10 +221,10 @@ __device__ inline HeapEntry heap_pop(HeapEntry* h, uint32_t& n) {
 
 // ---- PQueueTracker (pqueue_tracker.rs:10-144), thread 0 only ----
 struct TrackerRef {
-  uint32_t* lc;
-  uint32_t* pc;
-  uint64_t* total;
-  uint64_t* thr;
+  Gm<uint32_t>* lc;
+  Gm<uint32_t>* pc;
+  Sh<uint64_t>* total;
+  Sh<uint64_t>* thr;
   uint64_t cap;
   __device__ void insert(uint32_t v) {
     lc[v]++;
@@ -248,7 +264,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 // wave-uniform counters (lane 0 holds them)
-__device__ inline void flush_counters(Ctl& ctl, const WaveCounters& wc) {
+__device__ inline void flush_counters(Sh<Ctl>& ctl, const WaveCounters& wc) {
   if (lane_id() == 0) {
     if (wc.updates) atomicAdd((unsigned long long*)&ctl.cnt[S_UPDATES], (unsigned long long)wc.updates);
     if (wc.w_out) atomicAdd((unsigned long long*)&ctl.cnt[S_WOUT], (unsigned long long)wc.w_out);
@@ -258,7 +274,7 @@ __device__ inline void flush_counters(Ctl& ctl, const WaveCounters& wc) {
   }
 }
 // per-thread counters (every lane its own): wave-reduce, then lane 0 adds
-__device__ inline void flush_thread_counters(Ctl& ctl, WaveCounters c) {
+__device__ inline void flush_thread_counters(Sh<Ctl>& ctl, WaveCounters c) {
   c.updates = wave_sum_u32(c.updates);
   c.w_out = wave_sum_u32(c.w_out);
   c.compares = wave_sum_u32(c.compares);
@@ -273,53 +289,75 @@ __device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_read
 // per-workgroup engine context (registers)
 struct Eng {
   const EngineArgs* A;
-  uint8_t* ws;
+  DevConfig cfg;  // by value: uniform registers, not loads through A
+  uint32_t chain;
+  Gm<uint8_t>* ws;
+  const Gm<uint8_t>* rbytes;
+  const Gm<uint64_t>* roff;
+  const Gm<uint32_t>* rlenp;
   uint64_t sbytes;
   uint32_t nmax, wcap, lcap, pcap, sides, n;
-  uint32_t* trk;  // [lc0 | pc0 | lc1 | pc1], each lcap+2 u32
-  uint32_t* total_active;
-  uint32_t* active_min;
-  uint32_t* scratch;
+  Gm<uint32_t>* trk;  // [lc0 | pc0 | lc1 | pc1], each lcap+2 u32
+  Gm<uint32_t>* total_active;
+  Gm<uint32_t>* active_min;
+  Gm<uint32_t>* scratch;
   DevProblem P;
   Lds L;
   __device__ SideView sv(uint32_t slot, uint32_t side) const {
     return side_view(ws + (uint64_t)slot * sbytes, side, nmax, wcap, lcap);
   }
-  __device__ const uint8_t* read(uint32_t r) const { return A->rbytes + A->roff[P.read_begin + r]; }
-  __device__ uint32_t rlen(uint32_t r) const { return A->rlen[P.read_begin + r]; }
-  __device__ TrackerRef tracker(Ctl& ctl, int k) const {
+  __device__ const Gm<uint8_t>* read(uint32_t r) const { return rbytes + roff[P.read_begin + r]; }
+  __device__ uint32_t rlen(uint32_t r) const { return rlenp[P.read_begin + r]; }
+  __device__ TrackerRef tracker(Sh<Ctl>& ctl, int k) const {
     const uint64_t L2 = lcap + 2;
     return TrackerRef{trk + 2 * k * L2, trk + (2 * k + 1) * L2, &ctl.trk_total[k], &ctl.trk_thr[k],
-                      A->cfg.max_capacity_per_size};
+                      cfg.max_capacity_per_size};
   }
 };
 
-__device__ inline Eng make_eng(const EngineArgs& A, uint8_t* smem) {
+// Copy of an engine context into scalar registers: every field is
+// workgroup-uniform, so each 32-bit word goes through readfirstlane.
+__device__ inline Eng eng_uniform(const Eng& s) {
+  static_assert(sizeof(Eng) % 4 == 0, "Eng is copied as words");
+  Eng d;
+  const uint32_t* sp = reinterpret_cast<const uint32_t*>(&s);
+  uint32_t* dp = reinterpret_cast<uint32_t*>(&d);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(Eng) / 4); ++i) dp[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sp[i]);
+  return d;
+}
+
+__device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
   Eng E;
   E.A = &A;
+  E.cfg = A.cfg;
+  E.chain = A.chain;
+  E.rbytes = (const Gm<uint8_t>*)A.rbytes;
+  E.roff = (const Gm<uint64_t>*)A.roff;
+  E.rlenp = (const Gm<uint32_t>*)A.rlen;
   E.nmax = A.nmax;
   E.wcap = A.wcap;
   E.lcap = A.lcap;
   E.pcap = A.pcap;
   E.sides = A.sides;
-  E.ws = A.ws + (uint64_t)blockIdx.x * A.ws_stride;
+  E.ws = (Gm<uint8_t>*)A.ws + (uint64_t)blockIdx.x * A.ws_stride;
   E.sbytes = slot_bytes(A.sides, A.nmax, A.wcap, A.lcap);
-  uint32_t* t = (uint32_t*)(E.ws + (uint64_t)A.pcap * E.sbytes);
+  Gm<uint32_t>* t = (Gm<uint32_t>*)(E.ws + (uint64_t)A.pcap * E.sbytes);
   const uint32_t L2 = A.lcap + 2;
   E.trk = t;
-  uint8_t* q = E.ws + (uint64_t)A.pcap * E.sbytes + align16((uint64_t)4 * L2 * 4);
-  E.total_active = (uint32_t*)q;
+  Gm<uint8_t>* q = E.ws + (uint64_t)A.pcap * E.sbytes + align16((uint64_t)4 * L2 * 4);
+  E.total_active = (Gm<uint32_t>*)q;
   E.active_min = E.total_active + L2;
   q += align16((uint64_t)2 * L2 * 4);
-  E.scratch = (uint32_t*)q + (uint64_t)wave_id() * (A.wcap + 2);
+  E.scratch = (Gm<uint32_t>*)q + (uint64_t)wave_id() * (A.wcap + 2);
   E.L = carve(smem, A.sides, A.pcap, A.nmax, A.chain);
   return E;
 }
 
 // ---- per-problem init: free stack, trackers, root node (consensus.rs:384-403) ----
-__device__ inline void init_problem(Eng& E, Ctl& ctl) {
+__device__ inline void init_problem(Eng& E, Sh<Ctl>& ctl) {
   const int tid = threadIdx.x;
-  const DevConfig& cfg = E.A->cfg;
+  const DevConfig& cfg = E.cfg;
   if (tid == 0) {
     ctl.heap_n = 0;
     ctl.nfree = E.pcap - 1;  // slot 0 (the stack top) becomes the root
@@ -355,7 +393,7 @@ __device__ inline void init_problem(Eng& E, Ctl& ctl) {
   }
   __syncthreads();
   if (tid == 0) {
-    SlotMeta& m = E.L.meta[0];
+    auto& m = E.L.meta[0];
     m.len[0] = m.len[1] = 0;
     m.nsome[0] = E.P.n_active;
     m.nsome[1] = 0;
@@ -374,16 +412,16 @@ __device__ inline void init_problem(Eng& E, Ctl& ctl) {
 // Where a node's per-read RStates live: in its HBM slot, or (kHot) in the
 // LDS copy of the node being expanded (single engine: the popped node).
 template <bool kHot>
-__device__ __forceinline__ RState* node_rs(Eng& E, uint32_t slot, uint32_t side) {
+__device__ __forceinline__ auto node_rs(Eng& E, uint32_t slot, uint32_t side) {
   if constexpr (kHot) return E.L.hot + side * E.nmax;
   else return E.sv(slot, side).rs;
 }
 
 template <bool kHot>
-__device__ inline void analyze_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t side, uint32_t len, RInfo* out) {
+__device__ inline void analyze_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t len, Sh<RInfo>* out) {
   const int tid = threadIdx.x, lane = lane_id();
   SideView v = E.sv(slot, side);
-  const RState* rs = node_rs<kHot>(E, slot, side);
+  const auto rs = node_rs<kHot>(E, slot, side);
   if (tid == 0) ctl.nheavy = 0;
   __syncthreads();
   uint32_t ends = 0, multi = 0;
@@ -425,11 +463,11 @@ __device__ inline void analyze_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t si
 
 // ---- FINALIZE one side on scratch (the node is not modified) ----
 template <bool kHot>
-__device__ inline void finalize_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t side, uint32_t len, uint32_t* fe,
+__device__ inline void finalize_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t len, uint32_t* fe,
                                      WaveCounters& cnt) {
   const int lane = lane_id();
   SideView v = E.sv(slot, side);
-  const RState* rs = node_rs<kHot>(E, slot, side);
+  const auto rs = node_rs<kHot>(E, slot, side);
   for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
     const uint32_t e = rs[r].e;
     if (e == kInactive) {
@@ -438,7 +476,7 @@ __device__ inline void finalize_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t s
     }
     uint32_t f = 0;
     const bool ok = wave_finalize_read(v.wf + (uint64_t)r * E.wcap, e, rs[r].off, E.read(r), E.rlen(r), v.con,
-                                       len, E.A->cfg.wildcard, E.scratch, E.wcap, f, cnt);
+                                       len, E.cfg.wildcard, E.scratch, E.wcap, f, cnt);
     if (lane == 0) {
       if (!ok) atomicOr(&ctl.ovf, 4u);
       fe[r] = ok ? f : kInactive;
@@ -456,10 +494,10 @@ __device__ inline void finalize_side(Eng& E, Ctl& ctl, uint32_t slot, uint32_t s
 // kSrcHot: the parent's RStates are the LDS copy (else the slot's own);
 // kDstHot: the child's RStates go to the LDS copy (else to the slot).
 template <bool kSrcHot, bool kDstHot>
-__device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
-                                  bool want_cost, RInfo* info) {
+__device__ inline void push_sides(Eng& E, Sh<Ctl>& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
+                                  bool want_cost, Sh<RInfo>* info) {
   const int tid = threadIdx.x, lane = lane_id();
-  const DevConfig& cfg = E.A->cfg;
+  const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
   if (tid == 0) ctl.nheavy = 0;
   __syncthreads();
@@ -473,9 +511,9 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
     const uint32_t hi = it >= E.n ? 1u : 0u, r = it - hi * E.n, side = first + hi;
     const int sym = side == 0 ? s0 : s1;
     SideView v = E.sv(slot, side);
-    RState* dst = node_rs<kDstHot>(E, slot, side);
+    const auto dst = node_rs<kDstHot>(E, slot, side);
     const RRaw s = rstate_load(&node_rs<kSrcHot>(E, slot, side)[r]);
-    RInfo* out = (info && side == 0) ? &info[r] : nullptr;
+    Sh<RInfo>* out = (info && side == 0) ? &info[r] : nullptr;
     if (rraw_e(s) == kInactive) {
       if (kSrcHot != kDstHot) rstate_store(&dst[r], s);
       if (out) {
@@ -486,7 +524,7 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
       continue;
     }
     const uint32_t olen = side == 0 ? len0 : len1;
-    const uint8_t* rd = E.read(r);
+    const Gm<uint8_t>* rd = E.read(r);
     const uint32_t blen = E.rlen(r);
     if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
       if (kSrcHot != kDstHot) rstate_store(&dst[r], s);
@@ -531,8 +569,8 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
     const uint32_t olen = side == 0 ? len0 : len1;
     const int sym = side == 0 ? s0 : s1;
     uint32_t e = 0;
-    uint32_t* wf = v.wf + (uint64_t)r * E.wcap;
-    RState* dst = node_rs<kDstHot>(E, slot, side);
+    Gm<uint32_t>* wf = v.wf + (uint64_t)r * E.wcap;
+    const auto dst = node_rs<kDstHot>(E, slot, side);
     if (!wave_heavy(&dst[r], wf, E.read(r), E.rlen(r), v.con, olen, (uint8_t)sym, cfg.wildcard, early, E.wcap, cnt,
                     e)) {
       if (lane == 0) atomicOr(&ctl.ovf, 4u);
@@ -553,21 +591,21 @@ __device__ inline void push_sides(Eng& E, Ctl& ctl, uint32_t slot, int s0, int s
   PH_MARK(6);
 }
 
-__device__ inline void copy_bytes(uint8_t* d, const uint8_t* s, uint32_t len) {
+__device__ inline void copy_bytes(Gm<uint8_t>* d, const Gm<uint8_t>* s, uint32_t len) {
   const uint32_t n16 = len >> 4;
-  for (uint32_t i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+  for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((Gm<uint4>*)d)[i] = ((const Gm<uint4>*)s)[i];
   for (uint32_t i = (n16 << 4) + threadIdx.x; i < len; i += kBlock) d[i] = s[i];
 }
 
 // move the RStates of one node side between its slot and the LDS copy
 __device__ inline void hot_store(Eng& E, uint32_t slot, uint32_t side) {
-  RState* d = E.sv(slot, side).rs;
-  const RState* h = E.L.hot + side * E.nmax;
+  Gm<RState>* d = E.sv(slot, side).rs;
+  const Sh<RState>* h = E.L.hot + side * E.nmax;
   for (uint32_t r = threadIdx.x; r < E.n; r += kBlock) rstate_store(&d[r], rstate_load(&h[r]));
 }
 __device__ inline void hot_fetch(Eng& E, uint32_t slot, uint32_t side) {
-  const RState* d = E.sv(slot, side).rs;
-  RState* h = E.L.hot + side * E.nmax;
+  const Gm<RState>* d = E.sv(slot, side).rs;
+  Sh<RState>* h = E.L.hot + side * E.nmax;
   for (uint32_t r = threadIdx.x; r < E.n; r += kBlock) rstate_store(&h[r], rstate_load(&d[r]));
 }
 
@@ -578,7 +616,7 @@ template <bool kSrcHot>
 __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t dst, uint32_t sdst, uint32_t len) {
   const int tid = threadIdx.x, lane = lane_id();
   SideView a = E.sv(src, ssrc), b = E.sv(dst, sdst);
-  const RState* ars = node_rs<kSrcHot>(E, src, ssrc);
+  const auto ars = node_rs<kSrcHot>(E, src, ssrc);
   copy_bytes(b.con, a.con, len);
   if (!kSrcHot)
     for (uint32_t r = tid; r < E.n; r += kBlock) rstate_store(&b.rs[r], rstate_load(&ars[r]));
@@ -586,8 +624,8 @@ __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t d
     const uint32_t e = ars[r].e;
     if (e == kInactive) continue;
     const uint32_t W = 2 * e + 1;
-    const uint32_t* wa = a.wf + (uint64_t)r * E.wcap;
-    uint32_t* wb = b.wf + (uint64_t)r * E.wcap;
+    const Gm<uint32_t>* wa = a.wf + (uint64_t)r * E.wcap;
+    Gm<uint32_t>* wb = b.wf + (uint64_t)r * E.wcap;
     for (uint32_t i = lane; i < W; i += 64) wb[i] = wa[i];
   }
 }
@@ -599,7 +637,7 @@ __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t d
 // distinct symbols (and no weights), every contribution is exactly 1.0, so the
 // per-key sums are exact integer counts (order-independent) and are taken
 // with ballots. Weights follow get_ed_weights (dual_consensus.rs:1299-1336).
-__device__ inline double vote_weight(const RInfo* r0, const RInfo* r1, uint32_t r, bool is_dual, bool side1) {
+__device__ inline double vote_weight(const Sh<RInfo>* r0, const Sh<RInfo>* r1, uint32_t r, bool is_dual, bool side1) {
   if (!is_dual) return 1.0;
   const bool h1 = r0[r].e != kInactive, h2 = r1[r].e != kInactive;
   const double v1 = h1 ? fmax((double)r0[r].e, 0.5) : 0.0;
@@ -615,10 +653,10 @@ struct RInfoReg {
   uint64_t sym;    // sym[k] = byte k
   uint4 occ;       // occ[k] = 16-bit halves: k=0,1 in .x ... k=6,7 in .w
 };
-__device__ __forceinline__ RInfoReg rinfo_load(const RInfo* p) {
+__device__ __forceinline__ RInfoReg rinfo_load(const Sh<RInfo>* p) {
   static_assert(sizeof(RInfo) == 32, "RInfo layout");
-  const uint4 a = reinterpret_cast<const uint4*>(p)[0];
-  const uint4 b = reinterpret_cast<const uint4*>(p)[1];
+  const uint4 a = ((const Sh<uint4>*)p)[0];
+  const uint4 b = ((const Sh<uint4>*)p)[1];
   RInfoReg x;
   x.n = a.x & 0xFFu;
   x.split = a.x >> 16;
@@ -797,7 +835,7 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
 }
 
 
-__device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, const RInfo* r0, const RInfo* r1,
+__device__ inline bool wave_votes(Sh<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, const Sh<RInfo>* r0, const Sh<RInfo>* r1,
                                   uint32_t n, bool weighted, bool is_dual, bool multi, int wc) {
   const int lane = lane_id();
   const bool side1 = side == 0;
@@ -819,14 +857,14 @@ __device__ inline bool wave_votes(Ctl& ctl, uint32_t side, const RInfo* ri, cons
 #include "chain.hip.hpp"
 
 // ---- write one result record (finalized node) ----
-__device__ inline void store_record(Eng& E, Ctl& ctl, uint8_t* outp, uint32_t slot, uint32_t nsides,
+__device__ inline void store_record(Eng& E, Sh<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t slot, uint32_t nsides,
                                     const uint32_t* lens, bool is_dual) {
   const int tid = threadIdx.x;
   const uint64_t rb = result_bytes(E.sides, E.nmax, E.lcap);
-  uint8_t* rec = outp + 16 + (uint64_t)ctl.store_idx * rb;
+  Gm<uint8_t>* rec = outp + 16 + (uint64_t)ctl.store_idx * rb;
   for (uint32_t s = 0; s < E.sides; ++s) {
-    uint8_t* rcon = rec + 16 + s * align16(E.lcap);
-    uint32_t* rfe = (uint32_t*)(rec + 16 + E.sides * align16(E.lcap) + s * align16((uint64_t)E.nmax * 4));
+    Gm<uint8_t>* rcon = rec + 16 + s * align16(E.lcap);
+    Gm<uint32_t>* rfe = (Gm<uint32_t>*)(rec + 16 + E.sides * align16(E.lcap) + s * align16((uint64_t)E.nmax * 4));
     if (s < nsides) {
       SideView v = E.sv(slot, s);
       for (uint32_t i = tid; i < lens[s]; i += kBlock) rcon[i] = v.con[i];
@@ -834,7 +872,7 @@ __device__ inline void store_record(Eng& E, Ctl& ctl, uint8_t* outp, uint32_t sl
     for (uint32_t r = tid; r < E.n; r += kBlock) rfe[r] = s < nsides ? E.L.fe[s * E.nmax + r] : kInactive;
   }
   if (tid == 0) {
-    uint32_t* h = (uint32_t*)rec;
+    Gm<uint32_t>* h = (Gm<uint32_t>*)rec;
     h[0] = lens[0];
     h[1] = nsides > 1 ? lens[1] : 0;
     h[2] = is_dual ? 1u : 0u;
@@ -854,7 +892,7 @@ __device__ inline void trace_pop(const EngineArgs& A, uint32_t prob, const HeapE
   A.trace[0] = k + 1;
 }
 
-__device__ inline void finish_problem(const EngineArgs& A, Ctl& ctl, uint8_t* outp, uint32_t prob) {
+__device__ inline void finish_problem(const EngineArgs& A, Sh<Ctl>& ctl, uint8_t* outp, uint32_t prob) {
   __syncthreads();
   if (threadIdx.x == 0) {
     ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
@@ -873,12 +911,13 @@ __device__ inline void finish_problem(const EngineArgs& A, Ctl& ctl, uint8_t* ou
 // =====================================================================
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) single_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ Ctl ctl;
+  __shared__ Ctl ctl_lds;
+  Sh<Ctl>& ctl = *(Sh<Ctl>*)&ctl_lds;
   const int tid = threadIdx.x;
   const int lane = lane_id();
   const DevConfig& cfg = A.cfg;
   const bool early = cfg.early != 0;
-  Eng E = make_eng(A, smem);
+  Eng E = make_eng(A, (Sh<uint8_t>*)smem);
 
   for (;;) {
     if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
@@ -887,7 +926,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
     if (prob >= A.n_problems) break;
     E.P = A.problems[prob];
     E.n = E.P.n_reads;
-    uint8_t* outp = A.out + (uint64_t)prob * A.out_stride;
+    Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)prob * A.out_stride;
     init_problem(E, ctl);
 
     for (;;) {
@@ -1114,15 +1153,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
 // =====================================================================
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ Ctl ctl;
+  __shared__ Ctl ctl_lds;
+  Sh<Ctl>& ctl = *(Sh<Ctl>*)&ctl_lds;
   const int tid = threadIdx.x;
   const int lane = lane_id();
   const DevConfig& cfg = A.cfg;
   const bool early = cfg.early != 0;
   const bool weighted = cfg.weighted != 0;
-  Eng E = make_eng(A, smem);
-  RInfo* R0 = E.L.rinfo;
-  RInfo* R1 = E.L.rinfo + E.nmax;
+  Eng E = make_eng(A, (Sh<uint8_t>*)smem);
+  Sh<RInfo>* R0 = E.L.rinfo;
+  Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
 
   for (;;) {
     if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
@@ -1131,7 +1171,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
     if (prob >= A.n_problems) break;
     E.P = A.problems[prob];
     E.n = E.P.n_reads;
-    uint8_t* outp = A.out + (uint64_t)prob * A.out_stride;
+    Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)prob * A.out_stride;
     init_problem(E, ctl);
     const uint64_t full_min = max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.n));
 
@@ -1152,7 +1192,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
             }
           }
           HeapEntry top = heap_pop(E.L.heap, ctl.heap_n);
-          const SlotMeta& m = E.L.meta[top.slot];
+          const auto& m = E.L.meta[top.slot];
           const uint32_t dual = m.flags & 1u;
           TrackerRef t = E.tracker(ctl, dual);
           t.remove(top.len);
@@ -1332,8 +1372,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
             nc++;
           }
           // split children from every pair of sorted candidates (:682-734)
-          double* cv = ctl.srt_v;
-          uint8_t* cs = ctl.srt_s;
+          Sh<double>* cv = ctl.srt_v;
+          Sh<uint8_t>* cs = ctl.srt_s;
           uint32_t ns = 0, passing = 0;
           for (uint32_t k = 0; k < ctl.nkeys[0]; ++k) {
             if (cfg.wildcard >= 0 && ctl.keys[0][k] == (uint8_t)cfg.wildcard) continue;
@@ -1457,7 +1497,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (tid == 0) {
           if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
           else if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
-          SlotMeta& m = E.L.meta[slot];
+          auto& m = E.L.meta[slot];
           m.nsome[0] = ctl.some_acc[0];
           m.nsome[1] = ctl.some_acc[1];
           ctl.ch_cost[c] = ctl.cost_acc;
@@ -1487,19 +1527,22 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
 __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
   DwfaDevJob& j = jobs[blockIdx.x];
   const int lane = lane_id();
+  Gm<uint32_t>* wf = (Gm<uint32_t>*)j.wf;
+  const Gm<uint8_t>* base = (const Gm<uint8_t>*)j.baseline;
+  const Gm<uint8_t>* other = (const Gm<uint8_t>*)j.other;
   uint32_t e = j.e;
   WaveCounters cnt = {0, 0, 0, 0, 0};
   uint32_t status = 0;
   if (j.op == 0) {
     uint32_t mo = 0, mb = 0;
-    if (!wave_update_general(j.wf, e, j.offset, j.baseline, j.blen, j.other, j.olen, j.wildcard, j.early != 0, j.wf_cap,
+    if (!wave_update_general(wf, e, j.offset, base, j.blen, other, j.olen, j.wildcard, j.early != 0, j.wf_cap,
                              cnt, mo, mb))
       status = WC_E_LIMIT_CODE;
     else if (!(mo == j.olen || (j.early && mb == j.blen)))
       status = WC_E_INVARIANT_CODE;  // dynamic_wfa.rs:94-97 assert
   } else if (j.op == 1) {
     uint32_t W = 2 * e + 1, mb = 0;
-    for (uint32_t i = lane; i < W; i += 64) mb = max(mb, j.wf[i] + e - i);
+    for (uint32_t i = lane; i < W; i += 64) mb = max(mb, wf[i] + e - i);
     mb = wave_max_u32(mb);
     uint32_t cmp = 0;
     while (mb < j.blen) {
@@ -1507,15 +1550,16 @@ __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
         status = WC_E_LIMIT_CODE;
         break;
       }
-      wave_grow(j.wf, W);
+      wave_grow(wf, W);
       W += 2;
       e += 1;
       uint32_t mo;
-      wave_extend_all(j.wf, W, e, j.offset, j.baseline, j.blen, j.other, j.olen, j.wildcard, mo, mb, cmp);
+      wave_extend_all(wf, W, e, j.offset, base, j.blen, other, j.olen, j.wildcard, mo, mb, cmp);
     }
   } else {
-    __shared__ RInfo ri;
-    if (!wave_analyze_read(j.wf, e, j.offset, j.baseline, j.blen, j.olen, &ri)) status = WC_E_LIMIT_CODE;
+    __shared__ RInfo ri_lds;
+    Sh<RInfo>& ri = *(Sh<RInfo>*)&ri_lds;
+    if (!wave_analyze_read(wf, e, j.offset, base, j.blen, j.olen, &ri)) status = WC_E_LIMIT_CODE;
     __builtin_amdgcn_wave_barrier();
     if (lane == 0 && status == 0) {
       j.n_cand = ri.n;

@@ -13,6 +13,19 @@
 
 namespace wc {
 
+// Explicit address spaces: HBM (global) and LDS pointers compile to global_* /
+// ds_* instructions instead of flat_* (which wait on both counters and take
+// the slower path). The engines keep every pointer in one of these types.
+// (The host pass of this single-source file only parses device code; it sees
+// plain types.)
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T> using Gm = __attribute__((address_space(1))) T;
+template <class T> using Sh = __attribute__((address_space(3))) T;
+#else
+template <class T> using Gm = T;
+template <class T> using Sh = T;
+#endif
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
@@ -40,9 +53,10 @@ __device__ __forceinline__ uint64_t cost_of(uint32_t e, int mode) {
 // ascending bucket order; iteration is ascending bucket order.
 __device__ inline uint32_t fx_cap(uint32_t b) { return b == 0 ? 0 : (b < 8 ? b - 1 : b / 8 * 7); }
 __device__ inline uint32_t fx_buckets_for(uint32_t cap) { return cap < 4 ? 4 : (cap < 8 ? 8 : 16); }
+// h1 = (k * FxSEED) & (B - 1) only depends on FxSEED mod B; B <= 16 and
+// FxSEED = 0x517cc1b727220a95 = 5 (mod 16), so h1 = (5k) & (B - 1).
 __device__ inline uint64_t fx_put(uint64_t T, uint32_t B, uint32_t key, uint32_t tag) {
-  const uint64_t h = (uint64_t)(key & 0xFF) * 0x517cc1b727220a95ULL;
-  uint32_t pos = (uint32_t)h & (B - 1);
+  uint32_t pos = ((key & 0xFFu) * 5u) & (B - 1);
   for (uint32_t t = 0; t < B; ++t) {
     const uint32_t b = (pos + t) & (B - 1);
     if (((T >> (4 * b)) & 15ull) == 0) return T | ((uint64_t)tag << (4 * b));
@@ -87,16 +101,17 @@ __device__ __forceinline__ uint32_t byte_at(uint64_t x, uint32_t i) { return (ui
 
 // --- per-read DWFA views ---
 struct SideView {
-  RState* rs;    // [nmax]
-  uint32_t* wf;  // [nmax * wcap]
-  uint8_t* con;  // [lcap]
+  Gm<RState>* rs;    // [nmax]
+  Gm<uint32_t>* wf;  // [nmax * wcap]
+  Gm<uint8_t>* con;  // [lcap]
 };
 
-__device__ inline SideView side_view(uint8_t* slot_base, uint32_t side, uint32_t nmax, uint32_t wcap, uint32_t lcap) {
-  uint8_t* b = slot_base + (uint64_t)side * side_bytes(nmax, wcap, lcap);
+__device__ inline SideView side_view(Gm<uint8_t>* slot_base, uint32_t side, uint32_t nmax, uint32_t wcap,
+                                     uint32_t lcap) {
+  Gm<uint8_t>* b = slot_base + (uint64_t)side * side_bytes(nmax, wcap, lcap);
   SideView v;
-  v.rs = (RState*)b;
-  v.wf = (uint32_t*)(b + (uint64_t)nmax * sizeof(RState));
+  v.rs = (Gm<RState>*)b;
+  v.wf = (Gm<uint32_t>*)(b + (uint64_t)nmax * sizeof(RState));
   v.con = b + align16((uint64_t)nmax * sizeof(RState) + (uint64_t)nmax * wcap * 4);
   return v;
 }
@@ -106,17 +121,32 @@ __device__ inline SideView side_view(uint8_t* slot_base, uint32_t side, uint32_t
 struct RRaw {
   uint4 a, b, c, d;
 };
-__device__ __forceinline__ RRaw rstate_load(const RState* p) {
-  const uint4* q = reinterpret_cast<const uint4*>(p);
+__device__ __forceinline__ RRaw rstate_load(const Gm<RState>* p) {
+  const Gm<uint4>* q = (const Gm<uint4>*)p;
   return RRaw{q[0], q[1], q[2], q[3]};
 }
-__device__ __forceinline__ void rstate_store(RState* p, const RRaw& s) {
-  uint4* q = reinterpret_cast<uint4*>(p);
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ RRaw rstate_load(const Sh<RState>* p) {
+  const Sh<uint4>* q = (const Sh<uint4>*)p;
+  return RRaw{q[0], q[1], q[2], q[3]};
+}
+#endif
+__device__ __forceinline__ void rstate_store(Gm<RState>* p, const RRaw& s) {
+  Gm<uint4>* q = (Gm<uint4>*)p;
   q[0] = s.a;
   q[1] = s.b;
   q[2] = s.c;
   q[3] = s.d;
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void rstate_store(Sh<RState>* p, const RRaw& s) {
+  Sh<uint4>* q = (Sh<uint4>*)p;
+  q[0] = s.a;
+  q[1] = s.b;
+  q[2] = s.c;
+  q[3] = s.d;
+}
+#endif
 __device__ __forceinline__ uint32_t rraw_e(const RRaw& s) { return s.a.x; }
 __device__ __forceinline__ uint32_t rraw_flags(const RRaw& s) { return s.a.w >> 24; }
 
@@ -127,8 +157,8 @@ struct WaveCounters {
 // Full extend of every diagonal of `wf[0..W)` (dynamic_wfa.rs:109-153),
 // lanes over diagonals. Returns (via refs) wave-reduced max_other - off and
 // max_baseline. Counts byte compares as the reference loop would.
-__device__ inline void wave_extend_all(uint32_t* wf, uint32_t W, uint32_t e, uint32_t off, const uint8_t* rd,
-                                       uint32_t blen, const uint8_t* con, uint32_t olen, int wc, uint32_t& maxo,
+__device__ inline void wave_extend_all(Gm<uint32_t>* wf, uint32_t W, uint32_t e, uint32_t off, const Gm<uint8_t>* rd,
+                                       uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc, uint32_t& maxo,
                                        uint32_t& maxb, uint32_t& cmp) {
   const int lane = lane_id();
   uint32_t mo = 0, mb = 0, c = 0;
@@ -159,7 +189,7 @@ __device__ inline void wave_extend_all(uint32_t* wf, uint32_t W, uint32_t e, uin
 // increase_edit_distance in place (dynamic_wfa.rs:162-183): W -> W+2.
 // Chunks are processed from the top so a chunk never reads an entry that a
 // previously processed chunk overwrote.
-__device__ inline void wave_grow(uint32_t* wf, uint32_t Wold) {
+__device__ inline void wave_grow(Gm<uint32_t>* wf, uint32_t Wold) {
   const int lane = lane_id();
   const uint32_t Wn = Wold + 2;
   for (int base = (int)((Wn - 1) / 64) * 64; base >= 0; base -= 64) {
@@ -182,8 +212,8 @@ __device__ inline void wave_grow(uint32_t* wf, uint32_t Wold) {
 // mismatch / read end as in the previous extend, so it is only counted, not
 // re-compared. Then the ED-increase loop of dynamic_wfa.rs:84-91.
 // Returns false on wavefront capacity overflow.
-__device__ inline bool wave_push_read(uint32_t* wf, uint32_t& e, uint32_t off, const uint8_t* rd, uint32_t blen,
-                                      const uint8_t* con, uint32_t olen, uint8_t sym, int wc, bool early,
+__device__ inline bool wave_push_read(Gm<uint32_t>* wf, uint32_t& e, uint32_t off, const Gm<uint8_t>* rd,
+                                      uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, uint8_t sym, int wc, bool early,
                                       uint32_t wcap, WaveCounters& cnt) {
   const int lane = lane_id();
   uint32_t W = 2 * e + 1;
@@ -229,8 +259,8 @@ __device__ inline bool wave_push_read(uint32_t* wf, uint32_t& e, uint32_t off, c
 
 // General DWFALite::update (other may have grown by any amount):
 // dynamic_wfa.rs:75-99 with a full extend first.
-__device__ inline bool wave_update_general(uint32_t* wf, uint32_t& e, uint32_t off, const uint8_t* rd, uint32_t blen,
-                                           const uint8_t* con, uint32_t olen, int wc, bool early, uint32_t wcap,
+__device__ inline bool wave_update_general(Gm<uint32_t>* wf, uint32_t& e, uint32_t off, const Gm<uint8_t>* rd,
+                                           uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc, bool early, uint32_t wcap,
                                            WaveCounters& cnt, uint32_t& mo, uint32_t& mb) {
   uint32_t W = 2 * e + 1, cmp = 0;
   wave_extend_all(wf, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
@@ -252,8 +282,9 @@ __device__ inline bool wave_update_general(uint32_t* wf, uint32_t& e, uint32_t o
 
 // DWFALite::finalize (dynamic_wfa.rs:201-210) on a scratch copy of the
 // wavefront; the node itself is untouched (the reference finalizes a clone).
-__device__ inline bool wave_finalize_read(const uint32_t* wf, uint32_t e, uint32_t off, const uint8_t* rd,
-                                          uint32_t blen, const uint8_t* con, uint32_t olen, int wc, uint32_t* scratch,
+__device__ inline bool wave_finalize_read(const Gm<uint32_t>* wf, uint32_t e, uint32_t off, const Gm<uint8_t>* rd,
+                                          uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc,
+                                          Gm<uint32_t>* scratch,
                                           uint32_t wcap, uint32_t& e_out, WaveCounters& cnt) {
   const int lane = lane_id();
   uint32_t W = 2 * e + 1;
@@ -289,8 +320,8 @@ __device__ inline bool wave_finalize_read(const uint32_t* wf, uint32_t e, uint32
 // first-appearance order (ascending diagonal), then permuted into FxHashMap
 // iteration order. Keys/counts are wave-uniform packed registers. Returns
 // false when more than kKmax distinct symbols sit at the tips.
-__device__ inline bool wave_analyze_read(const uint32_t* wf, uint32_t e, uint32_t off, const uint8_t* rd,
-                                         uint32_t blen, uint32_t olen, RInfo* out) {
+__device__ inline bool wave_analyze_read(const Gm<uint32_t>* wf, uint32_t e, uint32_t off, const Gm<uint8_t>* rd,
+                                         uint32_t blen, uint32_t olen, Sh<RInfo>* out) {
   const int lane = lane_id();
   const uint32_t W = 2 * e + 1;
   uint64_t keys = 0, cnt_lo = 0, cnt_hi = 0;  // 8 keys (bytes), 8 x 16-bit counts
@@ -387,7 +418,8 @@ __device__ __forceinline__ void front_load(const RRaw& s, Front& f) {
   f.fd[7] = s.d.w;
 }
 // write the compacted frontier back (memory stores at computed positions)
-__device__ __forceinline__ void front_store(RState* p, const Front& f) {
+template <class P>
+__device__ __forceinline__ void front_store(P p, const Front& f) {
   uint32_t n = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
@@ -415,13 +447,13 @@ struct Nom {
 };
 // read byte sources for the thread-level steps
 struct GlobalBytes {
-  const uint8_t* rd;
+  const Gm<uint8_t>* rd;
   __device__ __forceinline__ uint32_t operator()(uint32_t p) const { return rd[p]; }
 };
 // a 64-byte window of the read staged in LDS ([wb, wb+64)), global beyond it
 struct WindowBytes {
-  const uint8_t* rd;
-  const uint8_t* win;
+  const Gm<uint8_t>* rd;
+  const Sh<uint8_t>* win;
   uint32_t wb;
   __device__ __forceinline__ uint32_t operator()(uint32_t p) const {
     const uint32_t q = p - wb;
@@ -481,19 +513,19 @@ __device__ inline Nom thread_nominate(const Front& f, RB rd, uint32_t blen, uint
   return o;
 }
 // RInfo from a nomination: two 16-byte stores
-__device__ __forceinline__ void rinfo_store(RInfo* out, const Nom& o, uint32_t e) {
+__device__ __forceinline__ void rinfo_store(Sh<RInfo>* out, const Nom& o, uint32_t e) {
   static_assert(sizeof(RInfo) == 32, "RInfo layout");
   const uint32_t o16[4] = {
       (uint32_t)(o.occ & 0xFF) | (uint32_t)((o.occ >> 8) & 0xFF) << 16,
       (uint32_t)((o.occ >> 16) & 0xFF) | (uint32_t)((o.occ >> 24) & 0xFF) << 16,
       (uint32_t)((o.occ >> 32) & 0xFF) | (uint32_t)((o.occ >> 40) & 0xFF) << 16,
       (uint32_t)((o.occ >> 48) & 0xFF) | (uint32_t)((o.occ >> 56) & 0xFF) << 16};
-  uint4* q = reinterpret_cast<uint4*>(out);
+  Sh<uint4>* q = (Sh<uint4>*)out;
   q[0] = make_uint4(o.n | (o.end << 8) | (o.split << 16), (uint32_t)o.sym, (uint32_t)(o.sym >> 32), o16[0]);
   q[1] = make_uint4(o16[1], o16[2], o16[3], e);
 }
-__device__ inline void thread_analyze(const Front& f, const uint8_t* rd, uint32_t blen, uint32_t len, RInfo* out,
-                                      bool& multi) {
+__device__ inline void thread_analyze(const Front& f, const Gm<uint8_t>* rd, uint32_t blen, uint32_t len,
+                                      Sh<RInfo>* out, bool& multi) {
   const Nom o = thread_nominate(f, GlobalBytes{rd}, blen, len);
   rinfo_store(out, o, f.e);
   multi = o.n > 1;
@@ -504,9 +536,13 @@ __device__ inline void thread_analyze(const Front& f, const uint8_t* rd, uint32_
 // by one or become stuck; everything else is unchanged. Returns true when the
 // read needs the wave path: the ED-increase loop (dynamic_wfa.rs:84-91).
 // `cmp` receives the compares the reference extend makes.
-template <class RB>
+// kLazy (linear-chain walk): the row is not written when a tip advances, only
+// when a diagonal leaves the frontier; front_flush writes the final frontier.
+// Between the two, RState (not the row) is authoritative for frontier
+// diagonals, so the hot loop issues no global stores.
+template <bool kLazy = false, class RB>
 __device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_len, uint8_t sym, int wc,
-                                   bool early, uint32_t* wf_row, uint32_t& cmp) {
+                                   bool early, Gm<uint32_t>* wf_row, uint32_t& cmp) {
   uint32_t x[kF];
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
@@ -528,12 +564,13 @@ __device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_
         c++;
         if (x[k] == sym || (wc >= 0 && x[k] == (uint32_t)(uint8_t)wc)) {
           f.fd[k] = d + 1;
-          wf_row[f.fi[k]] = d + 1;
+          if (!kLazy) wf_row[f.fi[k]] = d + 1;
           mb = max(mb, bo + 1);
           continue;
         }
         f.nscmp++;  // stuck on a mismatch: compared (and failing) on every later push
       }
+      if (kLazy) wf_row[f.fi[k]] = d;
       f.maxb = max(f.maxb, bo);
       f.mask &= ~(1u << k);
     } else {
@@ -545,9 +582,17 @@ __device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_
   return f.mask == 0 && !(early && mb == blen);
 }
 
+// write the frontier diagonals back into the wavefront row (end of a lazy walk)
+__device__ __forceinline__ void front_flush(const Front& f, Gm<uint32_t>* wf_row) {
+#pragma unroll
+  for (int k = 0; k < kF; ++k)
+    if (f.mask & (1u << k)) wf_row[f.fi[k]] = f.fd[k];
+}
+
 // Rebuild an RState from the authoritative wavefront (one wave).
-__device__ inline void wave_rebuild(const uint32_t* wf, uint32_t e, uint32_t off, uint32_t blen, uint32_t len,
-                                    RState* out) {
+template <class P>
+__device__ inline void wave_rebuild(const Gm<uint32_t>* wf, uint32_t e, uint32_t off, uint32_t blen, uint32_t len,
+                                    P out) {
   const int lane = lane_id();
   const uint32_t W = 2 * e + 1;
   uint32_t nf = 0, mb = 0, nsc = 0;
@@ -585,8 +630,9 @@ __device__ inline void wave_rebuild(const uint32_t* wf, uint32_t e, uint32_t off
 // full-scan push for a wide frontier, otherwise the ED-increase loop from the
 // post-extend wavefront; then rebuild the RState. Returns false on wavefront
 // capacity overflow.
-__device__ inline bool wave_heavy(RState* rsp, uint32_t* wf, const uint8_t* rd, uint32_t blen, const uint8_t* con,
-                                  uint32_t olen, uint8_t sym, int wc, bool early, uint32_t wcap, WaveCounters& cnt,
+template <class P>
+__device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
+                                  const Gm<uint8_t>* con, uint32_t olen, uint8_t sym, int wc, bool early, uint32_t wcap, WaveCounters& cnt,
                                   uint32_t& e_out) {
   const uint32_t flags = rsp->flags;
   uint32_t e = rsp->e;

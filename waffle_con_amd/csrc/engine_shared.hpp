@@ -90,7 +90,7 @@ struct EngineArgs {
   uint32_t _pad2;
   unsigned long long* phases;  // debug (WC_PHASE_PROF builds): shader cycles per phase, kPhases
 };
-constexpr int kPhases = 16;
+constexpr int kPhases = 32;  // 0..15 block phases, 16..31 wave-0 sub-phases
 
 // ---- byte layouts (host and device compute them identically) ----
 __host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
@@ -159,24 +159,28 @@ struct RInfo {
 // ---- linear-chain run-ahead (single engine, engine.hip run_chain) ----
 constexpr uint32_t kChainMax = 16;   // steps per chain
 constexpr uint32_t kChainOvf = 192;  // multi-symbol nominations stored per chain
-struct ChainStep {                   // aggregates of one speculative step (node N_j)
-  uint64_t cost;
-  uint32_t n_end, multi, upd, wout, cmp, edinc, ok, pad;
+struct ChainStep {  // aggregates of one speculative step (node N_j), LDS atomics (one per wave)
+  uint64_t cost;    // sum of the reads' costs
+  uint64_t po;      // votes in 1/840ths: for the predicted next symbol [0,32), for other symbols [32,64)
+  uint64_t ef;      // reads at their end [0,16) | multi-symbol reads [16,32) | fractional pred votes [32,48)
+  uint32_t ok, pad;
 };
+static_assert(sizeof(ChainStep) == 32, "ChainStep layout");
+__host__ __device__ inline uint32_t step_nend(uint64_t ef) { return (uint32_t)(ef & 0xFFFFu); }
+__host__ __device__ inline uint32_t step_nmulti(uint64_t ef) { return (uint32_t)((ef >> 16) & 0xFFFFu); }
+__host__ __device__ inline uint32_t step_nfrac(uint64_t ef) { return (uint32_t)((ef >> 32) & 0xFFFFu); }
 struct ChainOvf {  // nominations of a read with >= 2 distinct tip symbols
   uint64_t sym, occ;  // bytes in iteration order
   uint32_t split, n;
 };
 // chain LDS: steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[K+1][nmax] u32 |
-//            ce[K+1][nmax] u16 (edit distances) | win[nmax][64] (read windows) | wb[nmax] u32 |
-//            pc[K+1] u32 | pred[K+2] u8
+//            win[nmax][64] (read windows) | wb[nmax] u32 | pc[K+1] u32 | pred[K+2] u8
 __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K) {
   if (K == 0) return 0;
   uint64_t t = align16((uint64_t)(K + 1) * sizeof(ChainStep));
   t += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
   t += (uint64_t)kWaves * 64;
   t += align16((uint64_t)(K + 1) * nmax * 4);
-  t += align16((uint64_t)(K + 1) * nmax * 2);
   t += (uint64_t)nmax * 64;
   t += align16((uint64_t)nmax * 4);
   t += align16((uint64_t)(K + 1) * 4);
