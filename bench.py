@@ -19,6 +19,7 @@ Multi-GPU: one process per GPU (torch.distributed.run); loci are sharded
 Rank 0 prints one JSON line.
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -122,6 +123,11 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    # the setup (torch, 1000 loci of reads) leaves a large Python heap: move it
+    # to the permanent generation so a full collection inside the timed region
+    # does not traverse it
+    gc.collect()
+    gc.freeze()
     kernel_ms, upd, wout, cmp = 0.0, 0, 0, 0
     last = None
     with shard.Timer(dist, sync) as tm:

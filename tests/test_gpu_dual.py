@@ -8,13 +8,8 @@ import ref_cases as rc
 pytestmark = pytest.mark.gpu
 hip = pytest.importorskip("hip_runner")
 
-OFFSET_CASES = {"offset_windows", "offset_gap_err"}
-
-
 @pytest.mark.parametrize("name", sorted(rc.DUAL_CASES))
 def test_reference_dual(name):
-    if name in OFFSET_CASES:
-        pytest.xfail("device activation (add_sequence_offset) lands in a later milestone")
     rc.check_dual(rc.DUAL_CASES[name], hip)
 
 
@@ -27,11 +22,17 @@ def test_reference_priority(name):
 def test_dual_vs_oracle_full_equality(name):
     """Beyond the reference's PartialEq: scores1/scores2 and work counters too."""
     case = rc.DUAL_CASES[name]
-    if name in OFFSET_CASES:
-        pytest.skip("offset activation")
     seqs = [rc.b(s) for s in case["seqs"]]
-    exp, ec = orc.dual_consensus(seqs, counters=True, **case["cfg"])
-    got, gc = hip.dual_consensus(seqs, counters=True, **case["cfg"])
+    offs = case.get("offsets")
+    if "error" in case:
+        with pytest.raises(Exception) as eo:
+            orc.dual_consensus(seqs, offsets=offs, **case["cfg"])
+        with pytest.raises(Exception) as eh:
+            hip.dual_consensus(seqs, offsets=offs, **case["cfg"])
+        assert str(eh.value) == str(eo.value)
+        return
+    exp, ec = orc.dual_consensus(seqs, offsets=offs, counters=True, **case["cfg"])
+    got, gc = hip.dual_consensus(seqs, offsets=offs, counters=True, **case["cfg"])
     assert got == exp
     for k in ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
               "nodes_ignored", "peak_queue_size"):

@@ -9,13 +9,8 @@ pytestmark = pytest.mark.gpu
 
 hip = pytest.importorskip("hip_runner")
 
-OFFSET_CASES = {"offset_windows", "offset_gap_err"}
-
-
 @pytest.mark.parametrize("name", sorted(rc.SINGLE_CASES))
 def test_reference_single(name):
-    if name in OFFSET_CASES:
-        pytest.xfail("device activation (add_sequence_offset) lands in a later milestone")
     rc.check_single(rc.SINGLE_CASES[name], hip)
 
 

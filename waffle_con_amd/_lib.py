@@ -265,4 +265,4 @@ def u8_bytes(ptr, n):
 
 
 def u64_list(ptr, n):
-    return [ptr[i] for i in range(n)]
+    return ptr[:n] if n else []

@@ -29,6 +29,7 @@ namespace wc {
 #endif
 
 constexpr int kMaxChild = 64;
+constexpr uint32_t WC_E_COVERAGE_GAP_CODE = 3;  // include/waffle_con.h
 constexpr uint32_t WC_E_INVARIANT_CODE = 10;  // include/waffle_con.h
 constexpr uint32_t WC_E_LIMIT_CODE = 11;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
@@ -54,6 +55,7 @@ struct Ctl {
   uint64_t farthest[2], last_constraint[2];
   uint64_t trk_total[2], trk_thr[2];
   uint32_t am_len;
+  uint32_t act_cnt;  // reads activating at the popped length (dual active_min growth)
   uint32_t n_ret;
   int32_t store_idx;
   uint32_t cache_slot, cache_hit, cache_nend, cache_multi;
@@ -301,6 +303,8 @@ struct Eng {
   Gm<uint32_t>* total_active;
   Gm<uint32_t>* active_min;
   Gm<uint32_t>* scratch;
+  Gm<uint64_t>* act_scr;  // this wave's offset-activation scratch (nullptr = none)
+  uint32_t act_m;
   DevProblem P;
   Lds L;
   __device__ SideView sv(uint32_t slot, uint32_t side) const {
@@ -350,6 +354,10 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
   E.active_min = E.total_active + L2;
   q += align16((uint64_t)2 * L2 * 4);
   E.scratch = (Gm<uint32_t>*)q + (uint64_t)wave_id() * (A.wcap + 2);
+  E.act_m = A.act_m;
+  E.act_scr = A.act_scr ? (Gm<uint64_t>*)A.act_scr + (uint64_t)blockIdx.x * A.act_stride +
+                              (uint64_t)wave_id() * 2 * A.act_m * 64
+                        : nullptr;
   E.L = carve(smem, A.sides, A.pcap, A.nmax, A.chain);
   return E;
 }
@@ -628,6 +636,57 @@ __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t d
     Gm<uint32_t>* wb = b.wf + (uint64_t)r * E.wcap;
     for (uint32_t i = lane; i < W; i += 64) wb[i] = wa[i];
   }
+}
+
+// ---- offset activation of one node side (block-level, barriers) ----
+// Every read whose activation length is `alen` (consensus.rs:330-334,
+// dual_consensus.rs:633-639) is activated against this side's consensus
+// con[0..clen) (consensus.rs:413-448 / dual_consensus.rs:866-906), one wave
+// per read. Adds the new reads' costs to ctl.cost_acc (want_cost) and, when
+// `info` is set, writes their nominations there (the pushed child's analysis
+// cache) and counts their ends/multi. ctl.ovf: 4 wavefront capacity, 2 offset
+// scratch, 16 an already active read (the reference's assert).
+template <bool kHot>
+__device__ inline void activate_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t clen, uint32_t alen,
+                                     bool want_cost, Sh<RInfo>* info) {
+  const int tid = threadIdx.x, lane = lane_id();
+  if (tid == 0) ctl.nheavy = 0;
+  __syncthreads();
+  for (uint32_t r = tid; r < E.n; r += kBlock)
+    if (E.A->ractivate[E.P.read_begin + r] == (int64_t)alen) E.L.list[atomicAdd(&ctl.nheavy, 1u)] = r;
+  __syncthreads();
+  const uint32_t nh = uni(ctl.nheavy);
+  SideView v = E.sv(slot, side);
+  const auto dst = node_rs<kHot>(E, slot, side);
+  WaveCounters cnt = {0, 0, 0, 0, 0};
+  for (uint32_t k = wave_id(); k < nh; k += kWaves) {
+    const uint32_t r = E.L.list[k];
+    if (uni(dst[r].e) != kInactive) {
+      if (lane == 0) atomicOr(&ctl.ovf, 16u);
+      continue;
+    }
+    Gm<uint32_t>* wf = v.wf + (uint64_t)r * E.wcap;
+    uint32_t e = 0;
+    const int rc = wave_activate(&dst[r], wf, E.read(r), E.rlen(r), v.con, clen, E.cfg, E.wcap, E.act_scr, E.act_m,
+                                 cnt, e);
+    if (rc != 0) {
+      if (lane == 0) atomicOr(&ctl.ovf, rc == 1 ? 4u : 2u);
+      continue;
+    }
+    if (info) {
+      __builtin_amdgcn_wave_barrier();
+      const bool ok = wave_analyze_read(wf, e, dst[r].off, E.read(r), E.rlen(r), clen, &info[r]);
+      if (lane == 0) {
+        if (!ok) atomicOr(&ctl.ovf, 1u);
+        if (info[r].end) atomicAdd(&ctl.n_end[side], 1u);
+        if (info[r].n > 1) atomicOr(&ctl.multi[side], 1u);
+      }
+    }
+    if (want_cost && lane == 0)
+      atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost_of(e, E.cfg.cost_mode));
+  }
+  flush_counters(ctl, cnt);
+  __syncthreads();
 }
 
 // ---- VOTES (consensus.rs:540-564 / dual_consensus.rs:1242-1290) ----
@@ -1077,10 +1136,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       const uint32_t nc = uni(ctl.nchild);
       if (nc == 0) {
         if (tid == 0) {
+          if (len < E.P.max_act) {  // consensus.rs:303-305: coverage gap (the host formats the message)
+            ctl.status = WC_E_COVERAGE_GAP_CODE;
+            ((Gm<uint32_t>*)outp)[1] = len;
+          }
           E.L.freestack[ctl.nfree++] = top;
           ctl.hot_slot = kNoSlot;
         }
         __syncthreads();
+        if (uni(ctl.status) != ST_OK) break;
         continue;
       }
       if (len + 1 > E.lcap) {
@@ -1089,7 +1153,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         break;
       }
       // ---- one child and nothing else queued: linear-chain run-ahead ----
-      if (nc == 1 && A.chain && uni(ctl.heap_n) == 0 && E.P.n_active == E.n) {
+      // (past the last activation point every read of this lineage is active)
+      if (nc == 1 && A.chain && uni(ctl.heap_n) == 0 && (E.P.n_active == E.n || len >= E.P.max_act)) {
         const uint32_t jstar = run_chain(E, ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
         PH_MARK(14);
         if (jstar) continue;
@@ -1119,8 +1184,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         const int sym = uni((int32_t)ctl.ch_s[c][0]);
         if (slot != top) push_sides<true, false>(E, ctl, slot, sym, -1, len + 1, 0, true, E.L.rinfo);
         else push_sides<true, true>(E, ctl, slot, sym, -1, len + 1, 0, true, E.L.rinfo);
+        // reads whose offset activates at this length (consensus.rs:327-335)
+        if (len + 1 <= E.P.max_act) {
+          if (slot != top) activate_side<false>(E, ctl, slot, 0, len + 1, len + 1, true, E.L.rinfo);
+          else activate_side<true>(E, ctl, slot, 0, len + 1, len + 1, true, E.L.rinfo);
+        }
         if (tid == 0) {
-          if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
+          if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;
+          else if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
           else if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
           ctl.ch_cost[c] = ctl.cost_acc;
           ctl.ch_slot[c] = slot;
@@ -1305,8 +1376,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       }
 
       // ---- active_min_count growth (dual_consensus.rs:497-513) ----
+      uint32_t nadd = 0;  // reads activating at tlen
+      if (tlen <= E.P.max_act && uni(ctl.am_len) == tlen + 1) {
+        if (tid == 0) ctl.act_cnt = 0;
+        __syncthreads();
+        for (uint32_t r = tid; r < E.n; r += kBlock)
+          if (E.A->ractivate[E.P.read_begin + r] == (int64_t)tlen) atomicAdd(&ctl.act_cnt, 1u);
+        __syncthreads();
+        nadd = uni(ctl.act_cnt);
+      }
       if (tid == 0 && ctl.am_len == tlen + 1 && tlen + 1 < E.lcap + 2) {
-        const uint32_t nt = E.total_active[tlen];  // + activations at tlen (offset path)
+        const uint32_t nt = E.total_active[tlen] + nadd;
         E.total_active[tlen + 1] = nt;
         E.active_min[tlen + 1] = (uint32_t)max(cfg.min_count, ceil_u64(cfg.min_af * (double)nt));
         ctl.am_len++;
@@ -1465,8 +1545,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         __syncthreads();
         const uint32_t nl0 = E.L.meta[slot].len[0], nl1 = E.L.meta[slot].len[1];
         push_sides<false, false>(E, ctl, slot, s0, s1, nl0, nl1, false, nullptr);
-        // prune (dual_consensus.rs:1030-1045) + priority (:1092-1168)
         const bool cdual = (E.L.meta[slot].flags & 1u) != 0;
+        // reads whose offset activates at the new max length (dual_consensus.rs:633-639):
+        // consensus 1 always, consensus 2 too when dual (:866-906)
+        if (max(nl0, nl1) <= E.P.max_act) {
+          activate_side<false>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
+          if (cdual) activate_side<false>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
+        }
+        // prune (dual_consensus.rs:1030-1045) + priority (:1092-1168)
         {
           SideView a = E.sv(slot, 0), b = E.sv(slot, 1);
           uint64_t cost = 0;
@@ -1495,7 +1581,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         }
         __syncthreads();
         if (tid == 0) {
-          if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
+          if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;
+          else if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
           else if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
           auto& m = E.L.meta[slot];
           m.nsome[0] = ctl.some_acc[0];

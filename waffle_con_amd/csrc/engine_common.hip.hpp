@@ -659,4 +659,131 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
   return true;
 }
 
+// ---- offset activation (consensus.rs:413-448, dual_consensus.rs:866-906) ----
+// wfa_ed_config(v1, v2, require_both_end = false, wildcard)
+// (sequence_alignment.rs:36-87) for this lane's own (v1, v2): the same
+// furthest-reaching (i, j) pairs, max-merged lexicographically (packed as
+// i << 32 | j), and the same boundary rules. Each lane keeps its two pair
+// arrays in the wave's scratch, lane-interleaved (entry k of lane l at
+// k * 64 + l). Returns the edit count, or `cap` as soon as it reaches `cap`.
+// `m` bounds the arrays (entries); edits <= |v2| always, so m >= 2|v2| + 5
+// never truncates an uncapped run.
+constexpr uint32_t kEdOverflow = 0xFFFFFFFEu;
+__device__ inline uint32_t lane_wfa_ed(const Gm<uint8_t>* v1, uint32_t l1, const Gm<uint8_t>* v2, uint32_t l2, int wc,
+                                       uint32_t cap, uint32_t m, Gm<uint64_t>* A, Gm<uint64_t>* B) {
+  const int lane = lane_id();
+  auto wcm = [&](uint8_t a) { return wc >= 0 && a == (uint8_t)wc; };
+  Gm<uint64_t>* cur = A;
+  Gm<uint64_t>* nxt = B;
+  cur[lane] = 0;
+  for (uint32_t k = 0; k < 3; ++k) nxt[k * 64 + lane] = 0;
+  uint32_t edits = 0;
+  for (;;) {
+    const uint32_t ncur = 1 + 2 * edits;
+    for (uint32_t k = 0; k < ncur; ++k) {
+      const uint64_t pr = cur[k * 64 + lane];
+      uint32_t i = (uint32_t)(pr >> 32), j = (uint32_t)pr;
+      while (i < l1 && j < l2) {
+        const uint8_t a = v1[i], b = v2[j];
+        if (!(a == b || wcm(a) || wcm(b))) break;
+        ++i;
+        ++j;
+      }
+      if (j == l2) return edits;  // (i == l1 || !require_both_end) && j == l2
+      const uint64_t ij = (uint64_t)i << 32 | j;
+      uint64_t n0, n1, n2;
+      if (i == l1) {
+        n0 = ij;
+        n1 = ij + 1;
+        n2 = ij + 1;
+      } else {
+        n0 = ij + (1ull << 32);
+        n1 = ij + (1ull << 32) + 1;
+        n2 = ij + 1;
+      }
+      Gm<uint64_t>* q = nxt + (uint64_t)k * 64 + lane;
+      q[0] = max(q[0], n0);
+      q[64] = max(q[64], n1);
+      q[128] = max(q[128], n2);
+    }
+    edits++;
+    if (edits >= cap) return cap;
+    if (3 + 2 * edits > m) return kEdOverflow;  // scratch too small (reported, never truncated)
+    Gm<uint64_t>* t = cur;
+    cur = nxt;
+    nxt = t;
+    for (uint32_t k = 0; k < 3 + 2 * edits; ++k) nxt[k * 64 + lane] = 0;
+  }
+}
+
+// The best start offset of a read activated against con[0..clen)
+// (consensus.rs:418-437): the middle of the window is the default, replaced by
+// the first p in [start, end) whose prefix edit distance is strictly smaller
+// than the best so far — i.e. the smallest p attaining min_p ed(p) if that is
+// below ed(best0). Lanes take candidates in parallel; a first pass caps every
+// edit count at kCap (exact whenever the winner is below the cap), and only an
+// undecided window reruns uncapped. Wave-uniform result.
+__device__ inline uint32_t wave_pick_offset(const Gm<uint8_t>* con, uint32_t clen, const Gm<uint8_t>* rd, uint32_t ocl,
+                                            uint32_t window, int wc, Gm<uint64_t>* scr, uint32_t m) {
+  const int lane = lane_id();
+  auto sat = [](uint32_t a, uint32_t b) { return a > b ? a - b : 0u; };
+  const uint32_t start = sat(clen, window + ocl), end = sat(clen, ocl);
+  const uint32_t best0 = sat(clen, ocl + window / 2);
+  Gm<uint64_t>* A = scr;
+  Gm<uint64_t>* B = scr + (uint64_t)m * 64;
+  constexpr uint32_t kCap = 12;
+  for (int pass = 0; pass < 2; ++pass) {
+    const uint32_t cap = pass == 0 ? kCap : 0xFFFFFFFFu;
+    // best0 (lane 0 of the first chunk is spent on it)
+    uint32_t e0 = lane == 0 ? lane_wfa_ed(con + best0, clen - best0, rd, ocl, wc, cap, m, A, B) : 0u;
+    e0 = __shfl(e0, 0);
+    uint32_t mbest = 0xFFFFFFFFu, pbest = 0xFFFFFFFFu;  // min over [start, end), smallest p
+    for (uint32_t base = start; base < end; base += 64) {
+      const uint32_t p = base + lane;
+      uint32_t ed = 0xFFFFFFFFu;
+      if (p < end) ed = lane_wfa_ed(con + p, clen - p, rd, ocl, wc, cap, m, A, B);
+      // wave min of (ed, p)
+      uint64_t key = (uint64_t)ed << 32 | p;
+      for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t y = __shfl_xor(key, o);
+        key = min(key, y);
+      }
+      if (ballot(ed == kEdOverflow) || e0 == kEdOverflow) return kEdOverflow;
+      if ((uint32_t)(key >> 32) < mbest) {
+        mbest = (uint32_t)(key >> 32);
+        pbest = (uint32_t)key;
+      }
+    }
+    if (e0 == kEdOverflow) return kEdOverflow;
+    if (mbest < cap && mbest < e0) return pbest;      // exact strict win inside the window
+    if (e0 < cap && !(mbest < e0)) return best0;      // e0 exact and nothing below it
+    // undecided (everything reached the cap): rerun uncapped
+    if (pass == 1) return mbest < e0 ? pbest : best0;
+  }
+  return best0;
+}
+
+// Activate read (rd, blen) on one node side whose consensus is con[0..clen):
+// pick the offset, then DWFALite::new + set_offset + update (dynamic_wfa.rs:52-99)
+// on the read's wavefront row, and write the RState. Returns false on
+// wavefront capacity or offset-scratch overflow. e_out = the new edit distance.
+// Return: 0 ok, 1 wavefront capacity (retry with a larger wcap), 2 offset scratch.
+template <class P>
+__device__ inline int wave_activate(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
+                                     const Gm<uint8_t>* con, uint32_t clen, const DevConfig& cfg, uint32_t wcap,
+                                     Gm<uint64_t>* scr, uint32_t m, WaveCounters& cnt, uint32_t& e_out) {
+  const uint32_t ocl = (uint32_t)min((uint64_t)cfg.offset_compare_length, (uint64_t)blen);
+  const uint32_t off = wave_pick_offset(con, clen, rd, ocl, (uint32_t)cfg.offset_window, cfg.wildcard, scr, m);
+  if (off == kEdOverflow) return 2;
+  if (lane_id() == 0) wf[0] = 0;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t e = 0, mo, mb;
+  if (!wave_update_general(wf, e, off, rd, blen, con, clen, cfg.wildcard, cfg.early != 0, wcap, cnt, mo, mb))
+    return 1;
+  __builtin_amdgcn_wave_barrier();
+  wave_rebuild(wf, e, off, blen, clen, rsp);
+  e_out = e;
+  return 0;
+}
+
 }  // namespace wc

@@ -56,7 +56,10 @@ struct DevProblem {
   uint32_t n_reads;
   uint32_t max_read_len;
   uint32_t n_active;    // reads with offset None (after auto-shift)
+  uint32_t max_act;     // largest activation length (add_sequence_offset), 0 = none
+  uint32_t _pad[3];
 };
+static_assert(sizeof(DevProblem) == 32, "DevProblem layout");
 
 // Device result record (one per returned consensus); the host turns these into
 // Consensus / DualConsensus values. Layout inside the per-problem output area:
@@ -87,10 +90,14 @@ struct EngineArgs {
   uint32_t* work_counter;
   uint32_t* trace;       // debug: per-pop records of problem 0 (nullptr = off)
   uint32_t trace_cap;    // records (4 u32 each); trace[0] = count
-  uint32_t _pad2;
+  uint32_t act_m;        // offset activation: pair entries per lane per array (0 = no scratch)
+  uint64_t* act_scr;     // offset activation scratch: per workgroup act_stride u64
+  uint64_t act_stride;
   unsigned long long* phases;  // debug (WC_PHASE_PROF builds): shader cycles per phase, kPhases
 };
-constexpr int kPhases = 32;  // 0..15 block phases, 16..31 wave-0 sub-phases
+constexpr int kPhases = 32;
+// offset-activation scratch per workgroup (u64): per wave two lane-interleaved pair arrays of m entries
+__host__ __device__ inline uint64_t act_scr_u64(uint32_t m) { return (uint64_t)kWaves * 2 * m * 64; }  // 0..15 block phases, 16..31 wave-0 sub-phases
 
 // ---- byte layouts (host and device compute them identically) ----
 __host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }

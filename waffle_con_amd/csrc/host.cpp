@@ -59,13 +59,36 @@ struct DevBuf {
   }
 };
 
+// pinned host staging for the per-launch read-back (status, counters, first records)
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    release();
+    size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 struct wc_ctx {
   int device = 0;
   int n_cu = 256;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string err;
-  DevBuf ract, probs, ws, out, status, stats, counter, jobs;
+  DevBuf ract, probs, ws, out, status, stats, counter, jobs, act;
+  HostBuf stage;
 };
 
 namespace {
@@ -247,12 +270,6 @@ int activation_plan(const wc_config& cfg, const BatchProblem& q, std::vector<int
     err = err_msg(WC_E_NO_START);
     return WC_E_NO_START;
   }
-  for (auto a : act) {
-    if (a >= 0) {
-      err = "activation offsets (add_sequence_offset) are not supported by this build's device engine yet";
-      return WC_E_LIMIT;
-    }
-  }
   return WC_OK;
 }
 
@@ -277,8 +294,9 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
 
   // per-read activation lengths for the whole batch (indexed by global read)
   std::vector<int64_t> ract(std::max<size_t>(b->rlen_h.size(), 1), -1);
-  std::vector<uint32_t> n_active(NP, 0);
+  std::vector<uint32_t> n_active(NP, 0), max_act(NP, 0);
   std::vector<uint32_t> runnable;
+  bool any_act = false;
   for (uint32_t id : ids) {
     std::vector<int64_t> act;
     int rc = activation_plan(cfg, b->probs[id], act, n_active[id], R.error[id]);
@@ -287,6 +305,16 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
       continue;
     }
     std::copy(act.begin(), act.end(), ract.begin() + b->probs[id].read_begin);
+    for (auto a : act)
+      if (a >= 0) {
+        if (a > (int64_t)UINT32_MAX - 2) {
+          R.status[id] = WC_E_LIMIT;
+          R.error[id] = "activation offset beyond the device engine's u32 lengths";
+        }
+        max_act[id] = std::max<uint32_t>(max_act[id], (uint32_t)std::min<int64_t>(a, UINT32_MAX - 2));
+        any_act = true;
+      }
+    if (R.status[id] != WC_OK) continue;
     runnable.push_back(id);
   }
   ids = runnable;
@@ -328,6 +356,7 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
       dp[i].n_reads = q.n_reads;
       dp[i].max_read_len = q.max_len;
       dp[i].n_active = n_active[ids[i]];
+      dp[i].max_act = max_act[ids[i]];
     }
     size_t lds = (size_t)lds_bytes(sides, pcap, nmax, chain);
     if (lds > 60 * 1024) {
@@ -341,6 +370,23 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
     uint32_t grid = std::min<uint32_t>(P, (uint32_t)std::max(1, per_cu) * (uint32_t)ctx->n_cu);
     uint64_t wsb = ws_bytes(sides, pcap, nmax, wcap, lcap);
     uint64_t ob = out_bytes(sides, rmax, nmax, lcap);
+    // offset activation scratch (wfa_ed_config pair arrays): edits <= |v1| + |v2|
+    // with |v1| <= window + ocl and |v2| <= ocl (engine_common wave_pick_offset)
+    uint32_t act_m = 0;
+    if (any_act) {
+      const uint64_t ocl = std::min<uint64_t>(cfg.offset_compare_length, maxlen);
+      const uint64_t m = 3 + 2 * (cfg.offset_window + 2 * ocl) + 8;
+      if (m > 8192) {
+        for (uint32_t id : ids) {
+          R.status[id] = WC_E_LIMIT;
+          R.error[id] = "offset_window/offset_compare_length too large for the device activation scratch";
+        }
+        return WC_OK;
+      }
+      act_m = (uint32_t)m;
+    }
+    if (act_m && !ctx->act.ensure(act_scr_u64(act_m) * 8 * grid))
+      return set_err(ctx, WC_E_HIP, "device allocation failed (activation scratch)");
     if (!ctx->probs.ensure(P * sizeof(DevProblem)) || !ctx->ws.ensure(wsb * grid) || !ctx->out.ensure(ob * P) ||
         !ctx->status.ensure(P * 4) || !ctx->stats.ensure((size_t)P * S_NSTAT * 8) || !ctx->counter.ensure(4))
       return set_err(ctx, WC_E_HIP, "device allocation failed (workspace)");
@@ -370,6 +416,9 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
     a.status = (uint32_t*)ctx->status.p;
     a.stats = (uint64_t*)ctx->stats.p;
     a.work_counter = (uint32_t*)ctx->counter.p;
+    a.act_m = act_m;
+    a.act_scr = act_m ? (uint64_t*)ctx->act.p : nullptr;
+    a.act_stride = act_m ? act_scr_u64(act_m) : 0;
     // debug trace of problem 0's pops (WC_TRACE=<file>); off by default
     const char* trace_path = getenv("WC_TRACE");
     DevBuf tbuf;
@@ -423,14 +472,20 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
 
     // read back: status, stats, and the first record of every problem in one
     // strided copy; further records only for problems that returned ties
-    std::vector<uint32_t> hst(P);
-    std::vector<uint64_t> hstats((size_t)P * S_NSTAT);
     const uint64_t rb = result_bytes(sides, nmax, lcap);
     const uint64_t first = 16 + rb;
-    std::vector<uint8_t> hout((size_t)first * P);
-    HIPCHK(hipMemcpy(hst.data(), ctx->status.p, P * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(hstats.data(), ctx->stats.p, hstats.size() * 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy2D(hout.data(), first, ctx->out.p, ob, first, P, hipMemcpyDeviceToHost));
+    const size_t st_off = 0, stats_off = align16((uint64_t)P * 4),
+                 out_off = stats_off + align16((uint64_t)P * S_NSTAT * 8);
+    if (!ctx->stage.ensure(out_off + (size_t)first * P))
+      return set_err(ctx, WC_E_HIP, "pinned host allocation failed");
+    uint8_t* stg = (uint8_t*)ctx->stage.p;
+    HIPCHK(hipMemcpyAsync(stg + st_off, ctx->status.p, P * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(stg + stats_off, ctx->stats.p, (size_t)P * S_NSTAT * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpy2DAsync(stg + out_off, first, ctx->out.p, ob, first, P, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const uint32_t* hst = (const uint32_t*)(stg + st_off);
+    const uint64_t* hstats = (const uint64_t*)(stg + stats_off);
+    const uint8_t* hout = stg + out_off;
 
     std::vector<uint32_t> retry;
     uint32_t rflags = 0;
@@ -448,9 +503,13 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
       R.status[id] = (int)st;
       if (st != ST_OK) {
         R.error[id] = err_msg((int)st);
+        if (st == WC_E_COVERAGE_GAP)  // consensus.rs:305 / dual_consensus.rs message
+          R.error[id] = "Encountered coverage gap: consensus is length " +
+                        std::to_string(((const uint32_t*)(hout + (size_t)i * first))[1]) +
+                        " with no candidates, but sequences activate at " + std::to_string(max_act[id]);
         continue;
       }
-      const uint8_t* base = hout.data() + (size_t)i * first;
+      const uint8_t* base = hout + (size_t)i * first;
       const uint32_t nres = ((const uint32_t*)base)[0];
       if (nres > 1) {
         extra.resize((size_t)nres * rb);
@@ -712,8 +771,9 @@ int wc_ctx_create(int device, wc_ctx** out) {
 void wc_ctx_destroy(wc_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  for (DevBuf* b : {&ctx->ract, &ctx->probs, &ctx->ws, &ctx->out, &ctx->status, &ctx->stats, &ctx->counter, &ctx->jobs})
+  for (DevBuf* b : {&ctx->ract, &ctx->probs, &ctx->ws, &ctx->out, &ctx->status, &ctx->stats, &ctx->counter, &ctx->jobs, &ctx->act})
     b->release();
+  ctx->stage.release();
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
