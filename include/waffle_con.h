@@ -213,6 +213,14 @@ void wc_rng_seed_from_u64(uint64_t seed, uint32_t n, uint32_t* out);
 uint64_t wc_wfa_ed_config(const uint8_t* v1, uint64_t l1, const uint8_t* v2, uint64_t l2, uint8_t require_both_end,
                           int32_t wildcard);
 
+/* sequence_alignment.rs:18-87 — wfa_ed_config over a batch of pairs on the
+ * device (one wave64 per pair): out_ed[i] = wfa_ed_config(v1[i], v2[i],
+ * require_both_end, wildcard); wildcard < 0 = None; wfa_ed is
+ * (require_both_end = 1, wildcard = '*'). Lengths must be < 2^31. Inputs are
+ * host buffers, copied during the call. Returns WC_OK or an error code. */
+int wc_wfa_ed_batch(wc_ctx* ctx, uint32_t n, const uint8_t* const* v1, const uint64_t* l1, const uint8_t* const* v2,
+                    const uint64_t* l2, uint8_t require_both_end, int32_t wildcard, uint64_t* out_ed);
+
 #ifdef __cplusplus
 }
 #endif

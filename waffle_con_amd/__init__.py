@@ -11,11 +11,11 @@ from .example_gen import generate_test
 from .multi_consensus import MultiConsensus
 from .pqueue_tracker import PQueueTracker
 from .priority_consensus import PriorityConsensus, PriorityConsensusDWFA, priority_consensus_batch
-from .sequence_alignment import wfa_ed, wfa_ed_config
+from .sequence_alignment import wfa_ed, wfa_ed_batch, wfa_ed_config
 
 __all__ = [
     "CdwfaConfig", "CdwfaConfigBuilder", "ConsensusCost", "Consensus", "ConsensusDWFA", "consensus_batch",
     "DualConsensus", "DualConsensusDWFA", "dual_consensus_batch", "PriorityConsensus", "PriorityConsensusDWFA",
-    "priority_consensus_batch", "MultiConsensus", "PQueueTracker", "DWFALite", "generate_test", "wfa_ed",
+    "priority_consensus_batch", "MultiConsensus", "PQueueTracker", "DWFALite", "generate_test", "wfa_ed", "wfa_ed_batch",
     "wfa_ed_config", "Context", "WaffleConError", "default_context", "ResidentBatch",
 ]

@@ -115,7 +115,7 @@ EXPORTED = (
     "wc_results_count", "wc_results_single", "wc_results_dual", "wc_results_chain_len",
     "wc_results_chain", "wc_results_sequence_indices", "wc_results_stats",
     "wc_results_problem_stats", "wc_dwfa_batch", "wc_generate_test", "wc_gen_consensus",
-    "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_rng_words", "wc_rng_stdrng_chain",
+    "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_wfa_ed_batch", "wc_rng_words", "wc_rng_stdrng_chain",
     "wc_rng_seed_from_u64",
 )
 
@@ -183,6 +183,9 @@ def lib():
         L.wc_wfa_ed_config.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                                        ctypes.c_uint8, ctypes.c_int32]
         L.wc_wfa_ed_config.restype = ctypes.c_uint64
+        L.wc_wfa_ed_batch.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(_u8p), ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(_u8p), ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint8,
+                                      ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]
         _lib = L
         return L
 

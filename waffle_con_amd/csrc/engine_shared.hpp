@@ -226,4 +226,11 @@ struct DwfaDevJob {
   uint8_t cand_syms[16];
   uint32_t cand_counts[16];
 };
+// one standalone wfa_ed_config pair (wc_wfa_ed_batch); offsets into the
+// batch's sequence arena and scratch rows (two rows of `cap` u64 entries)
+struct EdDevJob {
+  uint64_t v1_off, v2_off, scr_off;
+  uint32_t l1, l2;
+  uint64_t cap;
+};
 }  // namespace wc

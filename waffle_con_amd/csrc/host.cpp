@@ -31,6 +31,8 @@ void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStr
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 int engine_blocks_per_cu(uint32_t sides, size_t lds);
 void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s);
+void launch_wfa_ed_batch(const EdDevJob* jobs, uint32_t n, const uint8_t* seqs, uint64_t* scratch, int wc,
+                         uint32_t both, uint64_t* out, hipStream_t s);
 }  // namespace wc
 
 using namespace wc;
@@ -1159,6 +1161,86 @@ int wc_dwfa_batch(wc_ctx* ctx, uint32_t n, wc_dwfa_job* jobs) {
     }
   } while (0);
   arena.release();
+  return rc;
+}
+
+// ---- batched wfa_ed_config (sequence_alignment.rs:18-87) ----
+// Pairs go to the device in launches whose sequence arena + scratch rows stay
+// under kEdLaunchBytes (a single larger pair gets a launch of its own).
+int wc_wfa_ed_batch(wc_ctx* ctx, uint32_t n, const uint8_t* const* v1, const uint64_t* l1, const uint8_t* const* v2,
+                    const uint64_t* l2, uint8_t require_both_end, int32_t wildcard, uint64_t* out_ed) {
+  if (n == 0) return WC_OK;
+  if (!v1 || !l1 || !v2 || !l2 || !out_ed) return set_err(ctx, WC_E_BAD_INPUT, "wc_wfa_ed_batch: null argument");
+  for (uint32_t i = 0; i < n; ++i) {
+    if (l1[i] >= (1ull << 31) || l2[i] >= (1ull << 31))
+      return set_err(ctx, WC_E_BAD_INPUT, "wc_wfa_ed_batch: sequence length must be < 2^31");
+    if ((l1[i] && !v1[i]) || (l2[i] && !v2[i])) return set_err(ctx, WC_E_BAD_INPUT, "wc_wfa_ed_batch: null sequence");
+  }
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
+  constexpr uint64_t kEdLaunchBytes = 1ull << 30;
+  auto a16 = [](uint64_t x) { return (x + 15) & ~15ull; };
+  auto cap_of = [&](uint32_t i) { return 2 * (l1[i] + l2[i]) + 3; };
+  DevBuf arena, scratch, jobs, out;
+  int rc = WC_OK;
+  for (uint32_t b = 0; b < n && rc == WC_OK;) {
+    // [b, e): pairs of this launch
+    uint32_t e = b;
+    uint64_t sbytes = 0, sents = 0;
+    while (e < n) {
+      const uint64_t add = a16(l1[e]) + a16(l2[e]), ents = 2 * cap_of(e);
+      if (e > b && sbytes + add + 8 * (sents + ents) > kEdLaunchBytes) break;
+      sbytes += add;
+      sents += ents;
+      ++e;
+    }
+    const uint32_t m = e - b;
+    std::vector<uint8_t> h(sbytes + 16);
+    std::vector<EdDevJob> dj(m);
+    uint64_t so = 0, eo = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+      const uint32_t i = b + k;
+      EdDevJob& d = dj[k];
+      d.v1_off = so;
+      if (l1[i]) memcpy(h.data() + so, v1[i], l1[i]);
+      so += a16(l1[i]);
+      d.v2_off = so;
+      if (l2[i]) memcpy(h.data() + so, v2[i], l2[i]);
+      so += a16(l2[i]);
+      d.l1 = (uint32_t)l1[i];
+      d.l2 = (uint32_t)l2[i];
+      d.cap = cap_of(i);
+      d.scr_off = eo;
+      eo += 2 * d.cap;
+    }
+    if (!arena.ensure(h.size()) || !scratch.ensure(8 * eo) || !jobs.ensure(m * sizeof(EdDevJob)) ||
+        !out.ensure(8ull * m)) {
+      rc = set_err(ctx, WC_E_HIP, "device allocation failed (wfa_ed batch)");
+      break;
+    }
+    if (hipMemcpyAsync(arena.p, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(jobs.p, dj.data(), m * sizeof(EdDevJob), hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+      rc = set_err(ctx, WC_E_HIP, "copy to device failed (wfa_ed batch)");
+      break;
+    }
+    launch_wfa_ed_batch((const EdDevJob*)jobs.p, m, (const uint8_t*)arena.p, (uint64_t*)scratch.p, (int)wildcard,
+                        require_both_end ? 1u : 0u, (uint64_t*)out.p, ctx->stream);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(out_ed + b, out.p, 8ull * m, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      rc = set_err(ctx, WC_E_HIP, "wfa_ed kernel failed");
+      break;
+    }
+    for (uint32_t k = 0; k < m; ++k)
+      if (out_ed[b + k] == ~0ull) {
+        rc = set_err(ctx, WC_E_LIMIT, "wfa_ed scratch row too short");
+        break;
+      }
+    b = e;
+  }
+  arena.release();
+  scratch.release();
+  jobs.release();
+  out.release();
   return rc;
 }
 
