@@ -43,7 +43,7 @@ def test_batch_matches_individual():
         assert g == orc.consensus(p, **cfg)
 
 
-@pytest.mark.parametrize("chain", ["0", "2", "5", "16"])
+@pytest.mark.parametrize("chain", ["0", "2", "5", "16", "31", "40"])
 @pytest.mark.parametrize("L,N,err,seed", [(1500, 20, 0.01, 11), (800, 12, 0.04, 12), (600, 9, 0.08, 13)])
 def test_chain_length_invariance(chain, L, N, err, seed, monkeypatch):
     """The linear-chain run-ahead (WC_CHAIN = max steps, 0 = off) must not

@@ -29,20 +29,20 @@
 // queue with its nominations cached), which handles ends, branching and
 // everything else.
 
-// nomination record of one read at one chain step (u32)
-constexpr uint32_t kNomSymMask = 0xFFu;   // first symbol
+// nomination record of one read at one chain step (u16)
+constexpr uint32_t kNomSymMask = 0xFFu;   // the symbol, or the ChainOvf index with kNomOvf
 constexpr uint32_t kNomOne = 1u << 8;     // exactly one distinct symbol
 constexpr uint32_t kNomEnd = 1u << 12;    // reached_baseline_end
 constexpr uint32_t kNomActive = 1u << 13; // Some(dwfa)
-constexpr uint32_t kNomOvf = 1u << 14;    // >= 2 symbols: ChainOvf[code >> 16]
+constexpr uint32_t kNomOvf = 1u << 14;    // >= 2 symbols: ChainOvf[code & kNomSymMask]
 
-__device__ __forceinline__ RInfoReg nom_load(const Sh<uint32_t>* nom, const Sh<ChainOvf>* ovf, uint32_t r) {
+__device__ __forceinline__ RInfoReg nom_load(const Sh<uint16_t>* nom, const Sh<ChainOvf>* ovf, uint32_t r) {
   const uint32_t c = nom[r];
   RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
   if (!(c & kNomActive)) return x;
   x.e = 0;
   if (c & kNomOvf) {
-    const ChainOvf o = ovf[c >> 16];
+    const ChainOvf o = ovf[c & kNomSymMask];
     x.n = o.n;
     x.split = o.split;
     x.sym = o.sym;
@@ -379,13 +379,13 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
               q.occ = o.occ;
               q.split = o.split;
               q.n = o.n;
-              code |= kNomOvf | (idx << 16);
+              code = (code & ~kNomSymMask) | kNomOvf | idx;
             } else {
               stop = true;
             }
           }
         }
-        E.L.cnom[j * E.nmax + r] = code;
+        E.L.cnom[j * E.nmax + r] = (uint16_t)code;
       }
       // step aggregates: cost; reads at their end; votes for the predicted
       // next symbol (P) and for all other symbols (O) in 1/840ths; counts of
@@ -479,7 +479,7 @@ __device__ inline void chain_votes(Eng& E, Sh<Ctl>& ctl, uint32_t K) {
     SUB_T0(tb);
     bool ok = dec == 1;
     if (dec < 0) {
-      const Sh<uint32_t>* nom = E.L.cnom + j * E.nmax;
+      const Sh<uint16_t>* nom = E.L.cnom + j * E.nmax;
       uint32_t m = 0, key = 0;
       double val = 0.0;
       ok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r); }, [&](uint32_t) { return 1.0; },

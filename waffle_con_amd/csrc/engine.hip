@@ -126,7 +126,7 @@ struct Lds {
   Sh<ChainStep>* cstep;  // chain area (single engine with A.chain > 0)
   Sh<ChainOvf>* covf;
   Sh<RState>* ctmp;      // [kWaves]
-  Sh<uint32_t>* cnom;    // [K+1][nmax]
+  Sh<uint16_t>* cnom;    // [K+1][nmax]
   Sh<uint8_t>* cwin;     // [nmax][64]
   Sh<uint32_t>* cwb;     // [nmax]
   Sh<uint32_t>* cpc;     // [K+1]
@@ -158,8 +158,8 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
     p += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
     l.ctmp = (Sh<RState>*)p;
     p += (uint64_t)kWaves * 64;
-    l.cnom = (Sh<uint32_t>*)p;
-    p += align16((uint64_t)(K + 1) * nmax * 4);
+    l.cnom = (Sh<uint16_t>*)p;
+    p += align16((uint64_t)(K + 1) * nmax * 2);
     l.cwin = p;
     p += (uint64_t)nmax * 64;
     l.cwb = (Sh<uint32_t>*)p;

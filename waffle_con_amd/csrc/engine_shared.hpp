@@ -164,8 +164,10 @@ struct RInfo {
   uint32_t e;     // current edit distance (kInactive = None)
 };
 // ---- linear-chain run-ahead (single engine, engine.hip run_chain) ----
-constexpr uint32_t kChainMax = 16;   // steps per chain
+constexpr uint32_t kChainMax = 40;      // steps per chain (upper bound; WC_CHAIN); longer chains outrun the 64-B read windows
+constexpr uint32_t kChainDefault = 16;  // steps per chain by default
 constexpr uint32_t kChainOvf = 192;  // multi-symbol nominations stored per chain
+static_assert(kChainOvf <= 256, "ChainOvf index is the low byte of a u16 nomination code");
 struct ChainStep {  // aggregates of one speculative step (node N_j), LDS atomics (one per wave)
   uint64_t cost;    // sum of the reads' costs
   uint64_t po;      // votes in 1/840ths: for the predicted next symbol [0,32), for other symbols [32,64)
@@ -180,14 +182,14 @@ struct ChainOvf {  // nominations of a read with >= 2 distinct tip symbols
   uint64_t sym, occ;  // bytes in iteration order
   uint32_t split, n;
 };
-// chain LDS: steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[K+1][nmax] u32 |
+// chain LDS: steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[K+1][nmax] u16 |
 //            win[nmax][64] (read windows) | wb[nmax] u32 | pc[K+1] u32 | pred[K+2] u8
 __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K) {
   if (K == 0) return 0;
   uint64_t t = align16((uint64_t)(K + 1) * sizeof(ChainStep));
   t += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
   t += (uint64_t)kWaves * 64;
-  t += align16((uint64_t)(K + 1) * nmax * 4);
+  t += align16((uint64_t)(K + 1) * nmax * 2);
   t += (uint64_t)nmax * 64;
   t += align16((uint64_t)nmax * 4);
   t += align16((uint64_t)(K + 1) * 4);

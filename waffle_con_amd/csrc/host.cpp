@@ -335,8 +335,9 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
   // node pool: as many slots as ~16 MiB of workspace per workgroup allows
   // (16..256), bounded by the LDS the heap/metadata need
   // single engine: linear-chain run-ahead length (WC_CHAIN=<k> overrides, 0 = off)
-  uint32_t chain = (sides == 1 && nmax <= (uint32_t)kBlock) ? kChainMax : 0;
-  if (const char* ev = getenv("WC_CHAIN")) chain = std::min<uint32_t>((uint32_t)atoi(ev), kChainMax);
+  uint32_t chain = (sides == 1 && nmax <= (uint32_t)kBlock) ? kChainDefault : 0;
+  const char* chain_env = getenv("WC_CHAIN");
+  if (chain_env) chain = std::min<uint32_t>((uint32_t)atoi(chain_env), kChainMax);
   if (sides != 1 || nmax > (uint32_t)kBlock) chain = 0;
   uint32_t pcap = 16;
   {
@@ -344,6 +345,17 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
     while (pcap < 256 && (uint64_t)(pcap * 2) * sb <= (16ull << 20) &&
            lds_bytes(sides, pcap * 2, nmax, chain) <= 40 * 1024)
       pcap *= 2;
+  }
+  // longer chains amortise the per-chain work (prediction, acceptance, the
+  // literal pop between chains); take the longest one whose LDS still gives
+  // the workgroups per CU of the default length (results do not depend on it)
+  if (!chain_env && chain > 0) {
+    const int occ = engine_blocks_per_cu(sides, (size_t)lds_bytes(sides, pcap, nmax, chain));
+    for (uint32_t k = chain + 1; k <= kChainMax; ++k) {
+      const uint64_t l = lds_bytes(sides, pcap, nmax, k);
+      if (l > 60 * 1024 || engine_blocks_per_cu(sides, (size_t)l) < occ) break;
+      chain = k;
+    }
   }
   const uint32_t rmax = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cfg.max_return_size, 1), 256);
 
