@@ -56,7 +56,8 @@ def main():
     rep["chains"] = {"count": c15 & 0xFFFFF, "full": (c15 >> 20) & 0xFFFFF, "accepted_steps": c15 >> 40}
     # wave-0 sub-phases (cycles per chain, summed over workgroups / chains)
     SUB = {16: "walk-push", 17: "walk-heavy", 18: "walk-nominate", 19: "walk-heavy-count(w0)", 20: "votes-fast",
-           21: "votes-exact", 23: "prepare-windows", 24: "prepare-predict", 25: "votes-exact-count(w0)"}
+           21: "votes-exact", 23: "prepare-windows", 24: "prepare-predict", 25: "votes-exact-count(w0)",
+           26: "nominate-tips", 27: "nominate-code"}
     nch = max(1, rep["chains"]["count"])
     rep["sub_cycles_per_chain"] = {SUB[k]: round(cyc[k] / nch, 1) for k in SUB if k < len(cyc)}
     rep["block_cycles_per_chain"] = {PHASES[k]: round(cyc[k] / nch, 1) for k in (8, 9, 10, 11, 14)}

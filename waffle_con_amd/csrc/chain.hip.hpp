@@ -125,28 +125,53 @@ __device__ inline void chain_prepare(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_
           }
       }
     }
-    for (uint32_t t = 1; t < K; ++t) {
-      const uint32_t p = bo_tip + t;
-      const uint32_t x = (bo_tip != kInactive && p < blen) ? rb(p) : 0x100u;
-      // plurality of x over the wave (ties: the first-seen symbol)
-      uint64_t rem = ballot(x != 0x100u);
-      uint32_t best = 0x100u, bestc = 0;
-      while (rem) {
-        const int l = __builtin_ctzll(rem);
-        const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)x, l);
-        const uint64_t mm = ballot(x == s);
-        const uint32_t c = (uint32_t)__popcll((unsigned long long)mm);
-        if (c > bestc) {
-          bestc = c;
-          best = s;
+    // bytes are fetched eight steps at a time (independent loads under one
+    // wait; past the LDS window they come from HBM)
+    for (uint32_t t0 = 1; t0 < K; t0 += 8) {
+      uint32_t xs[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const uint32_t t = t0 + u;
+        xs[u] = (bo_tip != kInactive && t < K && bo_tip + t < blen) ? rb(bo_tip + t) : 0x100u;
+      }
+      bool stop = false;
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const uint32_t t = t0 + u;
+        if (t >= K) break;
+        const uint32_t x = xs[u];
+        // plurality of x over the wave (ties: the first-seen symbol); a
+        // first-seen symbol held by a strict majority is the plurality
+        uint64_t rem = ballot(x != 0x100u);
+        uint32_t best = 0x100u, bestc = 0;
+        if (rem) {
+          const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)x, __builtin_ctzll(rem));
+          const uint64_t mm = ballot(x == s);
+          const uint32_t c = (uint32_t)__popcll((unsigned long long)mm);
+          if (2 * c > (uint32_t)__popcll((unsigned long long)rem)) {
+            best = s;
+            rem = 0;
+          }
         }
-        rem &= ~mm;
+        while (rem) {
+          const int l = __builtin_ctzll(rem);
+          const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+          const uint64_t mm = ballot(x == s);
+          const uint32_t c = (uint32_t)__popcll((unsigned long long)mm);
+          if (c > bestc) {
+            bestc = c;
+            best = s;
+          }
+          rem &= ~mm;
+        }
+        if (best == 0x100u) {
+          if (lane == 0) atomicMin(&ctl.chain_stop, t);  // nothing to predict N_{t+1} from
+          stop = true;
+          break;
+        }
+        if (lane == 0) E.L.cpred[t + 1] = (uint8_t)best;
       }
-      if (best == 0x100u) {
-        if (lane == 0) atomicMin(&ctl.chain_stop, t);  // nothing to predict N_{t+1} from
-        break;
-      }
-      if (lane == 0) E.L.cpred[t + 1] = (uint8_t)best;
+      if (stop) break;
     }
     wave_lds_sync();
     // the predicted symbols extend the node's own consensus buffer in place
@@ -258,6 +283,12 @@ __device__ __forceinline__ Nom chain_nominate(const Front& f, const uint32_t (&x
 // Votes in exact rational form: a read's contribution occ/split to a symbol
 // (split <= kF = 8) is an integer number of 1/840ths (840 = lcm(1..8)).
 constexpr uint32_t kVoteDen = 840;
+// kVoteDen / split for split in 1..kF, without an integer division
+__device__ __forceinline__ uint32_t vote_unit(uint32_t split) {
+  return split <= 4 ? (split <= 2 ? (split == 1 ? 840u : 420u) : (split == 3 ? 280u : 210u))
+                    : (split <= 6 ? (split == 5 ? 168u : 140u) : (split == 7 ? 120u : 105u));
+}
+static_assert(kF == 8, "vote_unit covers split <= 8");
 
 // (C) push the K predicted symbols through every read, thread per read.
 // kFirst: speculative pass; stores each step's nominations and aggregates,
@@ -266,18 +297,29 @@ constexpr uint32_t kVoteDen = 840;
 // Both passes add their work counters to ctl.chain_tot. Wavefront rows are
 // written lazily (thread_push<kLazy>): only when a diagonal leaves the
 // frontier, plus one flush of the final frontier.
+// Waves that walk the chain. Each walking wave runs the same per-step
+// instruction stream whatever its number of live lanes, and the workgroups of
+// a CU share its SIMDs, so fewer, fuller waves cost less issue time.
+#ifndef WC_WALK_WAVES
+#define WC_WALK_WAVES 4
+#endif
+__device__ __forceinline__ uint32_t walk_waves(uint32_t n) {
+  return n <= 64u * WC_WALK_WAVES ? (uint32_t)WC_WALK_WAVES : (uint32_t)kWaves;
+}
+
 template <bool kFirst>
 __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int lane = lane_id(), wave = wave_id();
-  // reads are dealt round-robin over the waves (read = lane * kWaves + wave):
-  // every wave walks a quarter of the reads, so the edit-distance increases,
-  // which a wave handles one read at a time, are spread over all four
-  if ((uint32_t)wave >= E.n) return;  // no reads in this wave (no barriers below)
+  // reads are dealt round-robin over the walking waves (read = lane * ww +
+  // wave), so the edit-distance increases, which a wave handles one read at a
+  // time, are spread over them
+  const uint32_t ww = walk_waves(E.n);
+  if ((uint32_t)wave >= ww || (uint32_t)wave >= E.n) return;  // no reads in this wave (no barriers below)
   const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
   const int wc = cfg.wildcard;
   SideView v = E.sv(top, 0);
-  const uint32_t r = (uint32_t)lane * kWaves + (uint32_t)wave;
+  const uint32_t r = (uint32_t)lane * ww + (uint32_t)wave;
   const bool has = r < E.n;
   Front f;
   f.e = kInactive;
@@ -326,7 +368,7 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
       hm &= hm - 1;
       if (lane == l) front_store(tmp, f);
       wave_lds_sync();
-      const uint32_t rl = (uint32_t)l * kWaves + (uint32_t)wave;
+      const uint32_t rl = (uint32_t)l * ww + (uint32_t)wave;
       if (kFirst && !((bak >> l) & 1ull)) {
         // first rewrite of this row in the chain: keep a copy in slot S (the
         // rows are otherwise only touched at frontier diagonals, which a
@@ -365,6 +407,8 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
     o.sym = o.occ = 0;
     o.n = o.split = o.end = 0;
     if (active) o = chain_nominate(f, x, blen, olen);
+    SUB_T1(26, tc);
+    SUB_T0(td);
     if (kFirst) {
       bool stop = oob;
       if (has) {
@@ -387,6 +431,7 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
         }
         E.L.cnom[j * E.nmax + r] = (uint16_t)code;
       }
+      SUB_T1(27, td);
       // step aggregates: cost; reads at their end; votes for the predicted
       // next symbol (P) and for all other symbols (O) in 1/840ths; counts of
       // multi-symbol reads and of fractional votes for the prediction
@@ -398,7 +443,7 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
           if ((uint32_t)(o.sym & 0xFF) == pred) vp = kVoteDen;
           else vo = kVoteDen;
         } else {
-          const uint32_t unit = kVoteDen / o.split;
+          const uint32_t unit = vote_unit(o.split);
           for (uint32_t k = 0; k < o.n; ++k) {
             const uint32_t c = unit * (uint32_t)((o.occ >> (8 * k)) & 0xFF);
             if ((uint32_t)((o.sym >> (8 * k)) & 0xFF) == pred) {
@@ -498,16 +543,29 @@ __device__ inline void chain_votes(Eng& E, Sh<Ctl>& ctl, uint32_t K) {
   }
 }
 
-// (E) thread 0: replay the pops of N_1.. on the scalar search state
+// (E) wave 0: replay the pops of N_1.. on the scalar search state
 // (consensus.rs:224-251 with the queue holding only the chain node) and
 // commit the accepted prefix. Returns j* = number of chain nodes generated.
+// The step-local tests (max_err, capacity, reached_end, one passing candidate)
+// are evaluated by lanes over j at once; only the PQueueTracker threshold walk
+// is sequential, on registers.
 __device__ inline uint32_t chain_accept(Eng& E, Sh<Ctl>& ctl, uint32_t L0, uint32_t Keff) {
   const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
+  const uint32_t lane = (uint32_t)lane_id();
   Gm<uint32_t>* pc = E.trk + (E.lcap + 2);
+  const uint32_t jl = 1 + lane;  // Keff <= kChainMax < 64: one step per lane
+  bool bad = true;
+  if (jl < Keff) {
+    const auto& st = E.L.cstep[jl];
+    const uint32_t n_end = step_nend(st.ef);
+    const bool reached = early ? (n_end == E.n) : (n_end > 0);
+    bad = st.cost > ctl.max_err || (uint64_t)E.L.cpc[jl] >= cfg.max_capacity_per_size || reached || !st.ok;
+  }
+  const uint32_t jbad = 1 + (uint32_t)__builtin_ctzll(ballot(bad));  // lane 63 is always bad
   uint32_t jstar = Keff >= 1 ? 1u : 0u;
   uint64_t thr = ctl.trk_thr[0], farthest = ctl.farthest[0], lcnst = ctl.last_constraint[0];
-  for (uint32_t j = 1; j < Keff; ++j) {
+  for (uint32_t j = 1; j < Keff && j < jbad; ++j) {
     const uint64_t L = L0 + j;
     uint64_t t_thr = thr, t_l = lcnst;
     uint64_t total = L >= t_thr ? 1u : 0u;  // the queue holds N_j only
@@ -516,23 +574,23 @@ __device__ inline uint32_t chain_accept(Eng& E, Sh<Ctl>& ctl, uint32_t L0, uint3
       t_thr++;
       t_l = 0;
     }
-    const auto& st = E.L.cstep[j];
-    if (st.cost > ctl.max_err || L < t_thr || (uint64_t)E.L.cpc[j] >= cfg.max_capacity_per_size) break;
-    const uint32_t n_end = step_nend(st.ef);
-    const bool reached = early ? (n_end == E.n) : (n_end > 0);
-    if (reached || !st.ok) break;
+    if (L < t_thr) break;
     thr = t_thr;
     lcnst = t_l + 1;
     farthest = max(farthest, L);
-    pc[L] = E.L.cpc[j] + 1;
-    ctl.cnt[S_POPS]++;
-    ctl.cnt[S_EXPLORED]++;
-    ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)1);
     jstar = j + 1;
   }
-  ctl.trk_thr[0] = thr;
-  ctl.farthest[0] = farthest;
-  ctl.last_constraint[0] = lcnst;
+  if (jl < jstar) pc[L0 + jl] = E.L.cpc[jl] + 1;
+  if (lane == 0) {
+    ctl.trk_thr[0] = thr;
+    ctl.farthest[0] = farthest;
+    ctl.last_constraint[0] = lcnst;
+    if (jstar > 1) {
+      ctl.cnt[S_POPS] += jstar - 1;
+      ctl.cnt[S_EXPLORED] += jstar - 1;
+      ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)1);
+    }
+  }
   return jstar;
 }
 
@@ -580,16 +638,18 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Sh<Ctl>& ctl, uint32_t top
   chain_votes(E, ctl, Keff);
   __syncthreads();
   PH_MARK(10);
-  if (tid == 0) {
+  if (wave_id() == 0) {
     const uint32_t js = chain_accept(E, ctl, L0, Keff);
-    ctl.chain_len = js;
-    if (js == K && Keff == K) {  // the speculative pass is the committed work
-      ctl.cnt[S_UPDATES] += ctl.chain_tot[0];
-      ctl.cnt[S_WOUT] += ctl.chain_tot[1];
-      ctl.cnt[S_COMPARES] += ctl.chain_tot[2];
-      ctl.cnt[S_EDINC] += ctl.chain_tot[3];
+    if (tid == 0) {
+      ctl.chain_len = js;
+      if (js == K && Keff == K) {  // the speculative pass is the committed work
+        ctl.cnt[S_UPDATES] += ctl.chain_tot[0];
+        ctl.cnt[S_WOUT] += ctl.chain_tot[1];
+        ctl.cnt[S_COMPARES] += ctl.chain_tot[2];
+        ctl.cnt[S_EDINC] += ctl.chain_tot[3];
+      }
+      for (int k = 0; k < 4; ++k) ctl.chain_tot[k] = 0;
     }
-    for (int k = 0; k < 4; ++k) ctl.chain_tot[k] = 0;
   }
   __syncthreads();
   PH_MARK(11);

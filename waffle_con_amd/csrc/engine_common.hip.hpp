@@ -34,10 +34,20 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
   return v;
 }
+// Wave64 sum through DPP lane moves (VALU, no LDS round trips): quad swaps,
+// half-row and row mirrors leave every lane with its 16-lane row sum; the four
+// row sums are read into scalar registers. Returns the (uniform) total.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xf, 0xf, true);
+}
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
-  return v;
+  v += dpp_u32<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_u32<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp_u32<0x141>(v);  // row_half_mirror
+  v += dpp_u32<0x140>(v);  // row_mirror
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
