@@ -107,15 +107,17 @@ __device__ inline void chain_prepare(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_
   __syncthreads();
   SUB_T1(23, ta);
   SUB_T0(tb);
-  if (wave_id() == 0) {
-    // upcoming bases of each read's first tip (reads 0..63)
-    uint32_t bo_tip = kInactive, blen = 0;
-    WindowBytes rb{nullptr, nullptr, 0};
+  {
+    // upcoming bases of each read's first tip (reads 0..63); every wave
+    // predicts the steps t = 1 + wave (mod kWaves)
+    const uint32_t wave = (uint32_t)wave_id();
+    uint32_t bo_tip = kInactive, blen = 0, wb = 0;
+    const Sh<uint8_t>* win = E.L.cwin + (uint64_t)min((uint32_t)lane, E.n - 1) * 64;
     if ((uint32_t)lane < E.n) {
       Front f;
       front_load(rstate_load(&E.L.hot[lane]), f);
       if (f.e != kInactive) {
-        rb = WindowBytes{E.read(lane), E.L.cwin + (uint64_t)lane * 64, E.L.cwb[lane]};
+        wb = E.L.cwb[lane];
         blen = E.rlen(lane);
 #pragma unroll
         for (int k = kF - 1; k >= 0; --k)
@@ -125,59 +127,57 @@ __device__ inline void chain_prepare(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_
           }
       }
     }
-    // bytes are fetched eight steps at a time (independent loads under one
-    // wait; past the LDS window they come from HBM)
-    for (uint32_t t0 = 1; t0 < K; t0 += 8) {
-      uint32_t xs[8];
+    // all of this wave's bytes under one wait; LDS windows only: a read whose
+    // next bases lie past its window does not vote (the prediction is a
+    // guess, acceptance is exact)
+    constexpr uint32_t kPer = (kChainMax + kWaves - 1) / kWaves;
+    uint32_t xs[kPer];
 #pragma unroll
-      for (uint32_t u = 0; u < 8; ++u) {
-        const uint32_t t = t0 + u;
-        xs[u] = (bo_tip != kInactive && t < K && bo_tip + t < blen) ? rb(bo_tip + t) : 0x100u;
-      }
-      bool stop = false;
-#pragma unroll
-      for (uint32_t u = 0; u < 8; ++u) {
-        const uint32_t t = t0 + u;
-        if (t >= K) break;
-        const uint32_t x = xs[u];
-        // plurality of x over the wave (ties: the first-seen symbol); a
-        // first-seen symbol held by a strict majority is the plurality
-        uint64_t rem = ballot(x != 0x100u);
-        uint32_t best = 0x100u, bestc = 0;
-        if (rem) {
-          const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)x, __builtin_ctzll(rem));
-          const uint64_t mm = ballot(x == s);
-          const uint32_t c = (uint32_t)__popcll((unsigned long long)mm);
-          if (2 * c > (uint32_t)__popcll((unsigned long long)rem)) {
-            best = s;
-            rem = 0;
-          }
-        }
-        while (rem) {
-          const int l = __builtin_ctzll(rem);
-          const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)x, l);
-          const uint64_t mm = ballot(x == s);
-          const uint32_t c = (uint32_t)__popcll((unsigned long long)mm);
-          if (c > bestc) {
-            bestc = c;
-            best = s;
-          }
-          rem &= ~mm;
-        }
-        if (best == 0x100u) {
-          if (lane == 0) atomicMin(&ctl.chain_stop, t);  // nothing to predict N_{t+1} from
-          stop = true;
-          break;
-        }
-        if (lane == 0) E.L.cpred[t + 1] = (uint8_t)best;
-      }
-      if (stop) break;
+    for (uint32_t u = 0; u < kPer; ++u) {
+      const uint32_t t = 1 + wave + kWaves * u;
+      const uint32_t q = bo_tip + t - wb;
+      xs[u] = (bo_tip != kInactive && t < K && bo_tip + t < blen && q < 64u) ? (uint32_t)win[q] : 0x100u;
     }
-    wave_lds_sync();
-    // the predicted symbols extend the node's own consensus buffer in place
-    // (positions >= L0 are not part of the node)
-    if ((uint32_t)lane >= 1 && (uint32_t)lane <= K) v.con[L0 + lane - 1] = E.L.cpred[lane];
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      const uint32_t t = 1 + wave + kWaves * u;
+      if (t >= K) break;
+      const uint32_t x = xs[u];
+      // plurality of x over the wave (ties: the first-seen symbol); a
+      // first-seen symbol held by a strict majority is the plurality
+      uint64_t rem = ballot(x != 0x100u);
+      uint32_t best = 0x100u, bestc = 0;
+      if (rem) {
+        const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)x, __builtin_ctzll(rem));
+        const uint64_t mm = ballot(x == s);
+        const uint32_t c = (uint32_t)__popcll((unsigned long long)mm);
+        if (2 * c > (uint32_t)__popcll((unsigned long long)rem)) {
+          best = s;
+          rem = 0;
+        }
+      }
+      while (rem) {
+        const int l = __builtin_ctzll(rem);
+        const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+        const uint64_t mm = ballot(x == s);
+        const uint32_t c = (uint32_t)__popcll((unsigned long long)mm);
+        if (c > bestc) {
+          bestc = c;
+          best = s;
+        }
+        rem &= ~mm;
+      }
+      if (best == 0x100u) {
+        if (lane == 0) atomicMin(&ctl.chain_stop, t);  // nothing to predict N_{t+1} from
+        break;
+      }
+      if (lane == 0) E.L.cpred[t + 1] = (uint8_t)best;
+    }
   }
+  __syncthreads();
+  // the predicted symbols extend the node's own consensus buffer in place
+  // (positions >= L0 are not part of the node)
+  if (tid >= 1 && (uint32_t)tid <= K) v.con[L0 + tid - 1] = E.L.cpred[tid];
   SUB_T1(24, tb);
 }
 
@@ -297,29 +297,18 @@ static_assert(kF == 8, "vote_unit covers split <= 8");
 // Both passes add their work counters to ctl.chain_tot. Wavefront rows are
 // written lazily (thread_push<kLazy>): only when a diagonal leaves the
 // frontier, plus one flush of the final frontier.
-// Waves that walk the chain. Each walking wave runs the same per-step
-// instruction stream whatever its number of live lanes, and the workgroups of
-// a CU share its SIMDs, so fewer, fuller waves cost less issue time.
-#ifndef WC_WALK_WAVES
-#define WC_WALK_WAVES 4
-#endif
-__device__ __forceinline__ uint32_t walk_waves(uint32_t n) {
-  return n <= 64u * WC_WALK_WAVES ? (uint32_t)WC_WALK_WAVES : (uint32_t)kWaves;
-}
-
 template <bool kFirst>
 __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int lane = lane_id(), wave = wave_id();
-  // reads are dealt round-robin over the walking waves (read = lane * ww +
-  // wave), so the edit-distance increases, which a wave handles one read at a
-  // time, are spread over them
-  const uint32_t ww = walk_waves(E.n);
-  if ((uint32_t)wave >= ww || (uint32_t)wave >= E.n) return;  // no reads in this wave (no barriers below)
+  // reads are dealt round-robin over the waves (read = lane * kWaves + wave):
+  // every wave walks a quarter of the reads, so the edit-distance increases,
+  // which a wave handles one read at a time, are spread over all four
+  if ((uint32_t)wave >= E.n) return;  // no reads in this wave (no barriers below)
   const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
   const int wc = cfg.wildcard;
   SideView v = E.sv(top, 0);
-  const uint32_t r = (uint32_t)lane * ww + (uint32_t)wave;
+  const uint32_t r = (uint32_t)lane * kWaves + (uint32_t)wave;
   const bool has = r < E.n;
   Front f;
   f.e = kInactive;
@@ -346,9 +335,11 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
     const bool oob = win_tip_bytes(W, f, blen, x) && active;
     if (kFirst && ballot(oob) && lane == 0) atomicMin(&ctl.chain_stop, 0u);
   }
+  uint32_t nsym = uni((uint32_t)E.L.cpred[1]);
   for (uint32_t j = 1; j <= K; ++j) {
     if (kFirst && j > uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
-    const uint32_t sym = uni((uint32_t)E.L.cpred[j]);
+    const uint32_t sym = nsym;
+    nsym = j < K ? uni((uint32_t)E.L.cpred[j + 1]) : 0x100u;  // issued early: used next step (and as `pred`)
     const uint32_t olen = L0 + j;
     uint32_t cmp = 0;
     bool heavy = false;
@@ -368,7 +359,7 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
       hm &= hm - 1;
       if (lane == l) front_store(tmp, f);
       wave_lds_sync();
-      const uint32_t rl = (uint32_t)l * ww + (uint32_t)wave;
+      const uint32_t rl = (uint32_t)l * kWaves + (uint32_t)wave;
       if (kFirst && !((bak >> l) & 1ull)) {
         // first rewrite of this row in the chain: keep a copy in slot S (the
         // rows are otherwise only touched at frontier diagonals, which a
@@ -435,7 +426,7 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
       // step aggregates: cost; reads at their end; votes for the predicted
       // next symbol (P) and for all other symbols (O) in 1/840ths; counts of
       // multi-symbol reads and of fractional votes for the prediction
-      const uint32_t pred = j < K ? (uint32_t)E.L.cpred[j + 1] : 0x100u;
+      const uint32_t pred = nsym;
       uint32_t vp = 0, vo = 0;
       bool frac = false;
       if (active && o.n > 0) {
