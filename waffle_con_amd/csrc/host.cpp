@@ -341,9 +341,17 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
   if (sides != 1 || nmax > (uint32_t)kBlock) chain = 0;
   uint32_t pcap = 16;
   {
+    // A dual search keeps far more nodes queued than a single one (children
+    // of both consensuses, both sides' DWFAs per node: cfg3 loci need ~512
+    // slots). An exhausted pool restarts the search with a bigger one, so it
+    // gets up to 48 GiB of HBM over the batch (<= 256 MiB per workgroup).
     const uint64_t sb = slot_bytes(sides, nmax, wcap, lcap);
-    while (pcap < 256 && (uint64_t)(pcap * 2) * sb <= (16ull << 20) &&
-           lds_bytes(sides, pcap * 2, nmax, chain) <= 40 * 1024)
+    const uint64_t budget =
+        sides == 1 ? (16ull << 20)
+                   : std::max<uint64_t>(16ull << 20, std::min<uint64_t>(256ull << 20, (48ull << 30) / std::max<size_t>(ids.size(), 1)));
+    const uint32_t pmax = sides == 1 ? 256u : 1024u;
+    const uint64_t lmax = sides == 1 ? 40 * 1024 : 48 * 1024;
+    while (pcap < pmax && (uint64_t)(pcap * 2) * sb <= budget && lds_bytes(sides, pcap * 2, nmax, chain) <= lmax)
       pcap *= 2;
   }
   // longer chains amortise the per-chain work (prediction, acceptance, the
@@ -547,9 +555,13 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
         R.recs[id].push_back(std::move(rr));
       }
     }
+    // debug: one line per launch on stderr (WC_LAUNCH_LOG=1); off by default
+    if (getenv("WC_LAUNCH_LOG"))
+      fprintf(stderr, "[wc] sides=%u problems=%u grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u chain=%u ms=%.3f retry=%zu flags=0x%x\n",
+              sides, P, grid, per_cu, lds, pcap, wcap, lcap, chain, ms, retry.size(), rflags);
     ids = retry;
     if (rflags & ST_RETRY_WCAP) wcap = wcap * 2;
-    if (rflags & (ST_RETRY_PCAP | ST_RETRY_HEAP)) pcap = pcap * 2;
+    if (rflags & (ST_RETRY_PCAP | ST_RETRY_HEAP)) pcap = pcap * 4;  // a failed attempt costs nearly a full search
     if (rflags & ST_RETRY_LCAP) lcap = lcap * 2;
   }
   for (uint32_t id : ids) {
