@@ -70,7 +70,10 @@ def main():
         gpu, st = batch.dual_consensus(cfg)
         dt = time.perf_counter() - t0
         rep.update({"gpu_loci_per_s": a.loci / dt, "gpu_kernel_ms": st["kernel_ms"], "gpu_wall_s": dt,
-                    "launches": st["launches"]})
+                    "launches": st["launches"],
+                    "per_locus": {k: st[k] / a.loci for k in ("pops", "nodes_explored", "nodes_ignored",
+                                                              "updates", "ed_increases", "finalizes")},
+                    "peak_queue_size": st["peak_queue_size"]})
     import oracle_ffi as orc
     n = min(a.cpu_loci, a.loci)
     t0 = time.perf_counter()
@@ -80,6 +83,8 @@ def main():
     rep.update({"cpu_loci": n, "cpu_threads": a.threads, "cpu_loci_per_s": n / dt, "cpu_wall_s": dt})
     if gpu is not None:
         def norm(rs):
+            if isinstance(rs, Exception):
+                return repr(rs)
             return [(r.consensus1().sequence(), r.consensus2().sequence() if r.consensus2() else None,
                      list(r.is_consensus1())) for r in rs]
         ok = 0

@@ -112,6 +112,13 @@ std::string err_msg(int code) {
   }
 }
 
+// HBM the node pools of one launch may take: half of what is free plus the
+// context's cached workspace (reused by the launch)
+inline uint64_t pool_hbm(wc_ctx* ctx) {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 32ull << 30;
+  return ((uint64_t)fr + (uint64_t)ctx->ws.cap) / 2;
+}
 inline int set_err(wc_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return code;
@@ -342,13 +349,17 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
   uint32_t pcap = 16;
   {
     // A dual search keeps far more nodes queued than a single one (children
-    // of both consensuses, both sides' DWFAs per node: cfg3 loci need ~512
-    // slots). An exhausted pool restarts the search with a bigger one, so it
-    // gets up to 48 GiB of HBM over the batch (<= 256 MiB per workgroup).
+    // of both consensuses, both sides' DWFAs per node: cfg3 loci peak at ~480
+    // queued nodes). An exhausted pool restarts the search with a bigger one,
+    // so the dual pool gets up to half of the free HBM over the workgroups
+    // that can run at once (<= 256 MiB each).
     const uint64_t sb = slot_bytes(sides, nmax, wcap, lcap);
-    const uint64_t budget =
-        sides == 1 ? (16ull << 20)
-                   : std::max<uint64_t>(16ull << 20, std::min<uint64_t>(256ull << 20, (48ull << 30) / std::max<size_t>(ids.size(), 1)));
+    uint64_t dual_budget = 16ull << 20;
+    if (sides == 2) {
+      const uint64_t conc = std::max<uint64_t>(1, std::min<uint64_t>(ids.size(), 4ull * (uint64_t)ctx->n_cu));
+      dual_budget = std::max<uint64_t>(16ull << 20, std::min<uint64_t>(256ull << 20, pool_hbm(ctx) / conc));
+    }
+    const uint64_t budget = sides == 1 ? (16ull << 20) : dual_budget;
     const uint32_t pmax = sides == 1 ? 256u : 1024u;
     const uint64_t lmax = sides == 1 ? 40 * 1024 : 48 * 1024;
     while (pcap < pmax && (uint64_t)(pcap * 2) * sb <= budget && lds_bytes(sides, pcap * 2, nmax, chain) <= lmax)
@@ -561,7 +572,14 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
               sides, P, grid, per_cu, lds, pcap, wcap, lcap, chain, ms, retry.size(), rflags);
     ids = retry;
     if (rflags & ST_RETRY_WCAP) wcap = wcap * 2;
-    if (rflags & (ST_RETRY_PCAP | ST_RETRY_HEAP)) pcap = pcap * 4;  // a failed attempt costs nearly a full search
+    if (rflags & (ST_RETRY_PCAP | ST_RETRY_HEAP)) {
+      // a failed attempt costs nearly a full search: grow 4x when the HBM
+      // share allows it
+      const uint64_t conc = std::min<uint64_t>(ids.size(), 4ull * (uint64_t)ctx->n_cu);
+      const bool big = ws_bytes(sides, pcap * 4, nmax, wcap, lcap) * conc <= pool_hbm(ctx) &&
+                       lds_bytes(sides, pcap * 4, nmax, chain) <= 60 * 1024;
+      pcap = pcap * (big ? 4 : 2);
+    }
     if (rflags & ST_RETRY_LCAP) lcap = lcap * 2;
   }
   for (uint32_t id : ids) {
