@@ -1293,6 +1293,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         ctl.ovf = 0;
       }
       __syncthreads();
+      PH_MARK(13);
       if (uni(ctl.action) == 2) break;
       if (uni(ctl.action) == 1) continue;
       if (uni(ctl.status) != ST_OK) break;
@@ -1319,6 +1320,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
       }
       __syncthreads();
+      PH_MARK(1);
       if (uni(ctl.status) != ST_OK) break;
 
       // ---- finalize a clone (dual_consensus.rs:438-492) ----
@@ -1373,6 +1375,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         __syncthreads();
         if (uni(ctl.status) != ST_OK) break;
         if (uni(ctl.store_idx) >= 0) store_record(E, ctl, outp, top, tdual ? 2 : 1, tlens, tdual);
+        PH_MARK(2);
       }
 
       // ---- active_min_count growth (dual_consensus.rs:497-513) ----
@@ -1486,6 +1489,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         ctl.nchild = nc;
       }
       __syncthreads();
+      PH_MARK(3);
       if (uni(ctl.status) != ST_OK) break;
       const uint32_t nc = uni(ctl.nchild);
       if (nc == 0) {
@@ -1521,6 +1525,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           if (tdual) copy_side<false>(E, top, 1, slot, 1, tlens[1]);
           __syncthreads();
         }
+        PH_MARK(4);
         // activate_dual (dual_consensus.rs:957-976): side 2 := side 1
         if (kind == 2) copy_side<false>(E, slot, 0, slot, 1, tlens[0]);
         if (tid == 0) {
@@ -1552,6 +1557,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           activate_side<false>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
           if (cdual) activate_side<false>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
         }
+        PH_MARK(10);
         // prune (dual_consensus.rs:1030-1045) + priority (:1092-1168)
         {
           SideView a = E.sv(slot, 0), b = E.sv(slot, 1);
@@ -1592,6 +1598,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           ctl.ch_len[c] = max(m.len[0], m.len[1]);
         }
         __syncthreads();
+        PH_MARK(11);
         if (uni(ctl.status) != ST_OK) break;
       }
       if (uni(ctl.status) != ST_OK) break;
@@ -1603,6 +1610,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         }
       }
       __syncthreads();
+      PH_MARK(7);
     }
     finish_problem(A, ctl, outp, prob);
   }
