@@ -124,3 +124,16 @@ def test_no_device_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(w.WaffleConError):
         w.Context(0)
+
+
+def test_hpc_codec_and_synthetic_shapes():
+    from waffle_con_amd import synth
+    assert synth.hpc_compress(b"AACCCGTT") == b"ACGT"
+    assert synth.hpc_compress(b"") == b"" and synth.hpc_compress(b"A") == b"A"
+    assert synth.hpc_chains([b"AAC", b"GGT"]) == [[b"AC", b"AAC"], [b"GT", b"GGT"]]
+    a = synth.cfg3_locus(1, length=300, reads=4)
+    assert len(a) == 8 and a == synth.cfg3_locus(1, length=300, reads=4)  # seeded
+    c4 = synth.cfg4_locus(2, length=400, reads=3, gaps=(0, 5, 10, 20))
+    assert len(c4) == 12
+    c5 = synth.cfg5_locus(3, len_range=(200, 300), reads_range=(3, 5))
+    assert all(len(ch) == 2 and ch[0] == synth.hpc_compress(ch[1]) for ch in c5)

@@ -86,3 +86,24 @@ def test_priority_synthetic_vs_oracle(seed):
     chains = [[r, r[: len(r) // 2]] for r in reads]
     cfg = dict(min_count=3, wildcard=ord("*"))
     assert hip.priority_consensus(chains, **cfg) == orc.priority_consensus(chains, **cfg)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_cfg4_shape_length_gaps_vs_oracle(seed):
+    # SURVEY §8(d) cfg4 shape, scaled down (4 haplotypes with inserted
+    # segments of different lengths, grouped reads) through the multi-split
+    # PriorityConsensusDWFA with the priority tests' wildcard config
+    from waffle_con_amd import synth
+    reads = synth.cfg4_locus(300 + seed, length=500, reads=5, err=0.01, gaps=(0, 4, 9, 20))
+    chains = [[r] for r in reads]
+    cfg = dict(min_count=3, wildcard=ord("*"))
+    assert hip.priority_consensus(chains, **cfg) == orc.priority_consensus(chains, **cfg)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_cfg5_shape_hpc_chains_vs_oracle(seed):
+    # SURVEY §8(d) cfg5 shape, scaled down: [HPC(read), read] chains
+    from waffle_con_amd import synth
+    chains = synth.cfg5_locus(400 + seed, len_range=(200, 500), reads_range=(4, 7), err=0.01, max_variants=6)
+    cfg = dict(min_count=3, wildcard=ord("*"))
+    assert hip.priority_consensus(chains, **cfg) == orc.priority_consensus(chains, **cfg)

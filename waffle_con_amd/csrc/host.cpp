@@ -767,6 +767,9 @@ struct PWork {
   std::vector<uint8_t> inc;
   uint32_t level;
   std::vector<ConsRec> chain;
+  // the sub-problem's DualConsensusDWFA result, computed ahead of its turn
+  bool done = false;
+  std::unique_ptr<ProbRes> res;
 };
 }  // namespace
 
@@ -928,25 +931,74 @@ int wc_priority_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, c
       stacks[i].push_back(std::move(w));
     }
   }
+  // Every stacked sub-problem is an independent DualConsensusDWFA over its
+  // own reads, so all of them are evaluated in one launch per round, ahead of
+  // their turn. The stacks are then unwound in the reference's LIFO order
+  // (priority_consensus.rs:195-307) as far as evaluated results reach: the
+  // pop order, the chains, their order and the work counters (added when an
+  // item is popped) are those of the one-at-a-time loop; the number of rounds
+  // drops from the number of sub-problems to the depth of the split tree.
   double kms = 0;
   uint64_t launches = 0;
   for (;;) {
-    std::vector<uint32_t> active;
-    for (uint32_t i = 0; i < n; ++i)
-      if (alive[i] && !stacks[i].empty()) active.push_back(i);
-    if (active.empty()) break;
-    // this round's sub-problems: the top of every live stack
-    std::vector<PWork> items;
-    std::vector<std::vector<const uint8_t*>> rp(active.size());
-    std::vector<std::vector<uint64_t>> rl(active.size());
-    std::vector<std::vector<int64_t>> ro(active.size());
-    std::vector<wc_problem> sub(active.size());
-    for (size_t k = 0; k < active.size(); ++k) {
-      const uint32_t i = active[k];
+    // unwind: pop evaluated tops in LIFO order
+    for (uint32_t i = 0; i < n; ++i) {
       const wc_chain_problem& q = problems[i];
-      items.push_back(std::move(stacks[i].back()));
-      stacks[i].pop_back();
-      const PWork& w = items.back();
+      ProbRes& pr = R->probs[i];
+      while (alive[i] && !stacks[i].empty() && stacks[i].back().done) {
+        PWork w = std::move(stacks[i].back());
+        stacks[i].pop_back();
+        const ProbRes& d = *w.res;
+        for (int s = 0; s < S_NSTAT; ++s)
+          pr.stats[s] = s == S_PEAKQ ? std::max(pr.stats[s], d.stats[s]) : pr.stats[s] + d.stats[s];
+        if (d.status != WC_OK) {
+          pr.status = d.status;
+          pr.error = d.error;
+          alive[i] = false;
+          break;
+        }
+        const DualRec& ch = d.dual[0];
+        if (ch.has_c2) {
+          std::vector<uint8_t> a1(q.n_chains, 0), a2(q.n_chains, 0);
+          size_t idx = 0;
+          for (uint32_t c = 0; c < q.n_chains; ++c) {
+            if (!w.inc[c]) continue;
+            if (ch.is_c1[idx]) a1[c] = 1;
+            else a2[c] = 1;
+            idx++;
+          }
+          stacks[i].push_back(PWork{a1, w.level, w.chain});
+          stacks[i].push_back(PWork{a2, w.level, w.chain});
+        } else {
+          w.chain.push_back(ch.c1);
+          if (w.level + 1 == q.levels) {
+            cons[i].push_back(w.chain);
+            assigns[i].push_back(w.inc);
+          } else {
+            stacks[i].push_back(PWork{w.inc, w.level + 1, w.chain});
+          }
+        }
+      }
+    }
+    // evaluate every stacked, not yet evaluated sub-problem of the live problems
+    std::vector<PWork*> items;
+    std::vector<uint32_t> owner;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (!alive[i]) continue;
+      for (PWork& w : stacks[i])
+        if (!w.done) {
+          items.push_back(&w);
+          owner.push_back(i);
+        }
+    }
+    if (items.empty()) break;
+    std::vector<std::vector<const uint8_t*>> rp(items.size());
+    std::vector<std::vector<uint64_t>> rl(items.size());
+    std::vector<std::vector<int64_t>> ro(items.size());
+    std::vector<wc_problem> sub(items.size());
+    for (size_t k = 0; k < items.size(); ++k) {
+      const wc_chain_problem& q = problems[owner[k]];
+      const PWork& w = *items[k];
       for (uint32_t c = 0; c < q.n_chains; ++c) {
         if (!w.inc[c]) continue;
         rp[k].push_back(q.reads[c * q.levels + w.level]);
@@ -964,41 +1016,9 @@ int wc_priority_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, c
     std::unique_ptr<wc_results> D(dr);
     kms += D->stats.kernel_ms;
     launches += D->stats.launches;
-    for (size_t k = 0; k < active.size(); ++k) {
-      const uint32_t i = active[k];
-      const wc_chain_problem& q = problems[i];
-      ProbRes& pr = R->probs[i];
-      const ProbRes& d = D->probs[k];
-      for (int s = 0; s < S_NSTAT; ++s)
-        pr.stats[s] = s == S_PEAKQ ? std::max(pr.stats[s], d.stats[s]) : pr.stats[s] + d.stats[s];
-      if (d.status != WC_OK) {
-        pr.status = d.status;
-        pr.error = d.error;
-        alive[i] = false;
-        continue;
-      }
-      PWork& w = items[k];
-      const DualRec& ch = d.dual[0];
-      if (ch.has_c2) {
-        std::vector<uint8_t> a1(q.n_chains, 0), a2(q.n_chains, 0);
-        size_t idx = 0;
-        for (uint32_t c = 0; c < q.n_chains; ++c) {
-          if (!w.inc[c]) continue;
-          if (ch.is_c1[idx]) a1[c] = 1;
-          else a2[c] = 1;
-          idx++;
-        }
-        stacks[i].push_back(PWork{a1, w.level, w.chain});
-        stacks[i].push_back(PWork{a2, w.level, w.chain});
-      } else {
-        w.chain.push_back(ch.c1);
-        if (w.level + 1 == q.levels) {
-          cons[i].push_back(w.chain);
-          assigns[i].push_back(w.inc);
-        } else {
-          stacks[i].push_back(PWork{w.inc, w.level + 1, w.chain});
-        }
-      }
+    for (size_t k = 0; k < items.size(); ++k) {
+      items[k]->res.reset(new ProbRes(std::move(D->probs[k])));
+      items[k]->done = true;
     }
   }
   for (uint32_t i = 0; i < n; ++i) {
