@@ -1,28 +1,43 @@
 """Benchmark: read-DWFA extension updates/sec + consensus loci/sec on MI355X.
 
-Workload (BASELINE.json configs[1], north-star throughput form): ConsensusDWFA
-over synthetic HiFi-like loci — generate_test(alphabet 4, 10 kb, 100 reads,
-0.5% error) with seed = locus id, min_count = 100/4 (consensus_bench.rs
-convention). One "step" = the whole batch of loci through the device-resident
-engine: one engine launch over reads already resident in HBM (ResidentBatch,
-uploaded before the timed region), plus the read-back of the consensus
-records. The engine kernel time is measured separately with HIP events on the
-library's stream (kernel_ms_per_step) and drives the roofline figure.
+Workloads (--workload, default cfg2):
+  cfg2          BASELINE configs[1] throughput form: ConsensusDWFA over
+                generate_test(4, 10 kb, 100 reads, 0.5%) loci, seed = locus id,
+                min_count 25; --loci per GPU (weak scaling, loci sharded).
+  cfg2-latency  one cfg2 locus at a time (single-locus latency); CPU = 1 thread.
+  cfg3          DualConsensusDWFA on cfg3 loci (5 kb, 2 x 100 reads); --loci per GPU.
+  cfg4          PriorityConsensusDWFA on one cfg4 locus (4 x 50 reads x 8 kb, length gaps).
+  cfg5          PriorityConsensusDWFA over a FIXED batch of --loci cfg5 PGx loci
+                (default 10,000) split over the ranks by a cost-sorted queue
+                (strong scaling, no collective on the data path).
 
-roofline.traffic is the HBM byte count per launch measured by the rocprofv3
-PMC passes committed under profiles/ (FETCH_SIZE and WRITE_SIZE in separate
-passes, FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 note); it is
-reported only when the recorded workload equals this run's.
+One step = one pass of the engine over the rank's batch, reads resident in HBM
+(ResidentBatch uploaded before timing; priority workloads upload per call and
+that is inside the step). W untimed warmup steps, then exactly K timed steps
+between barrier + device sync; value = work of all ranks / max-over-ranks time.
 
-Multi-GPU: one process per GPU (torch.distributed.run); loci are sharded
-(weak scaling: every rank owns --loci loci), no collective on the data path.
-Rank 0 prints one JSON line.
+Reported beside `value`:
+  * e2e_loci_per_s (cfg2): fresh batches every step, i.e. Python marshalling +
+    pinned staging + H2D of the reads, double-buffered against the compute of
+    the previous batch (two contexts on the device).
+  * roofline: HBM bytes the dominant kernel actually moves (rocprofv3 PMC
+    passes committed under profiles/, same workload) / its HIP-event time, with
+    the reference-equivalent algorithmic bytes kept separately.
+  * cpu_baseline: the C++ oracle on every CPU this process may use
+    (affinity and cgroup quota), timed on the same host on a bounded sample.
+
+--gpus N without torch.distributed.run env: N worker processes are started
+(before anything touches the GPU) under torch.distributed.run.
 """
 import argparse
 import gc
 import json
 import os
+import platform
+import statistics
+import subprocess
 import sys
+import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 
@@ -30,60 +45,407 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "read-DWFA extension updates/sec + consensus loci/sec at 1/2/4/8 MI355X"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--loci", type=int, default=1000, help="loci per GPU")
-    ap.add_argument("--len", type=int, default=10000)
-    ap.add_argument("--reads", type=int, default=100)
-    ap.add_argument("--err", type=float, default=0.005)
-    ap.add_argument("--cpu-sample", type=int, default=1000, help="loci timed on the CPU oracle (rank 0, N=1)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--loci", type=int, default=None, help="loci per GPU (cfg2/cfg3) or in total (cfg5)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-oracle sample time")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable CPU")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     return ap.parse_args()
 
 
-def gen_loci(seeds, L, N, err, threads=16):
+# ---------------------------------------------------------------------------
+# host facts
+# ---------------------------------------------------------------------------
+def usable_cpus():
+    """CPUs this process may run on: the affinity set, capped by a cgroup v2
+    cpu.max quota when one is set."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def spawn_workers(a):
+    """--gpus N without a launcher: start N ranks under torch.distributed.run
+    (this process never initialises the GPU) and exit with their status."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+# ---------------------------------------------------------------------------
+# workloads
+# ---------------------------------------------------------------------------
+def _threads():
+    return max(1, min(16, usable_cpus()[0]))
+
+
+def gen_cfg2(seeds, L=10000, N=100, err=0.005):
     import waffle_con_amd as w
-    with ThreadPoolExecutor(max_workers=threads) as ex:
+    with ThreadPoolExecutor(max_workers=_threads()) as ex:
         return list(ex.map(lambda s: w.generate_test(4, L, N, err, s)[1], seeds))
 
 
-def cpu_baseline(loci, min_count, threads):
-    """CPU oracle (C++ restatement of the reference search) on a bounded sample."""
+def orc():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ffi as orc
-    orc.lib()
+    import oracle_ffi
+    oracle_ffi.lib()
+    return oracle_ffi
+
+
+def cpu_pool_run(fn, items, threads):
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=threads) as ex:
-        outs = list(ex.map(lambda p: orc.consensus(p, counters=True, min_count=min_count), loci))
-    dt = time.perf_counter() - t0
-    updates = sum(c["updates"] for _, c in outs)
-    return dt, updates, outs
+        outs = list(ex.map(fn, items))
+    return time.perf_counter() - t0, outs
 
 
-def pmc_traffic(loci, reads, length, err):
-    """HBM bytes per engine launch from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    if not os.path.exists(path):
+def sample_size(per_item_s, threads, target_s, cap):
+    return int(max(1, min(cap, round(target_s * threads / max(per_item_s, 1e-6)))))
+
+
+class Cfg2:
+    """ConsensusDWFA throughput (BASELINE configs[1], north-star 1,000-locus form)."""
+    name = "cfg2"
+    scaling = "weak"
+    kernel = "wc::single_engine_kernel"
+
+    def __init__(self, a, rank, world, ctx):
+        import waffle_con_amd as w
+        from waffle_con_amd.cdwfa_config import CdwfaConfig
+        self.a, self.ctx, self.rank, self.world = a, ctx, rank, world
+        self.n = a.loci or 1000
+        self.L, self.N, self.err = 10000, 100, 0.005
+        self.cfg = CdwfaConfig(min_count=self.N // 4)
+        from waffle_con_amd.shard import shard_seeds
+        self.seeds = shard_seeds(self.n, rank)
+        t0 = time.perf_counter()
+        self.loci = gen_cfg2(self.seeds, self.L, self.N, self.err)
+        self.gen_s = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        self.batch = w.ResidentBatch(self.loci, context=ctx)
+        self.upload_s = time.perf_counter() - t0
+        self.last = None
+
+    def step(self):
+        res, st = self.batch.consensus(self.cfg, return_errors=True)
+        bad = [r for r in res if isinstance(r, Exception)]
+        if bad:
+            raise RuntimeError("engine error: %s" % bad[0])
+        self.last = res
+        return st, len(res)
+
+    def config(self):
+        return {"workload": "ConsensusDWFA cfg2 throughput: %d loci/GPU x %d reads x %d bp @ %g error, min_count %d"
+                            % (self.n, self.N, self.L, self.err, self.N // 4),
+                "loci_per_gpu": self.n, "reads": self.N, "len": self.L, "error_rate": self.err,
+                "parallelism": "loci-sharded x%d (no collective)" % self.world}
+
+    def data(self):
+        return "synthetic: generate_test(4, %d, %d, %g) seeds 0..%d (reference RNG restated)" % (
+            self.L, self.N, self.err, self.n * self.world - 1)
+
+    def e2e(self, steps):
+        """Fresh batches every step: marshalling + pinned staging + H2D of batch
+        k+1 (upload context, own thread) overlap the compute of batch k (compute
+        context). Returns (loci/s, serial ms of one upload, serial ms of one compute)."""
+        import waffle_con_amd as w
+        up = self.ctx
+        run = w.Context(self.ctx.device)
+        bufs = [w.ResidentBatch(self.loci, context=up), w.ResidentBatch(self.loci, context=up)]
+        t0 = time.perf_counter()
+        bufs[0].refill(self.loci)
+        up_ms = (time.perf_counter() - t0) * 1e3
+        t0 = time.perf_counter()
+        bufs[0].consensus(self.cfg, context=run)
+        run_ms = (time.perf_counter() - t0) * 1e3
+        ready = [threading.Event() for _ in range(steps)]
+        free = [threading.Semaphore(1), threading.Semaphore(1)]
+        err = []
+
+        def uploader():
+            try:
+                for k in range(steps):
+                    free[k % 2].acquire()
+                    bufs[k % 2].refill(self.loci)
+                    ready[k].set()
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+                for ev in ready:
+                    ev.set()
+
+        t0 = time.perf_counter()
+        th = threading.Thread(target=uploader)
+        th.start()
+        for k in range(steps):
+            ready[k].wait()
+            if err:
+                break
+            bufs[k % 2].consensus(self.cfg, context=run)
+            free[k % 2].release()
+        th.join()
+        dt = time.perf_counter() - t0
+        if err:
+            raise err[0]
+        for b in bufs:
+            b.close()
+        run.close()
+        return steps * self.n / dt, up_ms, run_ms
+
+    def cpu(self, threads, target_s):
+        o = orc()
+        t0 = time.perf_counter()
+        o.consensus(self.loci[0], min_count=self.N // 4)
+        one = time.perf_counter() - t0
+        n = sample_size(one, threads, target_s, len(self.loci))
+        dt, outs = cpu_pool_run(lambda p: o.consensus(p, counters=True, min_count=self.N // 4), self.loci[:n], threads)
+        upd = sum(c["updates"] for _, c in outs)
+        ok = all([(c.sequence(), list(c.scores())) for c in self.last[i]] ==
+                 [(r["sequence"], r["scores"]) for r in outs[i][0]] for i in range(n))
+        return {"value": upd / dt, "unit": "updates/s", "loci_per_s": n / dt,
+                "sample": "%d loci of the same workload (seeds %d..%d), C++ oracle, one locus per thread, %.1f s wall"
+                          % (n, self.seeds[0], self.seeds[0] + n - 1, dt),
+                "gpu_matches_cpu_on_sample": ok, "checked": "sequences + per-read scores of every result"}
+
+
+class Cfg2Latency(Cfg2):
+    """One cfg2 locus per launch (single-locus configs, 1 CPU thread)."""
+    name = "cfg2-latency"
+    scaling = "weak"
+
+    def __init__(self, a, rank, world, ctx):
+        a.loci = 1
+        super().__init__(a, rank, world, ctx)
+
+    def config(self):
+        c = super().config()
+        c["workload"] = "ConsensusDWFA cfg2 single locus: %d reads x %d bp @ %g error, min_count %d (latency)" % (
+            self.N, self.L, self.err, self.N // 4)
+        return c
+
+    def e2e(self, steps):
         return None
-    with open(path) as f:
-        rec = json.load(f)
-    w = rec.get("workload", {})
-    if (w.get("loci_per_gpu"), w.get("reads"), w.get("len"), w.get("error_rate")) != (loci, reads, length, err):
+
+    def cpu(self, threads, target_s):
+        r = super().cpu(1, target_s)
+        r["cores"] = 1
+        return r
+
+
+class Cfg3(Cfg2):
+    """DualConsensusDWFA on cfg3 loci (BASELINE configs[2])."""
+    name = "cfg3"
+    kernel = "wc::dual_engine_kernel"
+
+    def __init__(self, a, rank, world, ctx):
+        import waffle_con_amd as w
+        from waffle_con_amd import synth
+        from waffle_con_amd.cdwfa_config import CdwfaConfig
+        self.a, self.ctx, self.rank, self.world = a, ctx, rank, world
+        self.n = a.loci or 768
+        self.cfg = CdwfaConfig()
+        self.seeds = list(range(rank * self.n, (rank + 1) * self.n))
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=_threads()) as ex:
+            self.loci = list(ex.map(synth.cfg3_locus, self.seeds))
+        self.gen_s = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        self.batch = w.ResidentBatch(self.loci, context=ctx)
+        self.upload_s = time.perf_counter() - t0
+
+    def step(self):
+        res, st = self.batch.dual_consensus(self.cfg, return_errors=True)
+        bad = [r for r in res if isinstance(r, Exception)]
+        if bad:
+            raise RuntimeError("engine error: %s" % bad[0])
+        self.last = res
+        return st, len(res)
+
+    def config(self):
+        return {"workload": "DualConsensusDWFA cfg3: %d loci/GPU, 5 kb haplotypes A/B (12 SNVs + 2 indels), "
+                            "2 x 100 reads @ 0.5%%, default config" % self.n,
+                "loci_per_gpu": self.n, "parallelism": "loci-sharded x%d (no collective)" % self.world}
+
+    def data(self):
+        return "synthetic: synth.cfg3_locus(seed) seeds %d..%d" % (0, self.n * self.world - 1)
+
+    def e2e(self, steps):
         return None
-    return rec.get("traffic_bytes_per_launch")
+
+    def cpu(self, threads, target_s):
+        o = orc()
+        t0 = time.perf_counter()
+        o.dual_consensus(self.loci[0])
+        one = time.perf_counter() - t0
+        n = sample_size(one, threads, target_s, len(self.loci))
+        dt, outs = cpu_pool_run(lambda p: o.dual_consensus(p, counters=True), self.loci[:n], threads)
+        upd = sum(c["updates"] for _, c in outs)
+
+        def norm(rs):
+            return [(r.consensus1().sequence(), r.consensus2().sequence() if r.consensus2() else None,
+                     list(r.is_consensus1()), list(r.scores1()), list(r.scores2())) for r in rs]
+        ok = all(norm(self.last[i]) == [(r["consensus1"]["sequence"],
+                                         r["consensus2"]["sequence"] if r["consensus2"] else None,
+                                         r["is_consensus1"], r["scores1"], r["scores2"]) for r in outs[i][0]]
+                 for i in range(n))
+        return {"value": upd / dt, "unit": "updates/s", "loci_per_s": n / dt,
+                "sample": "%d cfg3 loci, C++ oracle, one locus per thread, %.1f s wall" % (n, dt),
+                "gpu_matches_cpu_on_sample": ok}
+
+
+class Cfg5:
+    """PriorityConsensusDWFA over a fixed batch of cfg5 loci, strong-scaled."""
+    name = "cfg5"
+    scaling = "strong"
+    kernel = "wc::dual_engine_kernel"
+
+    def __init__(self, a, rank, world, ctx):
+        from waffle_con_amd import shard, synth
+        from waffle_con_amd.cdwfa_config import CdwfaConfig
+        self.a, self.ctx, self.rank, self.world = a, ctx, rank, world
+        self.total = a.loci or 10000
+        self.cfg = CdwfaConfig(wildcard=ord("*"))
+        t0 = time.perf_counter()
+        # every rank computes the same cost-sorted assignment from the loci's
+        # parameters (no generation, no communication) and generates its own loci
+        costs = [synth.cfg5_cost(s) for s in range(self.total)]
+        self.assign = shard.cost_sorted_assignment(costs, world)
+        self.mine = self.assign[rank]
+        with ThreadPoolExecutor(max_workers=_threads()) as ex:
+            self.loci = list(ex.map(synth.cfg5_locus, self.mine))
+        self.gen_s = time.perf_counter() - t0
+        self.upload_s = 0.0
+        self.n = len(self.loci)
+
+    def step(self):
+        import waffle_con_amd as w
+        probs = [(c, None, None) for c in self.loci]
+        res, st = w.priority_consensus_batch(probs, self.cfg, context=self.ctx, return_errors=True)
+        bad = [r for r in res if isinstance(r, Exception)]
+        if bad:
+            raise RuntimeError("engine error: %s" % bad[0])
+        self.last = res
+        return st, len(res)
+
+    def config(self):
+        return {"workload": "PriorityConsensusDWFA cfg5: fixed batch of %d PGx loci (1-6 kb, 2 haplotypes, 15-40 reads "
+                            "each @ 0.5%%, [HPC(read), read] chains, wildcard '*'), cost-sorted queue over %d GPU(s)"
+                            % (self.total, self.world),
+                "loci_total": self.total, "loci_this_rank": self.n,
+                "parallelism": "loci-sharded x%d, cost-sorted LPT assignment (no collective)" % self.world}
+
+    def data(self):
+        return "synthetic: synth.cfg5_locus(seed) seeds 0..%d" % (self.total - 1)
+
+    def e2e(self, steps):
+        return None
+
+    def cpu(self, threads, target_s):
+        o = orc()
+        t0 = time.perf_counter()
+        o.priority_consensus(self.loci[-1], wildcard=ord("*"))
+        one = time.perf_counter() - t0
+        # the rank's loci are in queue order (heaviest first): sample evenly
+        n = sample_size(one * 2, threads, target_s, len(self.loci))
+        idx = [int(k * len(self.loci) / n) for k in range(n)]
+        dt, outs = cpu_pool_run(lambda i: o.priority_consensus(self.loci[i], counters=True, wildcard=ord("*")), idx,
+                                threads)
+        upd = sum(c["updates"] for _, c in outs)
+        ok = all([[c.sequence() for c in ch] for ch in self.last[i].consensuses()] ==
+                 [[c["sequence"] for c in ch] for ch in outs[k][0]["consensuses"]] and
+                 list(self.last[i].sequence_indices()) == list(outs[k][0]["sequence_indices"])
+                 for k, i in enumerate(idx))
+        return {"value": upd / dt, "unit": "updates/s", "loci_per_s": n / dt,
+                "sample": "%d of the rank's cfg5 loci spread over the cost order, C++ oracle, %.1f s wall" % (n, dt),
+                "gpu_matches_cpu_on_sample": ok}
+
+
+class Cfg4(Cfg5):
+    """PriorityConsensusDWFA on one cfg4 locus (BASELINE configs[3])."""
+    name = "cfg4"
+    scaling = "weak"
+
+    def __init__(self, a, rank, world, ctx):
+        from waffle_con_amd import synth
+        from waffle_con_amd.cdwfa_config import CdwfaConfig
+        self.a, self.ctx, self.rank, self.world = a, ctx, rank, world
+        self.total = self.n = 1
+        self.cfg = CdwfaConfig(wildcard=ord("*"))
+        t0 = time.perf_counter()
+        self.loci = [[[r] for r in synth.cfg4_locus(4 + rank)]]
+        self.gen_s = time.perf_counter() - t0
+        self.upload_s = 0.0
+
+    def config(self):
+        return {"workload": "PriorityConsensusDWFA cfg4: one locus, 4 haplotypes x 50 reads x 8 kb, inserted "
+                            "segments {0, 25, 60, 150} bp + 3 SNVs each, 0.5% error, wildcard '*'",
+                "loci_per_gpu": 1, "parallelism": "replicas x%d" % self.world}
+
+    def data(self):
+        return "synthetic: synth.cfg4_locus(4 + rank)"
+
+    def cpu(self, threads, target_s):
+        return None  # the oracle needs ~2 min for this locus; measured separately (DESIGN.md §5)
+
+
+WORKLOADS = {"cfg2": Cfg2, "cfg2-latency": Cfg2Latency, "cfg3": Cfg3, "cfg4": Cfg4, "cfg5": Cfg5}
+
+
+# ---------------------------------------------------------------------------
+# roofline / profile records committed under profiles/
+# ---------------------------------------------------------------------------
+def profile_record(kind, workload_cfg):
+    """Latest committed PMC summary (profiles/r*_<kind>.json) recorded on this workload."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s.json" % kind)), reverse=True):
+        with open(path) as f:
+            rec = json.load(f)
+        if rec.get("workload") == workload_cfg:
+            rec["_file"] = os.path.relpath(path, ROOT)
+            return rec
+    return None
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_workers(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world:
+        print("bench.py: --gpus %d but WORLD_SIZE %d" % (a.gpus, world), file=sys.stderr)
+        sys.exit(2)
     # torch ships its own HIP runtime next to the one the library links: torch
     # must initialise the device first, or its later init finds no GPU
     import torch
@@ -95,75 +457,71 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     import waffle_con_amd as w
-    from waffle_con_amd.cdwfa_config import CdwfaConfig
+    from waffle_con_amd import shard
 
     ctx = w.Context(local_rank)
-    cfg = CdwfaConfig(min_count=a.reads // 4)
-    from waffle_con_amd.shard import shard_seeds
-    seeds = shard_seeds(a.loci, rank)
-    t0 = time.perf_counter()
-    loci = gen_loci(seeds, a.len, a.reads, a.err)
-    gen_s = time.perf_counter() - t0
-
-    t0 = time.perf_counter()
-    batch = w.ResidentBatch(loci, context=ctx)  # reads resident in HBM before timing
-    upload_s = time.perf_counter() - t0
-
-    def step():
-        res, stats = batch.consensus(cfg, return_errors=True)
-        bad = [r for r in res if isinstance(r, Exception)]
-        if bad:
-            raise RuntimeError("engine error: %s" % bad[0])
-        return res, stats
-
-    from waffle_con_amd import shard
+    W = WORKLOADS[a.workload](a, rank, world, ctx)
 
     def sync():
         torch.cuda.synchronize()
 
     for _ in range(a.warmup):
-        step()
-    # the setup (torch, 1000 loci of reads) leaves a large Python heap: move it
-    # to the permanent generation so a full collection inside the timed region
-    # does not traverse it
+        W.step()
+    # the setup leaves a large Python heap: move it to the permanent generation
+    # so a full collection inside the timed region does not traverse it
     gc.collect()
     gc.freeze()
-    kernel_ms, upd, wout, cmp = 0.0, 0, 0, 0
-    last = None
+    kernel_ms, upd, wout, cmp, loci, launches = 0.0, 0, 0, 0, 0, 0
+    step_ms = []
     with shard.Timer(dist, sync) as tm:
         for _ in range(a.steps):
-            last, st = step()
+            t0 = time.perf_counter()
+            st, nl = W.step()
+            step_ms.append((time.perf_counter() - t0) * 1e3)
             kernel_ms += st["kernel_ms"]
             upd += st["updates"]
             wout += st["w_out"]
             cmp += st["compares"]
+            launches += st["launches"]
+            loci += nl
     elapsed, total_upd, total_loci = shard.reduce_run(
-        dist, tm.elapsed, upd, a.loci * a.steps, device="cuda" if dist is not None else None)
+        dist, tm.elapsed, upd, loci, device="cuda" if dist is not None else None)
+
+    e2e = None
+    if world == 1 and not a.no_e2e:
+        e2e = W.e2e(max(3, a.steps))
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
 
-    # roofline of the engine kernel: algorithmic bytes per launch / kernel time
-    per_launch_bytes = (8.0 * wout + 2.0 * cmp) / a.steps
+    cfgd = W.config()
     avg_kernel_s = kernel_ms / a.steps / 1e3
-    achieved = per_launch_bytes / avg_kernel_s / 1e9
-    correct = sum(1 for r in last if r and r[0].sequence() is not None)
-    traffic = pmc_traffic(a.loci, a.reads, a.len, a.err)
-    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "wc::single_engine_kernel",
-                "algorithmic_bytes_per_launch": per_launch_bytes,
-                # `achieved` counts the reference's bytes (every wavefront entry
-                # read and written per update, every byte compare); the engine
-                # skips the stuck diagonals, so it can exceed the HBM peak. The
-                # bytes it really moves are the PMC traffic:
-                "measured_gbs": (traffic / avg_kernel_s / 1e9) if traffic else None,
-                "measured_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None}
+    ref_bytes = (8.0 * wout + 2.0 * cmp) / a.steps  # SURVEY §8(d) B_upd summed, per step
+    pmc = profile_record("pmc_traffic", cfgd["workload"])
+    traffic = pmc.get("traffic_bytes_per_launch") if pmc else None
+    launches_per_step = launches / a.steps
+    per_launch_s = avg_kernel_s / max(launches_per_step, 1)
+    roofline = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": W.kernel,
+                "achieved": None, "frac": None, "traffic": traffic,
+                "kernel_ms_per_launch": per_launch_s * 1e3,
+                "reference_equiv_bytes_per_step": ref_bytes,
+                "reference_equiv_gbs": ref_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else None,
+                "note": "achieved = HBM bytes the kernel moves (PMC, per launch) / HIP-event kernel time. The "
+                        "search is latency-bound (one sequential search per locus); reference_equiv counts the "
+                        "reference's wavefront re-reads that the frontier cache skips and is not a byte count."}
+    if traffic:
+        roofline["achieved"] = traffic / per_launch_s / 1e9
+        roofline["frac"] = roofline["achieved"] / HBM_PEAK_GBS
+        roofline["pmc_source"] = pmc["_file"]
+    issue = profile_record("issue_view", cfgd["workload"])
+    if issue:
+        roofline["issue_view"] = {k: v for k, v in issue.items() if not k.startswith("_") and k != "workload"}
+        roofline["issue_view"]["source"] = issue["_file"]
 
     line = {
-        "metric": "read-DWFA extension updates/sec + consensus loci/sec at 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": total_upd / elapsed,
         "unit": "updates/s",
         "loci_per_s": total_loci / elapsed,
@@ -171,32 +529,33 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
+        "ms_per_step_median": statistics.median(step_ms),
         "kernel_ms_per_step": kernel_ms / a.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": W.scaling,
         "vs_baseline": None,
         "dtype": "u8/u32 (integer DWFA) + f64 votes",
-        "data": "synthetic: generate_test(4, %d, %d, %g) seeds 0..%d (reference RNG restated)" % (
-            a.len, a.reads, a.err, a.loci * world - 1),
-        "config": {"workload": "ConsensusDWFA cfg2 throughput: %d loci/GPU x %d reads x %d bp @ %g error, "
-                               "min_count %d" % (a.loci, a.reads, a.len, a.err, a.reads // 4),
-                   "loci_per_gpu": a.loci, "reads": a.reads, "len": a.len, "error_rate": a.err,
-                   "parallelism": "loci-sharded x%d (no collective)" % world},
+        "data": W.data(),
+        "config": cfgd,
         "roofline": roofline,
-        "gen_s": gen_s,
-        "upload_s": upload_s,
-        "upload_bytes": batch.bytes,
-        "results_ok": correct,
+        "gen_s": W.gen_s,
+        "upload_s": W.upload_s,
     }
+    if e2e:
+        line["e2e_loci_per_s"], line["e2e_upload_ms"], line["e2e_compute_ms"] = e2e
+        line["e2e_note"] = ("fresh batch every step: Python marshalling + pinned staging + H2D of the reads, "
+                            "double-buffered against the previous batch's compute")
     if world == 1 and not a.no_cpu:
-        n = min(a.cpu_sample, len(loci))
-        dt, cu, outs = cpu_baseline(loci[:n], a.reads // 4, a.cpu_threads)
-        # parity spot check on the sample: GPU result == oracle result
-        match = all([c.sequence() for c in last[i]] == [r["sequence"] for r in outs[i][0]] for i in range(n))
-        line["cpu_baseline"] = {"value": cu / dt, "unit": "updates/s", "loci_per_s": n / dt, "cores": a.cpu_threads,
-                                "kind": "port", "sample": "%d loci of the same workload (seeds 0..%d), "
-                                                          "C++ oracle, %d threads, %.1f s wall" % (n, n - 1, a.cpu_threads, dt),
-                                "gpu_matches_cpu_on_sample": match}
+        cores, aff, quota = usable_cpus()
+        threads = a.cpu_threads or cores
+        cb = W.cpu(threads, a.cpu_seconds)
+        if cb:
+            cb.setdefault("cores", threads)
+            cb.update({"kind": "port", "cpu_model": cpu_model(), "affinity_cpus": aff, "cgroup_quota_cpus": quota})
+            line["cpu_baseline"] = cb
+            line["gpu_vs_cpu_loci"] = line["loci_per_s"] / cb["loci_per_s"]
+            if e2e:
+                line["e2e_vs_cpu_loci"] = line["e2e_loci_per_s"] / cb["loci_per_s"]
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

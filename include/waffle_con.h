@@ -34,7 +34,11 @@ enum {
   WC_E_ROOT_INACTIVE = 8,   /* consensus.rs:396, dual_consensus.rs:843 */
   WC_E_BAD_INPUT = 9,       /* priority_consensus.rs:144,148; empty inputs */
   WC_E_INVARIANT = 10,      /* reference assert!/panic sites */
-  WC_E_LIMIT = 11,          /* a device capacity limit was exceeded after retries */
+  WC_E_LIMIT = 11,          /* a device capacity limit was exceeded after retries. Hard limits
+                             * (the reference has none): at most 8 distinct symbols at one read's
+                             * wavefront tips, 14 distinct voted symbols per node side and 64
+                             * children per node (DNA plus a wildcard and N needs 6). Wavefront,
+                             * node-pool, consensus and result capacities grow by retry instead. */
   WC_E_HIP = 12,            /* HIP runtime failure (no device, launch failure) */
 };
 
@@ -106,6 +110,10 @@ int wc_priority_consensus_batch(wc_ctx* ctx, const wc_config* cfg, uint32_t n, c
  * wc_batch_consensus with the reads already resident). */
 typedef struct wc_batch wc_batch;
 int wc_batch_create(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch** out);
+/* Re-uploads a new set of problems into an existing batch, reusing its device
+ * buffers when they are large enough (no allocation, so no device-wide
+ * synchronisation): the streaming / double-buffered input path. */
+int wc_batch_refill(wc_ctx* ctx, wc_batch* b, uint32_t n, const wc_problem* problems);
 void wc_batch_free(wc_batch* b);
 uint64_t wc_batch_bytes(const wc_batch* b);
 int wc_batch_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out);

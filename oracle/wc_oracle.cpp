@@ -956,13 +956,16 @@ static uint64_t fx_hash_opt(int64_t v) {
   return fx_add(fx_add(0, 1), (uint64_t)v);
 }
 
-static std::vector<int64_t> seed_group_order(const std::vector<int64_t>& groups) {
+std::vector<int64_t> seed_group_order(const std::vector<int64_t>& groups) {
   // hashbrown table of Option<usize> keys (16-B entries): same placement rules as
   // FxByteMap but with a 64-bit hash
+  // built by `.collect()` (priority_consensus.rs:180): hashbrown's extend
+  // reserves the iterator's exact size hint (n_chains) up front, so the table
+  // starts at capacity_to_buckets(n_chains) buckets
   std::vector<int64_t> keys;
-  std::vector<int64_t> table;  // slot -> key index (-1 empty)
+  std::vector<int64_t> table(fx_buckets_for(std::max<size_t>(groups.size(), 1)), -1);  // slot -> key index
   std::vector<uint64_t> hashes;
-  size_t items = 0, growth_left = 0;
+  size_t items = 0, growth_left = fx_capacity(table.size());
   auto insert_slot = [&](uint64_t h) -> size_t {
     size_t B = table.size(), mask = B - 1, pos = (size_t)h & mask;
     if (B < 16) {

@@ -123,4 +123,6 @@ PriorityOut consensus_priority(const Config& cfg, const std::vector<std::vector<
 std::vector<double> test_ed_weights(const std::vector<Seq>& seqs, uint8_t s1, uint8_t s2, bool early, bool side1,
                                     bool weight_by_ed);
 
+// FxHashSet<Option<usize>> iteration order of the seed groups (priority_consensus.rs:180); -1 = None
+std::vector<int64_t> seed_group_order(const std::vector<int64_t>& groups);
 }  // namespace wco

@@ -295,4 +295,12 @@ uint32_t orc_fxmap_order(const uint8_t* keys, uint32_t n, uint8_t* out) {
   m.for_each([&](uint8_t s, uint64_t) { out[k++] = s; });
   return k;
 }
+
+// seed-group processing order (priority_consensus.rs:180), -1 = None; returns the key count
+uint32_t orc_seed_group_order(const int64_t* groups, uint32_t n, int64_t* out) {
+  std::vector<int64_t> g(groups, groups + n);
+  std::vector<int64_t> o = seed_group_order(g);
+  for (size_t i = 0; i < o.size(); ++i) out[i] = o[i];
+  return (uint32_t)o.size();
+}
 }

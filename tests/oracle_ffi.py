@@ -94,6 +94,9 @@ def lib():
         L.orc_wfa_ed_config.restype = ctypes.c_uint64
         L.orc_wfa_ed_config.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                                         ctypes.c_uint8, ctypes.c_int32]
+        L.orc_seed_group_order.restype = ctypes.c_uint32
+        L.orc_seed_group_order.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.c_int64)]
         L.orc_fxmap_order.restype = ctypes.c_uint32
         L.orc_fxmap_order.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p]
         _LIB = L
@@ -241,3 +244,12 @@ def fxmap_order(keys):
     out = ctypes.create_string_buffer(256)
     n = lib().orc_fxmap_order(bytes(keys), len(keys), out)
     return list(out.raw[:n])
+
+
+def seed_group_order(groups):
+    """Processing order of the seed groups (priority_consensus.rs:180); None = no seed."""
+    n = len(groups)
+    g = (ctypes.c_int64 * max(1, n))(*[-1 if x is None else x for x in groups])
+    out = (ctypes.c_int64 * max(1, n))()
+    k = lib().orc_seed_group_order(g, n, out)
+    return [None if out[i] < 0 else out[i] for i in range(k)]

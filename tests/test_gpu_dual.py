@@ -107,3 +107,29 @@ def test_cfg5_shape_hpc_chains_vs_oracle(seed):
     chains = synth.cfg5_locus(400 + seed, len_range=(200, 500), reads_range=(4, 7), err=0.01, max_variants=6)
     cfg = dict(min_count=3, wildcard=ord("*"))
     assert hip.priority_consensus(chains, **cfg) == orc.priority_consensus(chains, **cfg)
+
+
+@pytest.mark.parametrize("rmax", ["1", "2"])
+def test_result_record_retry(rmax, monkeypatch):
+    """More tied results than device result records (WC_RMAX shrinks the first
+    attempt) rerun with more records: nothing is dropped (dual_consensus.rs:744-766)."""
+    monkeypatch.setenv("WC_RMAX", rmax)
+    case = rc.DUAL_CASES["equal_options"]
+    seqs = [rc.b(s) for s in case["seqs"]]
+    exp = orc.dual_consensus(seqs, **case["cfg"])
+    assert len(exp) == 6
+    assert hip.dual_consensus(seqs, **case["cfg"]) == exp
+    single = rc.SINGLE_CASES["dual_sequence"]
+    s = [rc.b(x) for x in single["seqs"]]
+    assert hip.consensus(s, **single["cfg"]) == orc.consensus(s, **single["cfg"])
+
+
+def test_alphabet_limit_is_a_clear_error():
+    """The device engine votes at most 14 distinct symbols per node side
+    (engine_shared.hpp kKout); a wider alphabet at one node is reported as
+    WC_E_LIMIT, never as a wrong answer. The reference accepts any u8 alphabet."""
+    import waffle_con_amd as w
+    reads = [bytes([65 + i]) * 5 for i in range(20)]  # 20 distinct symbols at the root
+    with pytest.raises(w.WaffleConError) as e:
+        hip.consensus(reads, min_count=1)
+    assert e.value.code == 11 and "limit" in str(e.value)

@@ -6,7 +6,6 @@ loci. Diagnostic (not the headline bench). Usage:
 import argparse
 import json
 import os
-import random
 import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -16,38 +15,6 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def mutate(rng, s, rate):
-    out = bytearray()
-    for c in s:
-        r = rng.random()
-        if r < rate / 3:
-            out.append(rng.choice(b"ACGT".replace(bytes([c]), b"")))
-        elif r < 2 * rate / 3:
-            out.append(c)
-            out.append(rng.choice(b"ACGT"))
-        elif r < rate:
-            continue
-        else:
-            out.append(c)
-    return bytes(out)
-
-
-def cfg3_locus(seed, length=5000, reads=100, err=0.005):
-    rng = random.Random(seed)
-    a = bytes(rng.choice(b"ACGT") for _ in range(length))
-    b = bytearray(a)
-    for p in sorted(rng.sample(range(50, length - 50), 14), reverse=True)[:12]:
-        b[p] = rng.choice(b"ACGT".replace(bytes([b[p]]), b""))
-    for p in sorted(rng.sample(range(50, length - 50), 2), reverse=True):
-        k = rng.randint(1, 3)
-        if rng.random() < 0.5:
-            del b[p:p + k]
-        else:
-            b[p:p] = bytes(rng.choice(b"ACGT") for _ in range(k))
-    b = bytes(b)
-    return [mutate(rng, a, err) for _ in range(reads)] + [mutate(rng, b, err) for _ in range(reads)]
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--loci", type=int, default=256)
@@ -55,7 +22,8 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--no-gpu", action="store_true")
     a = ap.parse_args()
-    loci = [cfg3_locus(s) for s in range(a.loci)]
+    from waffle_con_amd import synth
+    loci = [synth.cfg3_locus(s) for s in range(a.loci)]
     rep = {"loci": a.loci, "workload": "cfg3-shaped DualConsensusDWFA: 2 x 100 reads x 5 kb @ 0.5%"}
     gpu = None
     if not a.no_gpu:

@@ -110,7 +110,7 @@ class WcDwfaJob(ctypes.Structure):
 EXPORTED = (
     "wc_config_default", "wc_ctx_create", "wc_ctx_destroy", "wc_last_error",
     "wc_consensus_batch", "wc_dual_consensus_batch", "wc_priority_consensus_batch",
-    "wc_batch_create", "wc_batch_free", "wc_batch_bytes", "wc_batch_consensus", "wc_batch_dual_consensus",
+    "wc_batch_create", "wc_batch_refill", "wc_batch_free", "wc_batch_bytes", "wc_batch_consensus", "wc_batch_dual_consensus",
     "wc_results_free", "wc_results_problems", "wc_results_status", "wc_results_error",
     "wc_results_count", "wc_results_single", "wc_results_dual", "wc_results_chain_len",
     "wc_results_chain", "wc_results_sequence_indices", "wc_results_stats",
@@ -143,6 +143,7 @@ def lib():
             fn = getattr(L, f)
             fn.argtypes = [vp, ctypes.POINTER(WcConfig), ctypes.c_uint32, ctypes.POINTER(pt), ctypes.POINTER(vp)]
         L.wc_batch_create.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(WcProblem), ctypes.POINTER(vp)]
+        L.wc_batch_refill.argtypes = [vp, vp, ctypes.c_uint32, ctypes.POINTER(WcProblem)]
         L.wc_batch_free.argtypes = [vp]
         L.wc_batch_bytes.argtypes = [vp]
         L.wc_batch_bytes.restype = ctypes.c_uint64
@@ -218,10 +219,11 @@ class Context:
 
 
 def default_context():
-    """Per-thread default context on the current device (LOCAL_RANK or 0)."""
+    """Per-thread default context: device WAFFLE_CON_DEVICE if set, else
+    LOCAL_RANK (one process per GPU under torch.distributed.run), else 0."""
     ctx = getattr(_ctx_local, "ctx", None)
     if ctx is None:
-        dev = int(os.environ.get("WAFFLE_CON_DEVICE", "0"))
+        dev = int(os.environ.get("WAFFLE_CON_DEVICE", os.environ.get("LOCAL_RANK", "0")))
         ctx = Context(dev)
         _ctx_local.ctx = ctx
     return ctx
@@ -248,13 +250,15 @@ def make_config(config):
 
 
 class PackedReads:
-    """Keeps ctypes buffers alive for one call."""
+    """Read pointer/length arrays for one call. Zero-copy: the pointers address
+    the bytes objects' own buffers (kept alive here); the library copies the
+    bytes once, into its pinned upload staging."""
 
     def __init__(self, seqs):
-        self.bufs = [ctypes.create_string_buffer(bytes(s), max(1, len(s))) for s in seqs]
+        self.bufs = [s if type(s) is bytes else bytes(s) for s in seqs]
         n = max(1, len(seqs))
-        self.ptrs = (_u8p * n)(*[ctypes.cast(b, _u8p) for b in self.bufs])
-        self.lens = (ctypes.c_uint64 * n)(*[len(s) for s in seqs])
+        self.ptrs = (ctypes.c_char_p * n)(*self.bufs)
+        self.lens = (ctypes.c_uint64 * n)(*map(len, self.bufs))
 
 
 def offsets_array(offsets):

@@ -22,17 +22,32 @@ class ResidentBatch:
         self.handle = h
         self.bytes = L.wc_batch_bytes(h)
 
+    def refill(self, problems):
+        """Upload a new set of problems into this batch's device buffers
+        (wc_batch_refill: reused when large enough, so no allocation)."""
+        L = _lib.lib()
+        self._batch = [(p, None) if not isinstance(p, tuple) else p for p in problems]
+        arr, keep = _problems(self._batch)
+        rc = L.wc_batch_refill(self.ctx.handle, self.handle, len(self._batch), arr)
+        if rc != _lib.WC_OK:
+            raise _lib.WaffleConError("wc_batch_refill failed: " + self.ctx.last_error(), rc)
+        self.bytes = L.wc_batch_bytes(self.handle)
+
     def __len__(self):
         return len(self._batch)
 
-    def consensus(self, config=None, return_errors=True, per_problem=False):
+    def consensus(self, config=None, return_errors=True, per_problem=False, context=None):
+        """ConsensusDWFA over every problem of the batch. `context` may name
+        another context on the same device (e.g. a compute context while this
+        batch's own context uploads the next batch)."""
         config = config or CdwfaConfig()
+        ctx = context or self.ctx
         L = _lib.lib()
         cfg = _lib.make_config(config)
         res = ctypes.c_void_p()
-        rc = L.wc_batch_consensus(self.ctx.handle, self.handle, ctypes.byref(cfg), ctypes.byref(res))
+        rc = L.wc_batch_consensus(ctx.handle, self.handle, ctypes.byref(cfg), ctypes.byref(res))
         if rc != _lib.WC_OK:
-            raise _lib.WaffleConError("wc_batch_consensus failed: " + self.ctx.last_error(), rc)
+            raise _lib.WaffleConError("wc_batch_consensus failed: " + ctx.last_error(), rc)
         try:
             out = []
             for p in range(len(self._batch)):
@@ -56,14 +71,15 @@ class ResidentBatch:
         finally:
             L.wc_results_free(res)
 
-    def dual_consensus(self, config=None, return_errors=True):
+    def dual_consensus(self, config=None, return_errors=True, context=None):
         config = config or CdwfaConfig()
+        ctx = context or self.ctx
         L = _lib.lib()
         cfg = _lib.make_config(config)
         res = ctypes.c_void_p()
-        rc = L.wc_batch_dual_consensus(self.ctx.handle, self.handle, ctypes.byref(cfg), ctypes.byref(res))
+        rc = L.wc_batch_dual_consensus(ctx.handle, self.handle, ctypes.byref(cfg), ctypes.byref(res))
         if rc != _lib.WC_OK:
-            raise _lib.WaffleConError("wc_batch_dual_consensus failed: " + self.ctx.last_error(), rc)
+            raise _lib.WaffleConError("wc_batch_dual_consensus failed: " + ctx.last_error(), rc)
         try:
             return _dual_results(res, self._batch, config, L, return_errors), _stats(res, L)
         finally:

@@ -954,6 +954,8 @@ __device__ inline void trace_pop(const EngineArgs& A, uint32_t prob, const HeapE
 __device__ inline void finish_problem(const EngineArgs& A, Sh<Ctl>& ctl, uint8_t* outp, uint32_t prob) {
   __syncthreads();
   if (threadIdx.x == 0) {
+    // every tied result must have a record; otherwise rerun with more records
+    if (ctl.status == ST_OK && ctl.n_ret > A.rmax) ctl.status = ST_RETRY | ST_RETRY_RMAX;
     ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
     A.status[prob] = ctl.status;
     for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)prob * S_NSTAT + s] = ctl.cnt[s];

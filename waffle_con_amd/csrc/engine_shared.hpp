@@ -20,6 +20,7 @@ enum : uint32_t {
   ST_RETRY_PCAP = 0x2,       // node pool exhausted
   ST_RETRY_LCAP = 0x4,       // consensus outgrew lcap
   ST_RETRY_HEAP = 0x8,       // priority queue outgrew pcap
+  ST_RETRY_RMAX = 0x10,      // more tied results than result records
 };
 
 enum StatIdx : int {

@@ -20,6 +20,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/waffle_con.h"
@@ -91,6 +92,7 @@ struct wc_ctx {
   std::string err;
   DevBuf ract, probs, ws, out, status, stats, counter, jobs, act;
   HostBuf stage;
+  HostBuf upstage;  // pinned staging of batch uploads (reused across batches)
 };
 
 namespace {
@@ -106,7 +108,9 @@ std::string err_msg(int code) {
     case WC_E_ROOT_INACTIVE: return "Root consensus node has no initially active sequences.";
     case WC_E_BAD_INPUT: return "invalid input";
     case WC_E_INVARIANT: return "internal invariant violated";
-    case WC_E_LIMIT: return "device capacity limit exceeded";
+    case WC_E_LIMIT:
+      return "device capacity limit exceeded (alphabet: more than 8 distinct symbols at one read's wavefront tips "
+             "or 14 voted at one node side; or more than 64 children of one node)";
     case WC_E_HIP: return "HIP runtime failure";
     default: return "ok";
   }
@@ -211,38 +215,82 @@ struct RawRecord {
 };
 
 namespace {
+// Copies every read of `problems` into one 16-byte-aligned arena and uploads it.
+// The host side is one pass of memcpy into pinned staging (split over threads
+// by bytes), then a single DMA; the device buffer of `b` is reused when it is
+// large enough (wc_batch_refill), so a refill needs no allocation.
 int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* b) {
   b->ctx = ctx;
-  b->probs.resize(n);
-  std::vector<uint64_t> roff;
-  uint64_t total = 0;
-  for (uint32_t i = 0; i < n; ++i)
-    for (uint32_t r = 0; r < problems[i].n_reads; ++r) total += (problems[i].lens[r] + 15) & ~15ull;
-  // reads start 16-byte aligned; 64 bytes of tail padding let the engine load
-  // 64-byte windows with 16-byte accesses anywhere inside a read
-  std::vector<uint8_t> h(total + 64);
-  uint64_t pos = 0;
+  b->probs.assign(n, BatchProblem());
+  b->rlen_h.clear();
+  uint64_t nr = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (problems[i].n_reads && (!problems[i].reads || !problems[i].lens))
+      return set_err(ctx, WC_E_BAD_INPUT, "problem with reads but no read/length arrays");
+    nr += problems[i].n_reads;
+  }
+  std::vector<uint64_t> roff(nr);
+  b->rlen_h.resize(nr);
+  std::vector<const uint8_t*> src(nr);
+  uint64_t pos = 0, k = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const wc_problem& p = problems[i];
     BatchProblem& q = b->probs[i];
-    q.read_begin = (uint32_t)roff.size();
+    q.read_begin = (uint32_t)k;
     q.n_reads = p.n_reads;
     q.offsets.assign(p.n_reads, -1);
-    for (uint32_t r = 0; r < p.n_reads; ++r) {
+    for (uint32_t r = 0; r < p.n_reads; ++r, ++k) {
       if (p.offsets) q.offsets[r] = p.offsets[r] < 0 ? -1 : p.offsets[r];
-      roff.push_back(pos);
-      b->rlen_h.push_back((uint32_t)p.lens[r]);
-      if (p.lens[r]) memcpy(h.data() + pos, p.reads[r], p.lens[r]);
+      if (p.lens[r] >= (1ull << 31)) return set_err(ctx, WC_E_BAD_INPUT, "read longer than 2^31 bytes");
+      roff[k] = pos;
+      src[k] = p.reads[r];
+      b->rlen_h[k] = (uint32_t)p.lens[r];
       pos += (p.lens[r] + 15) & ~15ull;
       q.max_len = std::max<uint32_t>(q.max_len, (uint32_t)p.lens[r]);
       q.work += p.lens[r];
     }
   }
-  b->bytes = h.size();
-  if (!b->reads.ensure(h.size()) || !b->roff.ensure(std::max<size_t>(roff.size(), 1) * 8) ||
+  // reads start 16-byte aligned; 64 bytes of tail padding let the engine load
+  // 64-byte windows with 16-byte accesses anywhere inside a read
+  const uint64_t total = pos + 64;
+  b->bytes = total;
+  std::vector<uint8_t> fallback;
+  uint8_t* h = nullptr;
+  if (ctx->upstage.ensure(total)) {
+    h = (uint8_t*)ctx->upstage.p;
+  } else {
+    fallback.resize(total);
+    h = fallback.data();
+  }
+  auto fill = [&](uint64_t r0, uint64_t r1) {
+    for (uint64_t r = r0; r < r1; ++r) {
+      const uint64_t len = b->rlen_h[r], pad = ((len + 15) & ~15ull) - len;
+      if (len) memcpy(h + roff[r], src[r], len);
+      if (pad) memset(h + roff[r] + len, 0, pad);
+    }
+  };
+  // split the reads into contiguous ranges of about equal bytes
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(hw, total >> 23));  // >= 8 MiB per thread
+  if (nt <= 1 || nr < 2) {
+    fill(0, nr);
+  } else {
+    std::vector<std::thread> th;
+    uint64_t r0 = 0;
+    for (unsigned t = 0; t < nt; ++t) {
+      const uint64_t want = pos * (t + 1) / nt;
+      uint64_t r1 = r0;
+      while (r1 < nr && (t + 1 == nt || roff[r1] < want)) ++r1;
+      th.emplace_back(fill, r0, r1);
+      r0 = r1;
+    }
+    for (auto& x : th) x.join();
+  }
+  memset(h + pos, 0, 64);
+  if (!b->reads.ensure(total) || !b->roff.ensure(std::max<size_t>(roff.size(), 1) * 8) ||
       !b->rlen.ensure(std::max<size_t>(b->rlen_h.size(), 1) * 4))
     return set_err(ctx, WC_E_HIP, "device allocation failed (reads)");
-  HIPCHK(hipMemcpyAsync(b->reads.p, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(b->reads.p, h, total, hipMemcpyHostToDevice, ctx->stream));
   if (!roff.empty()) HIPCHK(hipMemcpyAsync(b->roff.p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
   if (!b->rlen_h.empty())
     HIPCHK(hipMemcpyAsync(b->rlen.p, b->rlen_h.data(), b->rlen_h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
@@ -376,7 +424,11 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
       chain = k;
     }
   }
-  const uint32_t rmax = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cfg.max_return_size, 1), 256);
+  // result records per problem: up to 256 at first; a problem with more tied
+  // results than records reruns with more (ST_RETRY_RMAX), up to max_return_size
+  uint32_t rmax = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cfg.max_return_size, 1), 256);
+  if (const char* r0 = getenv("WC_RMAX"))  // test hook: a smaller first record count exercises the retry
+    rmax = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(rmax, (uint64_t)atoi(r0)));
 
   for (int attempt = 0; attempt < 8 && !ids.empty(); ++attempt) {
     std::stable_sort(ids.begin(), ids.end(),
@@ -581,6 +633,18 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
       pcap = pcap * (big ? 4 : 2);
     }
     if (rflags & ST_RETRY_LCAP) lcap = lcap * 2;
+    if (rflags & ST_RETRY_RMAX) {
+      const uint64_t want = std::min<uint64_t>(cfg.max_return_size, (uint64_t)rmax * 8);
+      const uint64_t bytes = out_bytes(sides, (uint32_t)std::min<uint64_t>(want, UINT32_MAX), nmax, lcap) * ids.size();
+      if (want > UINT32_MAX || bytes > pool_hbm(ctx)) {
+        for (uint32_t id : ids) {
+          R.status[id] = WC_E_LIMIT;
+          R.error[id] = "more tied results than the device result buffer holds (max_return_size)";
+        }
+        return WC_OK;
+      }
+      rmax = (uint32_t)want;
+    }
   }
   for (uint32_t id : ids) {
     R.status[id] = WC_E_LIMIT;
@@ -718,12 +782,16 @@ size_t fx_buckets_h(size_t cap) {
   while (p < adj) p <<= 1;
   return p;
 }
-// FxHashSet<Option<usize>> iteration order of the seed groups (priority_consensus.rs:180)
+// FxHashSet<Option<usize>> iteration order of the seed groups (priority_consensus.rs:180).
+// The set is built by `.collect()`: hashbrown's extend first reserves the
+// iterator's exact size hint (one entry per chain), so the table starts with
+// capacity_to_buckets(n_chains) buckets and never grows while the (at most
+// n_chains) distinct keys are inserted.
 std::vector<int64_t> seed_order(const std::vector<int64_t>& groups) {
   std::vector<int64_t> keys;
   std::vector<uint64_t> hashes;
-  std::vector<int64_t> tab;
-  size_t items = 0, growth = 0;
+  std::vector<int64_t> tab(fx_buckets_h(std::max<size_t>(groups.size(), 1)), -1);
+  size_t items = 0, growth = fx_cap_h(tab.size());
   auto slot = [&](uint64_t h) -> size_t {
     size_t B = tab.size(), mask = B - 1, pos = (size_t)h & mask;
     if (B < 16) {
@@ -821,6 +889,7 @@ void wc_ctx_destroy(wc_ctx* ctx) {
   for (DevBuf* b : {&ctx->ract, &ctx->probs, &ctx->ws, &ctx->out, &ctx->status, &ctx->stats, &ctx->counter, &ctx->jobs, &ctx->act})
     b->release();
   ctx->stage.release();
+  ctx->upstage.release();
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -837,6 +906,12 @@ int wc_batch_create(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batc
   if (rc != WC_OK) return rc;
   *out = b.release();
   return WC_OK;
+}
+
+int wc_batch_refill(wc_ctx* ctx, wc_batch* b, uint32_t n, const wc_problem* problems) {
+  if (!b) return set_err(ctx, WC_E_BAD_INPUT, "null batch");
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
+  return upload_batch(ctx, n, problems, b);
 }
 
 void wc_batch_free(wc_batch* b) { delete b; }

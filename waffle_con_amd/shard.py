@@ -21,6 +21,47 @@ def shard_items(items, rank, world):
     return items[lo:hi]
 
 
+def locus_cost(reads):
+    """Estimated search cost of one locus (~ N reads x L length):
+    the sum over its reads of the read length (chains: every level)."""
+    tot = 0
+    for r in reads:
+        tot += sum(len(x) for x in r) if isinstance(r, (list, tuple)) else len(r)
+    return tot * len(reads)
+
+
+def cost_sorted_assignment(costs, world):
+    """Strong scaling of a fixed item list over `world` ranks without any
+    communication: items are taken longest-first (the cost-sorted queue of
+    SURVEY §8(e)) and each goes to the rank with the least cost so far (LPT;
+    ties to the lowest rank). Every rank computes the same assignment.
+    Returns one list of item indices per rank, each in queue order."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    load = [0] * world
+    out = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        out[r].append(i)
+        load[r] += costs[i]
+    return out
+
+
+class SharedQueue:
+    """Dynamic form of the cost-sorted queue: ranks pull chunks of a fixed,
+    cost-sorted item order through an atomic counter in the process group's
+    store (TCPStore add = fetch-and-add). No collective touches the data path."""
+
+    def __init__(self, store, n_items, chunk, key="wc_queue"):
+        self.store, self.n, self.chunk, self.key = store, n_items, max(1, chunk), key
+
+    def next_chunk(self):
+        end = self.store.add(self.key, self.chunk)
+        start = end - self.chunk
+        if start >= self.n:
+            return None
+        return start, min(end, self.n)
+
+
 def barrier(dist, sync=None):
     if sync is not None:
         sync()
