@@ -92,3 +92,34 @@ def test_cfg4_full_locus_vs_oracle_fixture():
     assert [[(_digest(c["sequence"]), c["scores"]) for c in ch] for ch in got["consensuses"]] == \
         [[(c["sha256"], c["scores"]) for c in ch] for ch in gold["consensuses"]]
     _counters_equal(gc, gold["counters"])
+
+
+def test_thousand_reads_single_vs_oracle():
+    """1,000 reads in one locus (the reference accepts any number, consensus.rs:110-134):
+    per-read state beyond the LDS of a 4-workgroup/CU launch; the deep problem
+    runs in a launch of its own with up to 160 KiB of LDS."""
+    import waffle_con_amd as w
+    seqs = w.generate_test(4, 200, 1000, 0.01, 5)[1]
+    exp, ec = orc.consensus(seqs, counters=True, min_count=250)
+    got, gc = hip.consensus(seqs, counters=True, min_count=250)
+    assert got == exp
+    _counters_equal(gc, ec)
+    # and mixed into a batch of ordinary loci
+    small = [w.generate_test(4, 300, 20, 0.02, s)[1] for s in range(6)]
+    res = hip.consensus_batch(small + [seqs], min_count=5)
+    assert res[-1] == orc.consensus(seqs, min_count=5)
+    for p, r in zip(small, res):
+        assert r == orc.consensus(p, min_count=5)
+
+
+def test_thousand_reads_dual_vs_oracle():
+    import numpy as np
+    from waffle_con_amd import synth
+    rng = np.random.default_rng(9)
+    a = synth.random_seq(rng, 150).tobytes()
+    b = synth._variant(rng, a, 3, 1)
+    reads = [synth.mutate(rng, a, 0.01) for _ in range(500)] + [synth.mutate(rng, b, 0.01) for _ in range(500)]
+    exp, ec = orc.dual_consensus(reads, counters=True)
+    got, gc = hip.dual_consensus(reads, counters=True)
+    assert got == exp
+    _counters_equal(gc, ec)

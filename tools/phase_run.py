@@ -20,6 +20,8 @@ sys.path.insert(0, ROOT)
 PHASES = {0: "pop-broadcast", 1: "analyze", 2: "finalize", 3: "votes+select", 4: "clone-copy", 5: "push-thread",
           6: "push-heavy", 7: "heap-insert", 8: "chain-prepare", 9: "chain-walk", 10: "chain-votes",
           11: "chain-accept", 12: "votes-wave", 13: "pop-logic", 14: "chain-total"}
+# the dual engine marks the same ids: 10 = activation, 11 = prune + cost
+DUAL_PHASES = dict(PHASES, **{10: "activate", 11: "prune+cost"})
 
 
 def main():
@@ -29,6 +31,9 @@ def main():
     ap.add_argument("--reads", type=int, default=100)
     ap.add_argument("--err", type=float, default=0.005)
     ap.add_argument("--out", default="gpurun_out/phases")
+    ap.add_argument("--workload", default="cfg2", choices=("cfg2", "cfg3", "cfg5-hpc"),
+                    help="cfg2 single engine; cfg3 dual loci; cfg5-hpc: the first (HPC-level) dual "
+                         "sub-problem of cfg5 loci")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     ph_file = os.path.join(a.out, "phases.txt")
@@ -36,13 +41,25 @@ def main():
         os.remove(ph_file)
     import waffle_con_amd as w
     from waffle_con_amd.cdwfa_config import CdwfaConfig
-    cfg = CdwfaConfig(min_count=a.reads // 4)
-    loci = [w.generate_test(4, a.len, a.reads, a.err, s)[1] for s in range(a.loci)]
+    from waffle_con_amd import synth
+    if a.workload == "cfg2":
+        cfg = CdwfaConfig(min_count=a.reads // 4)
+        loci = [w.generate_test(4, a.len, a.reads, a.err, s)[1] for s in range(a.loci)]
+    elif a.workload == "cfg3":
+        cfg = CdwfaConfig()
+        loci = [synth.cfg3_locus(s) for s in range(a.loci)]
+    else:
+        cfg = CdwfaConfig(wildcard=ord("*"))
+        loci = [[ch[0] for ch in synth.cfg5_locus(s)] for s in range(a.loci)]
     batch = w.ResidentBatch(loci)
-    batch.consensus(cfg)  # warm-up (no phase file yet)
+    run = batch.consensus if a.workload == "cfg2" else batch.dual_consensus
+    run(cfg)  # warm-up (no phase file yet)
     os.environ["WC_PHASES"] = ph_file
     t0 = time.perf_counter()
-    res, st = batch.consensus(cfg, per_problem=True)
+    if a.workload == "cfg2":
+        res, st = batch.consensus(cfg, per_problem=True)
+    else:
+        res, st = batch.dual_consensus(cfg)
     wall = time.perf_counter() - t0
     del os.environ["WC_PHASES"]
     rep = {"loci": a.loci, "kernel_ms": st["kernel_ms"], "wall_s": wall, "updates": st["updates"],
@@ -50,8 +67,16 @@ def main():
     with open(ph_file) as f:
         line = f.read().strip().splitlines()[-1].split()
     cyc = [int(x) for x in line[2:]]
-    tot = sum(cyc[k] for k in PHASES if k not in (12, 14)) or 1
-    rep["phase_share"] = {PHASES[k]: round(cyc[k] / tot, 4) for k in PHASES}
+    names = PHASES if a.workload == "cfg2" else DUAL_PHASES
+    tot = sum(cyc[k] for k in names if k not in (12, 14)) or 1
+    rep["phase_share"] = {names[k]: round(cyc[k] / tot, 4) for k in names}
+    rep["workload"] = a.workload
+    if a.workload != "cfg2":
+        rep["cycles_per_pop_per_wg"] = round(tot / max(1, st["pops"]), 1)
+        print(json.dumps(rep, indent=1))
+        with open(os.path.join(a.out, "report.json"), "w") as f:
+            json.dump(rep, f, indent=1)
+        return
     c15 = cyc[15]
     rep["chains"] = {"count": c15 & 0xFFFFF, "full": (c15 >> 20) & 0xFFFFF, "accepted_steps": c15 >> 40}
     # wave-0 sub-phases (cycles per chain, summed over workgroups / chains)

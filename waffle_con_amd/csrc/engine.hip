@@ -36,6 +36,7 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 struct Ctl {
   uint32_t prob;
+  uint32_t oslot, obuf;  // stream mode: output slot of the claimed problem, slot parity
   uint32_t heap_n, nfree;
   uint32_t status;
   uint32_t action;  // 0 expand, 1 ignore, 2 done
@@ -297,6 +298,7 @@ struct Eng {
   const Gm<uint8_t>* rbytes;
   const Gm<uint64_t>* roff;
   const Gm<uint32_t>* rlenp;
+  const Gm<int64_t>* ract;  // activation length per read (-1 = active at the root)
   uint64_t sbytes;
   uint32_t nmax, wcap, lcap, pcap, sides, n;
   Gm<uint32_t>* trk;  // [lc0 | pc0 | lc1 | pc1], each lcap+2 u32
@@ -339,6 +341,7 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
   E.rbytes = (const Gm<uint8_t>*)A.rbytes;
   E.roff = (const Gm<uint64_t>*)A.roff;
   E.rlenp = (const Gm<uint32_t>*)A.rlen;
+  E.ract = (const Gm<int64_t>*)A.ractivate;
   E.nmax = A.nmax;
   E.wcap = A.wcap;
   E.lcap = A.lcap;
@@ -359,7 +362,106 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
                               (uint64_t)wave_id() * 2 * A.act_m * 64
                         : nullptr;
   E.L = carve(smem, A.sides, A.pcap, A.nmax, A.chain);
+  if (A.stream) {
+    // the claimed problem's read table is copied here (stream_claim)
+    Gm<uint8_t>* t = E.ws + ws_bytes(A.sides, A.pcap, A.nmax, A.wcap, A.lcap);
+    E.roff = (const Gm<uint64_t>*)t;
+    E.ract = (const Gm<int64_t>*)(t + align16((uint64_t)A.nmax * 8));
+    E.rlenp = (const Gm<uint32_t>*)(t + 2 * align16((uint64_t)A.nmax * 8));
+  }
   return E;
+}
+
+// ---- work claiming ----
+// Static mode: the next problem of the launch's list. Stream mode: the next
+// sequence number of the host-fed ring; wait (bounded by idle_ticks) until the
+// host has published it or has said nothing more will come, and until this
+// workgroup's next output slot has been consumed; then copy the problem's
+// descriptor and read table into the workgroup's workspace. Returns the
+// problem (sequence number), or ~0u to exit; `oslot` = output slot index.
+__device__ inline uint32_t claim_problem(const EngineArgs& A, Sh<Ctl>& ctl, Eng& E, uint32_t& oslot) {
+  const int tid = threadIdx.x;
+  if (!A.stream) {
+    if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
+    __syncthreads();
+    const uint32_t prob = uni(ctl.prob);
+    if (prob >= A.n_problems) return ~0u;
+    E.P = A.problems[prob];
+    oslot = prob;
+    return prob;
+  }
+  if (tid == 0) {
+    const uint32_t seq = atomicAdd(A.qhead, 1u);
+    uint32_t got = seq;
+    uint64_t t0 = wall_clock64();
+    // tail and stop in one 8-byte read of host memory; an idle workgroup
+    // backs off exponentially (up to ~1 ms between reads) so waiting
+    // workgroups put almost no load on the host link
+    uint32_t nap = 1, hb_seen = ~0u;
+    for (;;) {
+      const uint64_t ts = __hip_atomic_load(reinterpret_cast<uint64_t*>(A.sctl), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (seq < (uint32_t)ts) break;
+      if (ts >> 32) {  // stop: nothing more will be published
+        got = ~0u;
+        break;
+      }
+      // give up only when the host itself has stopped (no heartbeat), never
+      // because work is slow to come: a claimed sequence number must be served
+      const uint32_t hb = __hip_atomic_load(&A.sctl->heartbeat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (hb != hb_seen) {
+        hb_seen = hb;
+        t0 = wall_clock64();
+      } else if (wall_clock64() - t0 > A.idle_ticks) {
+        __hip_atomic_store(&A.sctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        got = ~0u;
+        break;
+      }
+      for (uint32_t k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(127);
+      nap = min(nap * 2, 256u);
+    }
+    if (got != ~0u) {
+      // two output slots per workgroup, used alternately; the host clears a
+      // slot's flag when it has consumed the result
+      ctl.obuf ^= 1u;
+      const uint32_t os = blockIdx.x * 2 + ctl.obuf;
+      t0 = wall_clock64();
+      nap = 1;
+      while (__hip_atomic_load(&A.done[os], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+        const uint32_t hb = __hip_atomic_load(&A.sctl->heartbeat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (hb != hb_seen) {
+          hb_seen = hb;
+          t0 = wall_clock64();
+        } else if (wall_clock64() - t0 > A.idle_ticks) {
+          __hip_atomic_store(&A.sctl->abort, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          got = ~0u;
+          break;
+        }
+        for (uint32_t k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(127);
+        nap = min(nap * 2, 64u);
+      }
+      ctl.oslot = os;
+    }
+    ctl.prob = got;
+  }
+  __syncthreads();
+  const uint32_t seq = uni(ctl.prob);
+  if (seq == ~0u) return ~0u;
+  oslot = uni(ctl.oslot);
+  DevProblem P = A.problems[seq % A.qcap];
+  const uint32_t base = P.read_begin;
+  Gm<uint64_t>* lroff = (Gm<uint64_t>*)E.roff;
+  Gm<int64_t>* lract = (Gm<int64_t>*)E.ract;
+  Gm<uint32_t>* lrlen = (Gm<uint32_t>*)E.rlenp;
+  for (uint32_t r = tid; r < P.n_reads; r += kBlock) {
+    const uint32_t q = (base + r) % A.qslots;
+    lroff[r] = A.roff[q];
+    lract[r] = A.ractivate[q];
+    lrlen[r] = A.rlen[q];
+  }
+  P.read_begin = 0;
+  E.P = P;
+  __syncthreads();
+  return seq;
 }
 
 // ---- per-problem init: free stack, trackers, root node (consensus.rs:384-403) ----
@@ -394,7 +496,7 @@ __device__ inline void init_problem(Eng& E, Sh<Ctl>& ctl) {
   for (uint32_t r = tid; r < E.n; r += kBlock) {
     // e = 0 (or None), off = 0, maxb = 0, nscmp = 0, nf = 1: the single
     // diagonal d=0 sits at the (empty) consensus end
-    const uint32_t e = E.A->ractivate[E.P.read_begin + r] < 0 ? 0u : kInactive;
+    const uint32_t e = E.ract[E.P.read_begin + r] < 0 ? 0u : kInactive;
     const uint4 z = make_uint4(0, 0, 0, 0);
     rstate_store(&v.rs[r], RRaw{make_uint4(e, 0, 0, 1u << 16), z, z, z});
     v.wf[(uint64_t)r * E.wcap] = 0;
@@ -653,7 +755,7 @@ __device__ inline void activate_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32
   if (tid == 0) ctl.nheavy = 0;
   __syncthreads();
   for (uint32_t r = tid; r < E.n; r += kBlock)
-    if (E.A->ractivate[E.P.read_begin + r] == (int64_t)alen) E.L.list[atomicAdd(&ctl.nheavy, 1u)] = r;
+    if (E.ract[E.P.read_begin + r] == (int64_t)alen) E.L.list[atomicAdd(&ctl.nheavy, 1u)] = r;
   __syncthreads();
   const uint32_t nh = uni(ctl.nheavy);
   SideView v = E.sv(slot, side);
@@ -926,7 +1028,7 @@ __device__ inline void store_record(Eng& E, Sh<Ctl>& ctl, Gm<uint8_t>* outp, uin
     Gm<uint32_t>* rfe = (Gm<uint32_t>*)(rec + 16 + E.sides * align16(E.lcap) + s * align16((uint64_t)E.nmax * 4));
     if (s < nsides) {
       SideView v = E.sv(slot, s);
-      for (uint32_t i = tid; i < lens[s]; i += kBlock) rcon[i] = v.con[i];
+      copy_bytes(rcon, v.con, lens[s]);  // both 16-byte aligned: 16-byte stores
     }
     for (uint32_t r = tid; r < E.n; r += kBlock) rfe[r] = s < nsides ? E.L.fe[s * E.nmax + r] : kInactive;
   }
@@ -951,18 +1053,26 @@ __device__ inline void trace_pop(const EngineArgs& A, uint32_t prob, const HeapE
   A.trace[0] = k + 1;
 }
 
-__device__ inline void finish_problem(const EngineArgs& A, Sh<Ctl>& ctl, uint8_t* outp, uint32_t prob) {
+__device__ inline void finish_problem(const EngineArgs& A, Sh<Ctl>& ctl, uint8_t* outp, uint32_t prob, uint32_t oslot) {
+  // every wave's result-record stores complete (system scope) before the flag
+  __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
     // every tied result must have a record; otherwise rerun with more records
     if (ctl.status == ST_OK && ctl.n_ret > A.rmax) ctl.status = ST_RETRY | ST_RETRY_RMAX;
     ((uint32_t*)outp)[0] = min(ctl.n_ret, A.rmax);
-    A.status[prob] = ctl.status;
-    for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)prob * S_NSTAT + s] = ctl.cnt[s];
+    A.status[oslot] = ctl.status;
+    for (int s = 0; s < S_NSTAT; ++s) A.stats[(uint64_t)oslot * S_NSTAT + s] = ctl.cnt[s];
 #ifdef WC_PHASE_PROF
     if (A.phases)
       for (int k = 0; k < kPhases; ++k) atomicAdd(&A.phases[k], (unsigned long long)ctl.ph[k]);
 #endif
+    if (A.done) {
+      // the host consumes this problem as soon as it sees the flag (while the
+      // launch goes on): status, counters and records first, then the flag
+      __threadfence_system();
+      __hip_atomic_store(&A.done[oslot], A.stream ? prob + 1 : 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   __syncthreads();
 }
@@ -980,14 +1090,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
   const bool early = cfg.early != 0;
   Eng E = make_eng(A, (Sh<uint8_t>*)smem);
 
+  if (tid == 0) ctl.obuf = 1;
   for (;;) {
-    if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
-    __syncthreads();
-    const uint32_t prob = uni(ctl.prob);
-    if (prob >= A.n_problems) break;
-    E.P = A.problems[prob];
+    uint32_t oslot = 0;
+    const uint32_t prob = claim_problem(A, ctl, E, oslot);
+    if (prob == ~0u) break;
     E.n = E.P.n_reads;
-    Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)prob * A.out_stride;
+    Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)oslot * A.out_stride;
     init_problem(E, ctl);
 
     for (;;) {
@@ -1217,7 +1326,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       __syncthreads();
       PH_MARK(7);
     }
-    finish_problem(A, ctl, outp, prob);
+    finish_problem(A, ctl, outp, prob, oslot);
   }
 }
 
@@ -1237,14 +1346,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
   Sh<RInfo>* R0 = E.L.rinfo;
   Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
 
+  if (tid == 0) ctl.obuf = 1;
   for (;;) {
-    if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
-    __syncthreads();
-    const uint32_t prob = uni(ctl.prob);
-    if (prob >= A.n_problems) break;
-    E.P = A.problems[prob];
+    uint32_t oslot = 0;
+    const uint32_t prob = claim_problem(A, ctl, E, oslot);
+    if (prob == ~0u) break;
     E.n = E.P.n_reads;
-    Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)prob * A.out_stride;
+    Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)oslot * A.out_stride;
     init_problem(E, ctl);
     const uint64_t full_min = max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.n));
 
@@ -1386,7 +1494,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (tid == 0) ctl.act_cnt = 0;
         __syncthreads();
         for (uint32_t r = tid; r < E.n; r += kBlock)
-          if (E.A->ractivate[E.P.read_begin + r] == (int64_t)tlen) atomicAdd(&ctl.act_cnt, 1u);
+          if (E.ract[E.P.read_begin + r] == (int64_t)tlen) atomicAdd(&ctl.act_cnt, 1u);
         __syncthreads();
         nadd = uni(ctl.act_cnt);
       }
@@ -1614,7 +1722,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       __syncthreads();
       PH_MARK(7);
     }
-    finish_problem(A, ctl, outp, prob);
+    finish_problem(A, ctl, outp, prob, oslot);
   }
 }
 

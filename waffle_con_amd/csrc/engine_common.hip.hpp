@@ -164,6 +164,56 @@ struct WaveCounters {
   uint32_t updates, w_out, compares, edinc, finalizes;
 };
 
+// ---- packed match runs (dynamic_wfa.rs:122-150) ----
+// 8 bytes at p[pos..pos+8): two aligned 8-byte loads and a funnel shift.
+// Reads start 16-byte aligned with 64 bytes of arena tail padding and the
+// consensus rows are followed by more workspace, so the second word is always
+// inside the allocation; bytes past a sequence's end are masked by the caller.
+__device__ __forceinline__ uint64_t load8(const Gm<uint8_t>* p, uint32_t pos) {
+  const Gm<uint64_t>* w = (const Gm<uint64_t>*)p + (pos >> 3);
+  const uint32_t sh = (pos & 7u) * 8u;
+  const uint64_t a = w[0], b = w[1];
+  return sh ? (a >> sh) | (b << (64u - sh)) : a;
+}
+// 0x80 in every byte of v that is non-zero
+__device__ __forceinline__ uint64_t nz_bytes(uint64_t v) {
+  constexpr uint64_t lo7 = 0x7f7f7f7f7f7f7f7full;
+  return (((v & lo7) + lo7) | v) & ~lo7;
+}
+// The extend loop of one diagonal from read position bo / consensus position
+// oo, eight bytes per step: XOR of the packed bytes, the wildcard masked on the
+// read side only (:138-140), ctz for the first mismatch. Returns how far d
+// advances; `cmp` gets the compares the byte-at-a-time reference loop makes
+// (one per matched byte, plus the failing one when the run stops on a
+// mismatch rather than at a sequence end).
+__device__ __forceinline__ uint32_t match_run(const Gm<uint8_t>* rd, uint32_t blen, const Gm<uint8_t>* con,
+                                              uint32_t olen, uint32_t bo, uint32_t oo, int wc, uint32_t& cmp) {
+  const uint64_t wcb = 0x0101010101010101ull * (uint64_t)(uint8_t)wc;
+  uint32_t adv = 0;
+  while (bo < blen && oo < olen) {
+    const uint32_t rem = min(blen - bo, olen - oo);
+    const uint64_t x = load8(rd, bo), y = load8(con, oo);
+    uint64_t mm = nz_bytes(x ^ y);
+    if (wc >= 0) mm &= nz_bytes(x ^ wcb);
+    const uint32_t k = mm ? (uint32_t)__builtin_ctzll(mm) >> 3 : 8u;
+    if (k >= rem) {  // everything up to the nearer sequence end matches
+      adv += rem;
+      cmp += rem;
+      break;
+    }
+    if (k < 8) {  // mismatch at byte k
+      adv += k;
+      cmp += k + 1;
+      break;
+    }
+    adv += 8;
+    cmp += 8;
+    bo += 8;
+    oo += 8;
+  }
+  return adv;
+}
+
 // Full extend of every diagonal of `wf[0..W)` (dynamic_wfa.rs:109-153),
 // lanes over diagonals. Returns (via refs) wave-reduced max_other - off and
 // max_baseline. Counts byte compares as the reference loop would.
@@ -175,17 +225,8 @@ __device__ inline void wave_extend_all(Gm<uint32_t>* wf, uint32_t W, uint32_t e,
   for (uint32_t base = 0; base < W; base += 64) {
     uint32_t i = base + lane;
     if (i < W) {
-      uint32_t d = wf[i];
-      uint32_t d0 = d;
-      for (;;) {
-        uint32_t bo = d + e - i;
-        uint32_t oo = d + off;
-        if (bo >= blen || oo >= olen) break;
-        c++;
-        uint8_t x = rd[bo];
-        if (x != con[oo] && !(wc >= 0 && x == (uint8_t)wc)) break;
-        d++;
-      }
+      const uint32_t d0 = wf[i];
+      const uint32_t d = d0 + match_run(rd, blen, con, olen, d0 + e - i, d0 + off, wc, c);
       if (d != d0) wf[i] = d;
       mo = max(mo, d);
       mb = max(mb, d + e - i);
@@ -194,6 +235,78 @@ __device__ inline void wave_extend_all(Gm<uint32_t>* wf, uint32_t W, uint32_t e,
   maxo = wave_max_u32(mo);
   maxb = wave_max_u32(mb);
   cmp += c;
+}
+
+// ---- register-resident wavefronts ----
+// The ED-increase loop (dynamic_wfa.rs:84-91 / :162-191) holds the row in
+// registers, lane-strided (entry lane + 64 q in v[q]), for W <= 64 * kRegQ:
+// one load and one store of the row per update instead of a round trip
+// through memory per increase.
+constexpr int kRegQ = 2;
+
+// increase_edit_distance on the register row: W -> W + 2,
+// new[j] = max(old[j] (j < W), old[j-1] + 1 (1 <= j <= W), old[j-2] + 1 (2 <= j <= W+1)).
+__device__ __forceinline__ void regs_grow(uint32_t (&v)[kRegQ], uint32_t W) {
+  const int lane = lane_id();
+  uint32_t nv[kRegQ];
+#pragma unroll
+  for (int q = 0; q < kRegQ; ++q) {
+    const uint32_t j = (uint32_t)lane + 64u * q;
+    uint32_t m1 = (uint32_t)__shfl_up((int)v[q], 1, 64);
+    uint32_t m2 = (uint32_t)__shfl_up((int)v[q], 2, 64);
+    if (q > 0) {
+      const uint32_t p63 = (uint32_t)__builtin_amdgcn_readlane((int)v[q - 1], 63);
+      const uint32_t p62 = (uint32_t)__builtin_amdgcn_readlane((int)v[q - 1], 62);
+      if (lane == 0) {
+        m1 = p63;
+        m2 = p62;
+      } else if (lane == 1) {
+        m2 = p63;
+      }
+    }
+    uint32_t x = 0;
+    if (j < W) x = v[q];
+    if (j >= 1 && j <= W) x = max(x, m1 + 1);
+    if (j >= 2 && j <= W + 1) x = max(x, m2 + 1);
+    nv[q] = x;
+  }
+#pragma unroll
+  for (int q = 0; q < kRegQ; ++q) v[q] = nv[q];
+}
+
+// extend every diagonal of the register row (wave_extend_all semantics)
+__device__ __forceinline__ void regs_extend(uint32_t (&v)[kRegQ], uint32_t W, uint32_t e, uint32_t off,
+                                            const Gm<uint8_t>* rd, uint32_t blen, const Gm<uint8_t>* con,
+                                            uint32_t olen, int wc, uint32_t& maxo, uint32_t& maxb, uint32_t& cmp) {
+  const int lane = lane_id();
+  uint32_t mo = 0, mb = 0;
+#pragma unroll
+  for (int q = 0; q < kRegQ; ++q) {
+    const uint32_t i = (uint32_t)lane + 64u * q;
+    if (i < W) {
+      const uint32_t d = v[q] + match_run(rd, blen, con, olen, v[q] + e - i, v[q] + off, wc, cmp);
+      v[q] = d;
+      mo = max(mo, d);
+      mb = max(mb, d + e - i);
+    }
+  }
+  maxo = wave_max_u32(mo);
+  maxb = wave_max_u32(mb);
+}
+
+__device__ __forceinline__ void regs_load(uint32_t (&v)[kRegQ], const Gm<uint32_t>* wf, uint32_t W) {
+#pragma unroll
+  for (int q = 0; q < kRegQ; ++q) {
+    const uint32_t i = (uint32_t)lane_id() + 64u * q;
+    v[q] = i < W ? wf[i] : 0u;
+  }
+}
+__device__ __forceinline__ void regs_store(const uint32_t (&v)[kRegQ], Gm<uint32_t>* wf, uint32_t W) {
+#pragma unroll
+  for (int q = 0; q < kRegQ; ++q) {
+    const uint32_t i = (uint32_t)lane_id() + 64u * q;
+    if (i < W) wf[i] = v[q];
+  }
 }
 
 // increase_edit_distance in place (dynamic_wfa.rs:162-183): W -> W+2.
@@ -290,35 +403,51 @@ __device__ inline bool wave_update_general(Gm<uint32_t>* wf, uint32_t& e, uint32
   return true;
 }
 
-// DWFALite::finalize (dynamic_wfa.rs:201-210) on a scratch copy of the
-// wavefront; the node itself is untouched (the reference finalizes a clone).
+// DWFALite::finalize (dynamic_wfa.rs:201-210) on a copy of the wavefront (in
+// registers while it fits, else the scratch row); the node itself is
+// untouched (the reference finalizes a clone).
 __device__ inline bool wave_finalize_read(const Gm<uint32_t>* wf, uint32_t e, uint32_t off, const Gm<uint8_t>* rd,
                                           uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc,
                                           Gm<uint32_t>* scratch,
                                           uint32_t wcap, uint32_t& e_out, WaveCounters& cnt) {
-  const int lane = lane_id();
   uint32_t W = 2 * e + 1;
+  uint32_t v[kRegQ];
+  regs_load(v, wf, W);
   uint32_t mb = 0;
-  for (uint32_t base = 0; base < W; base += 64) {
-    uint32_t i = base + lane;
-    if (i < W) {
-      uint32_t d = wf[i];
-      scratch[i] = d;
-      mb = max(mb, d + e - i);
-    }
+#pragma unroll
+  for (int q = 0; q < kRegQ; ++q) {
+    const uint32_t i = (uint32_t)lane_id() + 64u * q;
+    if (i < W) mb = max(mb, v[q] + e - i);
   }
+  for (uint32_t i = 64u * kRegQ + lane_id(); i < W; i += 64) mb = max(mb, wf[i] + e - i);
   mb = wave_max_u32(mb);
   uint32_t cmp = 0;
   cnt.finalizes++;
+  bool regs = true;
+  if (W > 64u * kRegQ) {
+    for (uint32_t i = lane_id(); i < W; i += 64) scratch[i] = wf[i];
+    regs = false;
+  }
   while (mb < blen) {
     if (W + 2 > wcap) return false;
-    __builtin_amdgcn_wave_barrier();
-    wave_grow(scratch, W);
-    W += 2;
-    e += 1;
-    cnt.edinc++;
+    if (regs && W + 2 > 64u * kRegQ) {
+      regs_store(v, scratch, W);
+      regs = false;
+    }
     uint32_t mo;
-    wave_extend_all(scratch, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
+    if (regs) {
+      regs_grow(v, W);
+      W += 2;
+      e += 1;
+      regs_extend(v, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
+    } else {
+      __builtin_amdgcn_wave_barrier();
+      wave_grow(scratch, W);
+      W += 2;
+      e += 1;
+      wave_extend_all(scratch, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
+    }
+    cnt.edinc++;
   }
   cnt.compares += wave_sum_u32(cmp);
   e_out = e;
@@ -636,10 +765,48 @@ __device__ inline void wave_rebuild(const Gm<uint32_t>* wf, uint32_t e, uint32_t
   }
 }
 
+// RState from a register row (wave_rebuild semantics)
+template <class P>
+__device__ inline void regs_rebuild(const uint32_t (&v)[kRegQ], uint32_t e, uint32_t off, uint32_t blen, uint32_t len,
+                                    P out) {
+  const int lane = lane_id();
+  const uint32_t W = 2 * e + 1;
+  uint32_t nf = 0, mb = 0, nsc = 0;
+#pragma unroll
+  for (int q = 0; q < kRegQ; ++q) {
+    const uint32_t i = (uint32_t)lane + 64u * q;
+    const bool valid = i < W;
+    const uint32_t d = v[q];
+    const uint32_t bo = d + e - i;
+    const bool inF = valid && d + off >= len;
+    const uint64_t m = ballot(inF);
+    const uint32_t pos = nf + (uint32_t)__popcll((unsigned long long)(m & ((1ull << lane) - 1ull)));
+    if (inF && pos < (uint32_t)kF) {
+      out->fi[pos] = (uint16_t)i;
+      out->fd[pos] = d;
+    }
+    nf += (uint32_t)__popcll((unsigned long long)m);
+    if (valid && !inF) {
+      mb = max(mb, bo);
+      nsc += bo < blen;
+    }
+  }
+  mb = wave_max_u32(mb);
+  nsc = wave_sum_u32(nsc);
+  if (lane == 0) {
+    out->e = e;
+    out->off = off;
+    out->maxb = mb;
+    out->nscmp = (uint16_t)min(nsc, 65535u);
+    out->nf = (uint8_t)min(nf, (uint32_t)kF);
+    out->flags = (nf > (uint32_t)kF || nsc > 65535u) ? kWide : 0;
+  }
+}
+
 // The wave part of a push for one read whose thread step returned true:
 // full-scan push for a wide frontier, otherwise the ED-increase loop from the
-// post-extend wavefront; then rebuild the RState. Returns false on wavefront
-// capacity overflow.
+// post-extend wavefront (in registers while W <= 64 * kRegQ); then rebuild the
+// RState. Returns false on wavefront capacity overflow.
 template <class P>
 __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
                                   const Gm<uint8_t>* con, uint32_t olen, uint8_t sym, int wc, bool early, uint32_t wcap, WaveCounters& cnt,
@@ -649,22 +816,45 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
   const uint32_t off = rsp->off;
   if (flags & kWide) {
     if (!wave_push_read(wf, e, off, rd, blen, con, olen, sym, wc, early, wcap, cnt)) return false;
-  } else {
-    uint32_t W = 2 * e + 1, mo, mb, cmp = 0;
-    do {
-      if (W + 2 > wcap) return false;
+    __builtin_amdgcn_wave_barrier();
+    wave_rebuild(wf, e, off, blen, olen, rsp);
+    e_out = e;
+    return true;
+  }
+  uint32_t W = 2 * e + 1, mo, mb, cmp = 0;
+  uint32_t v[kRegQ];
+  bool regs = W + 2 <= 64u * kRegQ;
+  if (regs) regs_load(v, wf, W);
+  do {
+    if (W + 2 > wcap) return false;
+    if (regs && W + 2 > 64u * kRegQ) {
+      regs_store(v, wf, W);
+      regs = false;
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (regs) {
+      regs_grow(v, W);
+      W += 2;
+      e += 1;
+      regs_extend(v, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
+    } else {
       wave_grow(wf, W);
       W += 2;
       e += 1;
-      cnt.edinc++;
       wave_extend_all(wf, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
-    } while (mo + off < olen && !(early && mb == blen));
-    cnt.updates++;
-    cnt.w_out += W;
-    cnt.compares += wave_sum_u32(cmp);
+    }
+    cnt.edinc++;
+  } while (mo + off < olen && !(early && mb == blen));
+  cnt.updates++;
+  cnt.w_out += W;
+  cnt.compares += wave_sum_u32(cmp);
+  if (regs) {
+    regs_store(v, wf, W);
+    regs_rebuild(v, e, off, blen, olen, rsp);
+  } else {
+    __builtin_amdgcn_wave_barrier();
+    wave_rebuild(wf, e, off, blen, olen, rsp);
   }
-  __builtin_amdgcn_wave_barrier();
-  wave_rebuild(wf, e, off, blen, olen, rsp);
   e_out = e;
   return true;
 }

@@ -1,0 +1,1060 @@
+// Host side of the device engines: capacity planning, engine launches (each
+// with its own stream, buffers and host-mapped result area), the synchronous
+// batch runner, and the streamed PriorityConsensusDWFA scheduler.
+//
+// Results, status and work counters of every problem are written by the
+// engine straight into fine-grained host memory, followed by a system-scope
+// completion flag (engine.hip finish_problem). The host can therefore consume
+// a problem the moment it finishes, while the rest of its launch still runs.
+// The priority scheduler uses that to keep the GPU busy: the children of a
+// finished DualConsensusDWFA sub-problem go into the next launch right away
+// (up to kSlots launches in flight), instead of waiting for the slowest
+// sub-problem of a round. The LIFO stack discipline of the reference
+// (priority_consensus.rs:195-307) is preserved by unwinding each problem's
+// stack only through finished tops.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <atomic>
+#include <deque>
+#include <memory>
+#include <numeric>
+#include <thread>
+
+#include "host_internal.hpp"
+
+using namespace wc;
+
+namespace wch {
+
+namespace {
+constexpr uint32_t kLdsMax = 160 * 1024;  // one workgroup may take the whole CU's LDS
+
+// HBM the node pools of one launch may take: `share` of what is free plus the
+// launch's own cached workspace (reused by the launch)
+uint64_t hbm_share(uint64_t cached, double share) {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 32ull << 30;
+  return (uint64_t)(((double)fr + (double)cached) * share);
+}
+}  // namespace
+
+struct Caps {
+  uint32_t sides = 1, pcap = 16, wcap = 64, lcap = 64, nmax = 1, chain = 0, rmax = 1, act_m = 0;
+  size_t lds = 0;
+  int per_cu = 1;
+  uint64_t wsb = 0, ob = 0;
+};
+
+// Capacities of one launch over items[ids] (SURVEY §8(a) sizes): wavefront row
+// capacity from the longest read, consensus capacity from the longest read,
+// node-pool slots from the HBM share, linear-chain length from the LDS left at
+// the same occupancy. Retry outcomes raise them per item (log2 multipliers).
+static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vector<SubProb>& items,
+                     const std::vector<uint32_t>& ids, uint64_t hbm_budget, Caps& c, std::string& err) {
+  uint32_t nmax = 1, maxlen = 1, wx = 0, px = 0, lx = 0, rx = 0;
+  bool any_act = false;
+  for (uint32_t id : ids) {
+    const SubProb& s = items[id];
+    nmax = std::max<uint32_t>(nmax, (uint32_t)s.gid.size());
+    maxlen = std::max(maxlen, s.max_len);
+    wx = std::max<uint32_t>(wx, s.wcap_x);
+    px = std::max<uint32_t>(px, s.pcap_x);
+    lx = std::max<uint32_t>(lx, s.lcap_x);
+    rx = std::max<uint32_t>(rx, s.rmax_x);
+    any_act |= s.max_act > 0;
+  }
+  c.sides = sides;
+  c.nmax = nmax;
+  const uint32_t ecap = std::max<uint32_t>(31, maxlen / 64);
+  c.wcap = (((2 * ecap + 1 + 63) / 64) * 64) << wx;
+  c.lcap = (((maxlen + maxlen / 8 + 64 + 15) / 16) * 16) << lx;
+  // single engine: linear-chain run-ahead length (WC_CHAIN=<k> overrides, 0 = off)
+  uint32_t chain = (sides == 1 && nmax <= (uint32_t)kBlock) ? kChainDefault : 0;
+  const char* chain_env = getenv("WC_CHAIN");
+  if (chain_env) chain = std::min<uint32_t>((uint32_t)atoi(chain_env), kChainMax);
+  if (sides != 1 || nmax > (uint32_t)kBlock) chain = 0;
+  // node pool. A dual search keeps far more nodes queued than a single one
+  // (children of both consensuses, both sides' DWFAs per node: cfg3 loci peak
+  // at ~480 queued nodes), so the dual pool gets the launch's HBM share over
+  // the workgroups that can run at once (16..256 MiB each).
+  const uint64_t sb = slot_bytes(sides, nmax, c.wcap, c.lcap);
+  const uint64_t conc = std::max<uint64_t>(1, std::min<uint64_t>(ids.size(), 4ull * (uint64_t)ctx->n_cu));
+  const uint64_t per_wg = std::max<uint64_t>(16ull << 20, hbm_budget / conc);
+  const uint64_t budget = sides == 1 ? (16ull << 20) : std::min<uint64_t>(256ull << 20, per_wg);
+  const uint32_t pmax = sides == 1 ? 256u : 1024u;
+  const uint64_t lmax = sides == 1 ? 40 * 1024 : 48 * 1024;
+  uint32_t pcap = 16;
+  while (pcap < pmax && (uint64_t)(pcap * 2) * sb <= budget && lds_bytes(sides, pcap * 2, nmax, chain) <= lmax)
+    pcap *= 2;
+  // a retried (pool-exhausted) item gets 4x per retry, as HBM and LDS allow
+  for (uint32_t k = 0; k < px; ++k) {
+    const uint32_t np = pcap * 2;
+    if ((uint64_t)np * sb > std::max<uint64_t>(budget, per_wg) || lds_bytes(sides, np, nmax, chain) > kLdsMax) break;
+    pcap = np;
+  }
+  // longer chains amortise the per-chain work (prediction, acceptance, the
+  // literal pop between chains); take the longest one whose LDS still gives
+  // the workgroups per CU of the default length (results do not depend on it)
+  if (!chain_env && chain > 0) {
+    const int occ = engine_blocks_per_cu(sides, (size_t)lds_bytes(sides, pcap, nmax, chain));
+    for (uint32_t k = chain + 1; k <= kChainMax; ++k) {
+      const uint64_t l = lds_bytes(sides, pcap, nmax, k);
+      if (l > 60 * 1024 || engine_blocks_per_cu(sides, (size_t)l) < occ) break;
+      chain = k;
+    }
+  }
+  c.pcap = pcap;
+  c.chain = chain;
+  // result records per problem: up to 256 at first; a problem with more tied
+  // results than records reruns with more (ST_RETRY_RMAX), up to max_return_size
+  uint64_t rmax = std::min<uint64_t>(std::max<uint64_t>(cfg.max_return_size, 1), 256);
+  if (const char* r0 = getenv("WC_RMAX"))  // test hook: a smaller first record count exercises the retry
+    rmax = std::max<uint64_t>(1, std::min<uint64_t>(rmax, (uint64_t)atoi(r0)));
+  for (uint32_t k = 0; k < rx; ++k) rmax = std::min<uint64_t>(std::max<uint64_t>(cfg.max_return_size, 1), rmax * 8);
+  if (rmax > (1u << 20)) {
+    err = "more tied results than the device result buffer holds (max_return_size)";
+    return WC_E_LIMIT;
+  }
+  c.rmax = (uint32_t)rmax;
+  // offset activation scratch (wfa_ed_config pair arrays): edits <= |v1| + |v2|
+  // with |v1| <= window + ocl and |v2| <= ocl (engine_common wave_pick_offset)
+  c.act_m = 0;
+  if (any_act) {
+    const uint64_t ocl = std::min<uint64_t>(cfg.offset_compare_length, maxlen);
+    const uint64_t m = 3 + 2 * (cfg.offset_window + 2 * ocl) + 8;
+    if (m > 8192) {
+      err = "offset_window/offset_compare_length too large for the device activation scratch";
+      return WC_E_LIMIT;
+    }
+    c.act_m = (uint32_t)m;
+  }
+  c.lds = (size_t)lds_bytes(sides, pcap, nmax, chain);
+  if (c.lds > kLdsMax) {
+    err = "problem needs more LDS than one workgroup has (reads x node pool)";
+    return WC_E_LIMIT;
+  }
+  c.per_cu = engine_blocks_per_cu(sides, c.lds);
+  c.wsb = ws_bytes(sides, pcap, nmax, c.wcap, c.lcap);
+  c.ob = out_bytes(sides, c.rmax, nmax, c.lcap);
+  return WC_OK;
+}
+
+// One engine launch and everything it owns.
+struct Launch {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DevBuf probs, sroff, srlen, ract, ws, counter, act, phases;
+  HostBuf host;  // mapped: done[P] | status[P] | stats[P][S_NSTAT] | out[P]
+  HostBuf ring;  // mapped (stream launches): StreamCtl | problem ring | read-table rings
+  Caps caps;
+  uint32_t P = 0, grid = 0;
+  uint64_t off_status = 0, off_stats = 0, off_out = 0;
+  std::vector<uint32_t> ids;  // launch problem k -> caller item id
+  std::vector<uint8_t> taken;
+  uint32_t n_taken = 0;
+  bool busy = false;
+  double kernel_ms = 0;
+  std::vector<DevProblem> dp;
+  std::vector<uint64_t> h_sroff;
+  std::vector<uint32_t> h_srlen;
+  std::vector<int64_t> h_ract;
+
+  volatile uint32_t* done() const { return (volatile uint32_t*)host.p; }
+  const uint32_t* status() const { return (const uint32_t*)((const uint8_t*)host.p + off_status); }
+  const uint64_t* stats() const { return (const uint64_t*)((const uint8_t*)host.p + off_stats); }
+  const uint8_t* out(uint32_t k) const { return (const uint8_t*)host.p + off_out + (uint64_t)k * caps.ob; }
+  ~Launch() {
+    for (DevBuf* b : {&probs, &sroff, &srlen, &ract, &ws, &counter, &act, &phases}) b->release();
+    host.release();
+    ring.release();
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+void destroy_launches(wc_ctx* ctx) {
+  for (Launch* L : ctx->launches) delete L;
+  ctx->launches.clear();
+}
+
+static Launch* launch_slot(wc_ctx* ctx, size_t k) {
+  while (ctx->launches.size() <= k) {
+    Launch* L = new Launch();
+    if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&L->ev0) != hipSuccess || hipEventCreate(&L->ev1) != hipSuccess) {
+      delete L;
+      return nullptr;
+    }
+    ctx->launches.push_back(L);
+  }
+  return ctx->launches[k];
+}
+
+// Starts one engine launch over items[ids] (already in scheduling order).
+static int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg, const std::vector<SubProb>& items,
+                        const std::vector<uint32_t>& ids, const Caps& caps) {
+  L.caps = caps;
+  L.ids = ids;
+  L.P = (uint32_t)ids.size();
+  L.taken.assign(L.P, 0);
+  L.n_taken = 0;
+  L.kernel_ms = 0;
+  const uint32_t P = L.P;
+  uint64_t nslots = 0;
+  for (uint32_t id : ids) nslots += items[id].gid.size();
+  L.dp.assign(P, DevProblem());
+  L.h_sroff.resize(std::max<uint64_t>(nslots, 1));
+  L.h_srlen.resize(std::max<uint64_t>(nslots, 1));
+  L.h_ract.resize(std::max<uint64_t>(nslots, 1));
+  uint64_t slot = 0;
+  for (uint32_t k = 0; k < P; ++k) {
+    const SubProb& s = items[ids[k]];
+    DevProblem& d = L.dp[k];
+    memset(&d, 0, sizeof(d));
+    d.read_begin = (uint32_t)slot;
+    d.n_reads = (uint32_t)s.gid.size();
+    d.max_read_len = s.max_len;
+    d.n_active = s.n_active;
+    d.max_act = s.max_act;
+    for (size_t r = 0; r < s.gid.size(); ++r, ++slot) {
+      L.h_sroff[slot] = b->roff_h[s.gid[r]];
+      L.h_srlen[slot] = b->rlen_h[s.gid[r]];
+      L.h_ract[slot] = s.act[r];
+    }
+  }
+  L.grid = std::min<uint32_t>(P, (uint32_t)std::max(1, caps.per_cu) * (uint32_t)ctx->n_cu);
+  L.off_status = align16((uint64_t)P * 4);
+  L.off_stats = L.off_status + align16((uint64_t)P * 4);
+  L.off_out = L.off_stats + align16((uint64_t)P * S_NSTAT * 8);
+  const uint64_t hbytes = L.off_out + (uint64_t)P * caps.ob;
+  if (!L.host.ensure(hbytes, true)) return set_err(ctx, WC_E_HIP, "pinned host allocation failed (results)");
+  memset(L.host.p, 0, L.off_out);  // done flags, status, counters
+  if (caps.act_m && !L.act.ensure(act_scr_u64(caps.act_m) * 8 * L.grid))
+    return set_err(ctx, WC_E_HIP, "device allocation failed (activation scratch)");
+  if (!L.probs.ensure(P * sizeof(DevProblem)) || !L.sroff.ensure(L.h_sroff.size() * 8) ||
+      !L.srlen.ensure(L.h_srlen.size() * 4) || !L.ract.ensure(L.h_ract.size() * 8) ||
+      !L.ws.ensure(caps.wsb * L.grid) || !L.counter.ensure(4))
+    return set_err(ctx, WC_E_HIP, "device allocation failed (workspace)");
+  HIPCHK(hipMemcpyAsync(L.probs.p, L.dp.data(), P * sizeof(DevProblem), hipMemcpyHostToDevice, L.stream));
+  HIPCHK(hipMemcpyAsync(L.sroff.p, L.h_sroff.data(), L.h_sroff.size() * 8, hipMemcpyHostToDevice, L.stream));
+  HIPCHK(hipMemcpyAsync(L.srlen.p, L.h_srlen.data(), L.h_srlen.size() * 4, hipMemcpyHostToDevice, L.stream));
+  HIPCHK(hipMemcpyAsync(L.ract.p, L.h_ract.data(), L.h_ract.size() * 8, hipMemcpyHostToDevice, L.stream));
+  HIPCHK(hipMemsetAsync(L.counter.p, 0, 4, L.stream));
+
+  void* dhost = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dhost, L.host.p, 0));
+  uint8_t* dh = (uint8_t*)dhost;
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.cfg = to_dev(cfg);
+  a.problems = (const DevProblem*)L.probs.p;
+  a.n_problems = P;
+  a.sides = caps.sides;
+  a.rbytes = (const uint8_t*)b->reads.p;
+  a.roff = (const uint64_t*)L.sroff.p;
+  a.rlen = (const uint32_t*)L.srlen.p;
+  a.ractivate = (const int64_t*)L.ract.p;
+  a.ws = (uint8_t*)L.ws.p;
+  a.ws_stride = caps.wsb;
+  a.pcap = caps.pcap;
+  a.wcap = caps.wcap;
+  a.lcap = caps.lcap;
+  a.nmax = caps.nmax;
+  a.rmax = caps.rmax;
+  a.chain = caps.chain;
+  a.out = dh + L.off_out;
+  a.out_stride = caps.ob;
+  a.status = (uint32_t*)(dh + L.off_status);
+  a.stats = (uint64_t*)(dh + L.off_stats);
+  a.done = (uint32_t*)dh;
+  a.work_counter = (uint32_t*)L.counter.p;
+  a.act_m = caps.act_m;
+  a.act_scr = caps.act_m ? (uint64_t*)L.act.p : nullptr;
+  a.act_stride = caps.act_m ? act_scr_u64(caps.act_m) : 0;
+  // debug phase cycle counters (WC_PHASES=<file>, WC_PHASE_PROF builds only)
+  if (getenv("WC_PHASES") && L.phases.ensure(kPhases * 8)) {
+    a.phases = (unsigned long long*)L.phases.p;
+    HIPCHK(hipMemsetAsync(L.phases.p, 0, kPhases * 8, L.stream));
+  }
+  HIPCHK(hipEventRecord(L.ev0, L.stream));
+  if (caps.sides == 1) launch_single_engine(a, L.grid, caps.lds, L.stream);
+  else launch_dual_engine(a, L.grid, caps.lds, L.stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(L.ev1, L.stream));
+  L.busy = true;
+  if (getenv("WC_LAUNCH_LOG"))
+    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
+            caps.sides, P, L.grid, caps.per_cu, caps.lds, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
+  return WC_OK;
+}
+
+// The outcome of launch problem k (its completion flag is set). Returns the
+// raw device status (ST_RETRY flags included); `o` gets records and counters.
+static uint32_t harvest(const Launch& L, uint32_t k, const SubProb& s, EngineOut& o) {
+  const uint32_t st = L.status()[k];
+  for (int q = 0; q < S_NSTAT; ++q) o.stats[q] = L.stats()[(uint64_t)k * S_NSTAT + q];
+  o.recs.clear();
+  o.status = (int)st;
+  o.error.clear();
+  if (st & ST_RETRY) return st;
+  const uint8_t* base = L.out(k);
+  if (st != ST_OK) {
+    o.error = err_msg((int)st);
+    if (st == WC_E_COVERAGE_GAP)  // consensus.rs:305 / dual_consensus.rs message
+      o.error = "Encountered coverage gap: consensus is length " + std::to_string(((const uint32_t*)base)[1]) +
+                " with no candidates, but sequences activate at " + std::to_string(s.max_act);
+    return st;
+  }
+  const Caps& c = L.caps;
+  const uint64_t rb = result_bytes(c.sides, c.nmax, c.lcap);
+  const uint32_t nres = ((const uint32_t*)base)[0];
+  const uint32_t n = (uint32_t)s.gid.size();
+  for (uint32_t r = 0; r < nres; ++r) {
+    const uint8_t* rec = base + 16 + (uint64_t)r * rb;
+    const uint32_t* h = (const uint32_t*)rec;
+    RawRecord rr;
+    rr.len[0] = h[0];
+    rr.len[1] = h[1];
+    rr.dual = h[2] != 0;
+    for (uint32_t sd = 0; sd < c.sides; ++sd) {
+      const uint8_t* con = rec + 16 + sd * align16(c.lcap);
+      rr.con[sd].assign(con, con + rr.len[sd]);
+      const uint32_t* fe = (const uint32_t*)(rec + 16 + c.sides * align16(c.lcap) + sd * align16((uint64_t)c.nmax * 4));
+      rr.fe[sd].assign(fe, fe + n);
+    }
+    o.recs.push_back(std::move(rr));
+  }
+  return st;
+}
+
+// capacity growth for a retried item
+static void bump(SubProb& s, uint32_t st) {
+  if (st & ST_RETRY_WCAP) s.wcap_x++;
+  if (st & (ST_RETRY_PCAP | ST_RETRY_HEAP)) s.pcap_x += 2;
+  if (st & ST_RETRY_LCAP) s.lcap_x++;
+  if (st & ST_RETRY_RMAX) s.rmax_x++;
+  s.attempts++;
+}
+
+static int launch_finish(wc_ctx* ctx, Launch& L) {
+  HIPCHK(hipStreamSynchronize(L.stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, L.ev0, L.ev1));
+  L.kernel_ms = ms;
+  L.busy = false;
+  if (const char* path = getenv("WC_PHASES")) {
+    unsigned long long ph[kPhases];
+    HIPCHK(hipMemcpy(ph, L.phases.p, sizeof(ph), hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(path, "a")) {
+      fprintf(f, "sides=%u kernel_ms=%.3f", L.caps.sides, ms);
+      for (int k = 0; k < kPhases; ++k) fprintf(f, " %llu", ph[k]);
+      fprintf(f, "\n");
+      fclose(f);
+    }
+  }
+  if (getenv("WC_LAUNCH_LOG")) fprintf(stderr, "[wc] done problems=%u ms=%.3f\n", L.P, ms);
+  return WC_OK;
+}
+
+constexpr uint32_t kMaxAttempts = 8;
+
+int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, std::vector<SubProb>& items,
+               std::vector<EngineOut>& out, double& kernel_ms, uint64_t& launches) {
+  out.resize(items.size());
+  std::vector<uint32_t> pending;
+  for (uint32_t i = 0; i < items.size(); ++i)
+    if (out[i].status == WC_OK) pending.push_back(i);
+  Launch* L = launch_slot(ctx, 0);
+  if (!L) return set_err(ctx, WC_E_HIP, "stream creation failed");
+  while (!pending.empty()) {
+    std::stable_sort(pending.begin(), pending.end(),
+                     [&](uint32_t x, uint32_t y) { return items[x].work > items[y].work; });
+    // capacities are planned per launch from its largest problem, so a few
+    // deep problems (many reads: LDS per read, no linear-chain area above
+    // kBlock reads) run in a launch of their own instead of shrinking the node
+    // pool and occupancy of every other problem
+    std::vector<uint32_t> run, later;
+    for (uint32_t id : pending) (items[id].gid.size() > (size_t)kBlock ? later : run).push_back(id);
+    if (run.empty()) run.swap(later);
+    Caps caps;
+    std::string err;
+    int rc = plan_caps(ctx, cfg, sides, items, run, hbm_share(L->ws.cap, 0.5), caps, err);
+    if (rc != WC_OK) {
+      for (uint32_t id : run) {
+        out[id].status = rc;
+        out[id].error = err;
+      }
+      pending.swap(later);
+      continue;
+    }
+    rc = launch_start(ctx, *L, b, cfg, items, run, caps);
+    if (rc != WC_OK) return rc;
+    rc = launch_finish(ctx, *L);
+    if (rc != WC_OK) return rc;
+    kernel_ms += L->kernel_ms;
+    launches++;
+    std::vector<uint32_t> retry;
+    for (uint32_t k = 0; k < L->P; ++k) {
+      const uint32_t id = L->ids[k];
+      const uint32_t st = harvest(*L, k, items[id], out[id]);
+      if (st & ST_RETRY) {
+        bump(items[id], st);
+        if (items[id].attempts >= kMaxAttempts) {
+          out[id].status = WC_E_LIMIT;
+          out[id].error = err_msg(WC_E_LIMIT);
+        } else {
+          retry.push_back(id);
+        }
+      }
+    }
+    retry.insert(retry.end(), later.begin(), later.end());
+    pending.swap(retry);
+  }
+  return WC_OK;
+}
+
+// One persistent engine launch fed from `ready` (and from whatever `on_done`
+// appends to it) until nothing is left to run. on_done(item, raw status) is
+// called for every finished item; live(item) = false drops an item unrun.
+template <class OnDone, class Live>
+static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg, const Caps& caps,
+                        std::vector<SubProb>& items, std::deque<uint32_t>& ready, OnDone on_done, Live live,
+                        std::vector<EngineOut>& outs) {
+  constexpr uint32_t kQcap = 1u << 16;   // published, unfinished problems
+  constexpr uint32_t kQslots = 1u << 23; // their read-table entries
+  L.caps = caps;
+  L.grid = (uint32_t)std::max(1, caps.per_cu) * (uint32_t)ctx->n_cu;
+  L.P = 2 * L.grid;  // two output slots per workgroup
+  L.kernel_ms = 0;
+  const uint32_t P = L.P;
+  L.off_status = align16((uint64_t)P * 4);
+  L.off_stats = L.off_status + align16((uint64_t)P * 4);
+  L.off_out = L.off_stats + align16((uint64_t)P * S_NSTAT * 8);
+  if (!L.host.ensure(L.off_out + (uint64_t)P * caps.ob, true))
+    return set_err(ctx, WC_E_HIP, "pinned host allocation failed (results)");
+  memset(L.host.p, 0, L.off_out);
+  const uint64_t off_q = align16(sizeof(StreamCtl));
+  const uint64_t off_roff = off_q + align16((uint64_t)kQcap * sizeof(DevProblem));
+  const uint64_t off_ract = off_roff + (uint64_t)kQslots * 8;
+  const uint64_t off_rlen = off_ract + (uint64_t)kQslots * 8;
+  if (!L.ring.ensure(off_rlen + (uint64_t)kQslots * 4, true))
+    return set_err(ctx, WC_E_HIP, "pinned host allocation failed (problem ring)");
+  uint8_t* rh = (uint8_t*)L.ring.p;
+  volatile StreamCtl* sc = (volatile StreamCtl*)rh;
+  sc->tail = 0;
+  sc->stop = 0;
+  sc->abort = 0;
+  sc->heartbeat = 0;
+  DevProblem* qp = (DevProblem*)(rh + off_q);
+  uint64_t* qroff = (uint64_t*)(rh + off_roff);
+  int64_t* qract = (int64_t*)(rh + off_ract);
+  uint32_t* qrlen = (uint32_t*)(rh + off_rlen);
+  const uint64_t wsb = caps.wsb + rtab_bytes(caps.nmax);
+  if (caps.act_m && !L.act.ensure(act_scr_u64(caps.act_m) * 8 * L.grid))
+    return set_err(ctx, WC_E_HIP, "device allocation failed (activation scratch)");
+  if (!L.ws.ensure(wsb * L.grid + 64) || !L.counter.ensure(4))
+    return set_err(ctx, WC_E_HIP, "device allocation failed (workspace)");
+  HIPCHK(hipMemsetAsync(L.counter.p, 0, 4, L.stream));
+  void *dhost = nullptr, *dring = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dhost, L.host.p, 0));
+  HIPCHK(hipHostGetDevicePointer(&dring, L.ring.p, 0));
+  uint8_t* dh = (uint8_t*)dhost;
+  uint8_t* dr = (uint8_t*)dring;
+  int clk = 0;
+  if (hipDeviceGetAttribute(&clk, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || clk <= 0) clk = 100000;
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.cfg = to_dev(cfg);
+  a.problems = (const DevProblem*)(dr + off_q);
+  a.sides = 2;
+  a.rbytes = (const uint8_t*)b->reads.p;
+  a.roff = (const uint64_t*)(dr + off_roff);
+  a.rlen = (const uint32_t*)(dr + off_rlen);
+  a.ractivate = (const int64_t*)(dr + off_ract);
+  a.ws = (uint8_t*)L.ws.p;
+  a.ws_stride = wsb;
+  a.pcap = caps.pcap;
+  a.wcap = caps.wcap;
+  a.lcap = caps.lcap;
+  a.nmax = caps.nmax;
+  a.rmax = caps.rmax;
+  a.chain = 0;
+  a.out = dh + L.off_out;
+  a.out_stride = caps.ob;
+  a.status = (uint32_t*)(dh + L.off_status);
+  a.stats = (uint64_t*)(dh + L.off_stats);
+  a.done = (uint32_t*)dh;
+  a.act_m = caps.act_m;
+  a.act_scr = caps.act_m ? (uint64_t*)L.act.p : nullptr;
+  a.act_stride = caps.act_m ? act_scr_u64(caps.act_m) : 0;
+  a.stream = 1;
+  a.qcap = kQcap;
+  a.qslots = kQslots;
+  a.sctl = (StreamCtl*)dr;
+  a.qhead = (uint32_t*)L.counter.p;
+  a.idle_ticks = (uint64_t)clk * 1000ull * 30ull;  // 30 s without a host heartbeat: the host is gone
+  HIPCHK(hipEventRecord(L.ev0, L.stream));
+  launch_dual_engine(a, L.grid, caps.lds, L.stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(L.ev1, L.stream));
+  L.busy = true;
+  if (getenv("WC_LAUNCH_LOG"))
+    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u\n", L.grid,
+            caps.per_cu, caps.lds, caps.pcap, caps.wcap, caps.lcap, caps.nmax, caps.rmax);
+
+  // publication state: seq -> item, read-ring position; incomplete seqs in order
+  std::vector<uint32_t> seq_item;
+  std::vector<uint64_t> seq_rw;
+  std::vector<uint8_t> seq_done;
+  uint64_t rw = 0;
+  uint32_t oldest = 0, outstanding = 0;
+  volatile uint32_t* done = L.done();
+  int rc = WC_OK;
+  auto t_idle = std::chrono::steady_clock::now();
+  uint32_t beat = 0;
+  for (;;) {
+    bool progress = false;
+    __atomic_store_n(&sc->heartbeat, ++beat, __ATOMIC_RELAXED);
+    // publish (largest first within what is ready now)
+    if (!ready.empty()) {
+      std::vector<uint32_t> batch(ready.begin(), ready.end());
+      ready.clear();
+      std::stable_sort(batch.begin(), batch.end(), [&](uint32_t x, uint32_t y) { return items[x].work > items[y].work; });
+      size_t k = 0;
+      for (; k < batch.size(); ++k) {
+        const uint32_t id = batch[k];
+        if (!live(id)) {
+          on_done(id, ~0u);  // dropped: its problem already failed
+          continue;
+        }
+        const SubProb& s = items[id];
+        const uint32_t seq = (uint32_t)seq_item.size();
+        const uint64_t ow = oldest < seq ? seq_rw[oldest] : rw;
+        if (seq - oldest >= kQcap || rw + s.gid.size() - ow > kQslots) break;  // ring full: later
+        DevProblem d;
+        memset(&d, 0, sizeof(d));
+        d.read_begin = (uint32_t)(rw % kQslots);
+        d.n_reads = (uint32_t)s.gid.size();
+        d.max_read_len = s.max_len;
+        d.n_active = s.n_active;
+        d.max_act = s.max_act;
+        qp[seq % kQcap] = d;
+        for (size_t r = 0; r < s.gid.size(); ++r) {
+          const uint64_t q = (rw + r) % kQslots;
+          qroff[q] = b->roff_h[s.gid[r]];
+          qract[q] = s.act[r];
+          qrlen[q] = b->rlen_h[s.gid[r]];
+        }
+        seq_item.push_back(id);
+        seq_rw.push_back(rw);
+        seq_done.push_back(0);
+        rw += s.gid.size();
+        outstanding++;
+      }
+      for (; k < batch.size(); ++k) ready.push_back(batch[k]);
+      std::atomic_thread_fence(std::memory_order_release);
+      __atomic_store_n(&sc->tail, (uint32_t)seq_item.size(), __ATOMIC_RELEASE);
+      progress = true;
+    }
+    // consume finished problems
+    for (uint32_t slot = 0; slot < P; ++slot) {
+      const uint32_t v = __atomic_load_n(&done[slot], __ATOMIC_ACQUIRE);
+      if (!v) continue;
+      const uint32_t seq = v - 1;
+      const uint32_t id = seq_item[seq];
+      const uint32_t st = harvest(L, slot, items[id], outs[id]);
+      __atomic_store_n(&done[slot], 0u, __ATOMIC_RELEASE);  // the slot may be reused
+      seq_done[seq] = 1;
+      outstanding--;
+      while (oldest < seq_item.size() && seq_done[oldest]) oldest++;
+      on_done(id, st);
+      progress = true;
+    }
+    if (outstanding == 0 && ready.empty()) break;
+    if (progress) {
+      t_idle = std::chrono::steady_clock::now();
+      continue;
+    }
+    // watchdog: the launch must not end (or give up) while problems are out
+    if (sc->abort || hipStreamQuery(L.stream) == hipSuccess) {
+      rc = set_err(ctx, WC_E_HIP, "stream launch ended with problems outstanding (abort=" +
+                                      std::to_string(sc->abort) + ")");
+      break;
+    }
+    const double idle = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_idle).count();
+    if (idle > 300.0) {
+      rc = set_err(ctx, WC_E_HIP, "stream launch made no progress for 300 s");
+      break;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  __atomic_store_n(&sc->stop, 1u, __ATOMIC_RELEASE);
+  const int frc = launch_finish(ctx, L);
+  return rc != WC_OK ? rc : frc;
+}
+
+// ---------------------------------------------------------------------------
+// PriorityConsensusDWFA (priority_consensus.rs:172-341), streamed
+// ---------------------------------------------------------------------------
+namespace {
+// FxHashSet<Option<usize>> iteration order of the seed groups (priority_consensus.rs:180).
+// The set is built by `.collect()`: hashbrown's extend first reserves the
+// iterator's exact size hint (one entry per chain), so the table starts with
+// capacity_to_buckets(n_chains) buckets and never grows while the (at most
+// n_chains) distinct keys are inserted.
+uint64_t fx_add(uint64_t h, uint64_t w) { return (((h << 5) | (h >> 59)) ^ w) * 0x517cc1b727220a95ULL; }
+uint64_t fx_hash_opt(int64_t v) { return v < 0 ? fx_add(0, 0) : fx_add(fx_add(0, 1), (uint64_t)v); }
+size_t fx_cap_h(size_t b) { return b == 0 ? 0 : (b < 8 ? b - 1 : b / 8 * 7); }
+size_t fx_buckets_h(size_t cap) {
+  if (cap < 8) return cap < 4 ? 4 : 8;
+  size_t adj = cap * 8 / 7, p = 1;
+  while (p < adj) p <<= 1;
+  return p;
+}
+std::vector<int64_t> seed_order(const std::vector<int64_t>& groups) {
+  std::vector<int64_t> keys;
+  std::vector<uint64_t> hashes;
+  std::vector<int64_t> tab(fx_buckets_h(std::max<size_t>(groups.size(), 1)), -1);
+  size_t items = 0, growth = fx_cap_h(tab.size());
+  auto slot = [&](uint64_t h) -> size_t {
+    size_t B = tab.size(), mask = B - 1, pos = (size_t)h & mask;
+    if (B < 16) {
+      for (size_t i = pos; i < B; ++i)
+        if (tab[i] < 0) return i;
+      for (size_t i = 0; i < B; ++i)
+        if (tab[i] < 0) return i;
+      return 0;
+    }
+    size_t stride = 0;
+    for (;;) {
+      for (size_t j = 0; j < 16; ++j)
+        if (tab[(pos + j) & mask] < 0) return (pos + j) & mask;
+      stride += 16;
+      pos = (pos + stride) & mask;
+    }
+  };
+  for (int64_t g : groups) {
+    if (std::find(keys.begin(), keys.end(), g) != keys.end()) continue;
+    if (growth == 0) {
+      size_t nb = fx_buckets_h(std::max(items + 1, fx_cap_h(tab.size()) + 1));
+      std::vector<int64_t> old = tab;
+      tab.assign(nb, -1);
+      for (auto o : old)
+        if (o >= 0) tab[slot(hashes[o])] = o;
+      growth = fx_cap_h(nb) - items;
+    }
+    keys.push_back(g);
+    hashes.push_back(fx_hash_opt(g));
+    tab[slot(hashes.back())] = (int64_t)keys.size() - 1;
+    items++;
+    growth--;
+  }
+  std::vector<int64_t> out;
+  for (auto t : tab)
+    if (t >= 0) out.push_back(keys[t]);
+  return out;
+}
+
+// one stacked sub-problem: a read subset at a chain level
+struct PWork {
+  uint32_t owner = 0;
+  std::vector<uint8_t> inc;
+  uint32_t level = 0;
+  std::vector<ConsRec> chain;
+  int state = 0;  // 0 waiting to launch, 1 launched, 2 done
+  std::unique_ptr<ProbRes> res;
+};
+}  // namespace
+
+int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chain_problem* problems, wc_results* R) {
+  R->probs.resize(n);
+  // 1. every read of every problem (all chain levels) resident in one arena:
+  //    read (problem i, chain c, level l) = arena read base[i] + c * levels + l
+  std::vector<wc_problem> flat(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    flat[i].n_reads = problems[i].n_chains * problems[i].levels;
+    flat[i].reads = problems[i].reads;
+    flat[i].lens = problems[i].lens;
+    flat[i].offsets = nullptr;
+  }
+  wc_batch all;
+  int rc = upload_batch(ctx, n, flat.data(), &all);
+  if (rc != WC_OK) return rc;
+
+  // 2. the reference's LIFO stacks, one per problem (pool indices)
+  std::vector<std::unique_ptr<PWork>> pool;
+  std::vector<SubProb> subs;  // parallel to pool
+  std::vector<EngineOut> outs;
+  std::vector<std::vector<uint32_t>> stacks(n);
+  std::vector<std::vector<std::vector<ConsRec>>> cons(n);
+  std::vector<std::vector<std::vector<uint8_t>>> assigns(n);
+  std::vector<bool> alive(n, true);
+  std::deque<uint32_t> ready, retry_ready;
+
+  auto make = [&](uint32_t i, std::vector<uint8_t> inc, uint32_t level, std::vector<ConsRec> chain) {
+    const wc_chain_problem& q = problems[i];
+    const uint32_t id = (uint32_t)pool.size();
+    pool.emplace_back(new PWork());
+    PWork& w = *pool.back();
+    w.owner = i;
+    w.inc = std::move(inc);
+    w.level = level;
+    w.chain = std::move(chain);
+    subs.emplace_back();
+    outs.emplace_back();
+    SubProb& s = subs.back();
+    std::vector<int64_t> offs;
+    for (uint32_t c = 0; c < q.n_chains; ++c) {
+      if (!w.inc[c]) continue;
+      const uint32_t g = all.probs[i].read_begin + c * q.levels + level;
+      s.gid.push_back(g);
+      const int64_t o = q.offsets ? q.offsets[c * q.levels + level] : -1;
+      offs.push_back(o < 0 ? -1 : o);
+      s.max_len = std::max(s.max_len, all.rlen_h[g]);
+      s.work += all.rlen_h[g];
+    }
+    std::string err;
+    const int arc = activation_plan(cfg, offs, s, err);
+    if (arc != WC_OK) {  // reported like an engine failure of this sub-problem
+      w.res.reset(new ProbRes());
+      w.res->status = arc;
+      w.res->error = err;
+      w.state = 2;
+    } else {
+      ready.push_back(id);
+    }
+    stacks[i].push_back(id);
+  };
+
+  for (uint32_t i = 0; i < n; ++i) {
+    const wc_chain_problem& q = problems[i];
+    if (q.n_chains == 0 || q.levels == 0) {
+      R->probs[i].status = WC_E_BAD_INPUT;
+      R->probs[i].error = "Must provide a non-empty sequences Vec";
+      alive[i] = false;
+      continue;
+    }
+    std::vector<int64_t> groups(q.n_chains, -1);
+    if (q.seed_groups)
+      for (uint32_t c = 0; c < q.n_chains; ++c) groups[c] = q.seed_groups[c] < 0 ? -1 : q.seed_groups[c];
+    for (int64_t g : seed_order(groups)) {
+      std::vector<uint8_t> inc(q.n_chains);
+      for (uint32_t c = 0; c < q.n_chains; ++c) inc[c] = groups[c] == g;
+      make(i, std::move(inc), 0, {});
+    }
+  }
+
+  // pop finished tops in LIFO order (priority_consensus.rs:195-307); the
+  // counters of a sub-problem are added when it is popped
+  auto unwind = [&](uint32_t i) {
+    const wc_chain_problem& q = problems[i];
+    ProbRes& pr = R->probs[i];
+    while (alive[i] && !stacks[i].empty() && pool[stacks[i].back()]->state == 2) {
+      const uint32_t id = stacks[i].back();
+      stacks[i].pop_back();
+      PWork& w = *pool[id];
+      const ProbRes& d = *w.res;
+      for (int s = 0; s < S_NSTAT; ++s)
+        pr.stats[s] = s == S_PEAKQ ? std::max(pr.stats[s], d.stats[s]) : pr.stats[s] + d.stats[s];
+      if (d.status != WC_OK) {
+        pr.status = d.status;
+        pr.error = d.error;
+        alive[i] = false;
+        break;
+      }
+      const DualRec& ch = d.dual[0];
+      if (ch.has_c2) {
+        std::vector<uint8_t> a1(q.n_chains, 0), a2(q.n_chains, 0);
+        size_t idx = 0;
+        for (uint32_t c = 0; c < q.n_chains; ++c) {
+          if (!w.inc[c]) continue;
+          if (ch.is_c1[idx]) a1[c] = 1;
+          else a2[c] = 1;
+          idx++;
+        }
+        std::vector<ConsRec> chain = w.chain;
+        make(i, std::move(a1), w.level, std::move(chain));
+        make(i, std::move(a2), w.level, std::move(w.chain));
+      } else {
+        w.chain.push_back(ch.c1);
+        if (w.level + 1 == q.levels) {
+          cons[i].push_back(std::move(w.chain));
+          assigns[i].push_back(w.inc);
+        } else {
+          make(i, w.inc, w.level + 1, std::move(w.chain));
+        }
+      }
+      w.res.reset();
+    }
+  };
+
+  // 3. epochs of one persistent engine launch each (engine.hip stream mode):
+  //    sub-problems are published into a host-mapped ring as soon as they
+  //    exist, workgroups claim them in publication order, and every finished
+  //    one is consumed (and its children published) while the launch goes on.
+  //    Sub-problems that outgrow the epoch's capacities (ST_RETRY) run in a
+  //    later epoch with larger ones.
+  uint32_t max_chains = 1, max_len = 1;
+  bool any_offsets = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    max_chains = std::max(max_chains, problems[i].n_chains);
+    for (uint32_t k = 0; k < problems[i].n_chains * problems[i].levels; ++k) {
+      max_len = std::max(max_len, all.rlen_h[all.probs[i].read_begin + k]);
+      if (problems[i].offsets && problems[i].offsets[k] >= 0) any_offsets = true;
+    }
+  }
+  double kms = 0;
+  uint64_t nl = 0;
+  for (uint32_t i = 0; i < n; ++i) unwind(i);
+  std::vector<uint32_t> retry;
+  while (!ready.empty()) {
+    // capacities for anything this epoch may see: every read of every problem,
+    // plus the growth earned by the items carried over from the last epoch
+    std::vector<SubProb> env(1);
+    env[0].gid.assign(max_chains, 0);
+    env[0].max_len = max_len;
+    env[0].max_act = any_offsets ? 1 : 0;
+    for (uint32_t id : ready) {
+      env[0].wcap_x = std::max(env[0].wcap_x, subs[id].wcap_x);
+      env[0].pcap_x = std::max(env[0].pcap_x, subs[id].pcap_x);
+      env[0].lcap_x = std::max(env[0].lcap_x, subs[id].lcap_x);
+      env[0].rmax_x = std::max(env[0].rmax_x, subs[id].rmax_x);
+    }
+    Launch* L = launch_slot(ctx, 0);
+    if (!L) return set_err(ctx, WC_E_HIP, "stream creation failed");
+    std::vector<uint32_t> ids(4 * ctx->n_cu, 0);  // the pool share is planned for a full chip of workgroups
+    Caps caps;
+    std::string err;
+    int prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(L->ws.cap, 0.8), caps, err);
+    if (prc != WC_OK) {
+      for (uint32_t id : ready) {
+        pool[id]->res.reset(new ProbRes());
+        pool[id]->res->status = prc;
+        pool[id]->res->error = err;
+        pool[id]->state = 2;
+      }
+      ready.clear();
+      for (uint32_t i = 0; i < n; ++i) unwind(i);
+      continue;
+    }
+    int rc2 = stream_epoch(ctx, *L, &all, cfg, caps, subs, ready, [&](uint32_t id, uint32_t st) {
+      PWork& w = *pool[id];
+      EngineOut& o = outs[id];
+      if (st == ~0u) {  // dropped unrun: its problem already failed
+        w.res.reset(new ProbRes());
+        w.state = 2;
+        return;
+      }
+      if (st & ST_RETRY) {
+        bump(subs[id], st);
+        if (subs[id].attempts < kMaxAttempts) {
+          retry.push_back(id);
+          return;
+        }
+        o.status = WC_E_LIMIT;
+        o.error = err_msg(WC_E_LIMIT);
+      }
+      w.res.reset(new ProbRes());
+      build_dual(o, (uint32_t)subs[id].gid.size(), cfg.consensus_cost, *w.res);
+      w.state = 2;
+      o.recs.clear();
+      unwind(w.owner);
+    }, [&](uint32_t id) { return (bool)alive[pool[id]->owner]; }, outs);
+    if (rc2 != WC_OK) return rc2;
+    kms += L->kernel_ms;
+    nl++;
+    for (uint32_t id : retry) ready.push_back(id);
+    retry.clear();
+  }
+  for (uint32_t i = 0; i < n; ++i) unwind(i);
+
+  for (uint32_t i = 0; i < n; ++i) {
+    ProbRes& pr = R->probs[i];
+    if (pr.status != WC_OK) continue;
+    const uint32_t M = problems[i].n_chains;
+    auto& C = cons[i];
+    if (C.size() > 1) {
+      // priority_consensus.rs:309-335: stable sort of the chains
+      std::vector<size_t> ord(C.size());
+      std::iota(ord.begin(), ord.end(), 0);
+      std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+        size_t m = std::min(C[a].size(), C[b].size());
+        for (size_t l = 0; l < m; ++l)
+          if (C[a][l].seq != C[b][l].seq) return C[a][l].seq < C[b][l].seq;
+        return C[a].size() < C[b].size();
+      });
+      pr.indices.assign(M, UINT64_MAX);
+      for (size_t ci = 0; ci < ord.size(); ++ci) {
+        for (uint32_t c = 0; c < M; ++c)
+          if (assigns[i][ord[ci]][c]) pr.indices[c] = ci;
+        pr.chains.push_back(C[ord[ci]]);
+      }
+    } else {
+      pr.chains = C;
+      pr.indices.assign(M, 0);
+    }
+  }
+  R->stats.kernel_ms = kms;
+  R->stats.launches = nl;
+  return WC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// result types
+// ---------------------------------------------------------------------------
+int activation_plan(const wc_config& cfg, const std::vector<int64_t>& offsets, SubProb& sp, std::string& err) {
+  const size_t n = offsets.size();
+  if (n == 0) {
+    err = "No sequences provided";
+    return WC_E_BAD_INPUT;
+  }
+  std::vector<int64_t> offs = offsets;
+  if (cfg.auto_shift_offsets) {
+    int64_t mn = INT64_MAX;
+    bool start = false;
+    for (auto o : offs) {
+      if (o < 0) start = true;
+      else mn = std::min(mn, o);
+    }
+    if (!start)
+      for (auto& o : offs) o = (o == mn) ? -1 : o - mn;
+  }
+  sp.act.assign(n, -1);
+  sp.n_active = 0;
+  sp.max_act = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (offs[i] >= 0) {
+      const int64_t a = offs[i] + (int64_t)cfg.offset_compare_length;
+      if (a > (int64_t)UINT32_MAX - 2) {
+        err = "activation offset beyond the device engine's u32 lengths";
+        return WC_E_LIMIT;
+      }
+      sp.act[i] = a;
+      sp.max_act = std::max<uint32_t>(sp.max_act, (uint32_t)a);
+    } else {
+      sp.n_active++;
+    }
+  }
+  if (sp.n_active == 0) {
+    err = err_msg(WC_E_NO_START);
+    return WC_E_NO_START;
+  }
+  return WC_OK;
+}
+
+void fill_stats(wc_results* R, double kernel_ms, uint64_t launches, double wall_ms) {
+  memset(&R->stats, 0, sizeof(R->stats));
+  for (auto& p : R->probs) {
+    R->stats.updates += p.stats[S_UPDATES];
+    R->stats.w_out += p.stats[S_WOUT];
+    R->stats.compares += p.stats[S_COMPARES];
+    R->stats.ed_increases += p.stats[S_EDINC];
+    R->stats.finalizes += p.stats[S_FINALIZES];
+    R->stats.pops += p.stats[S_POPS];
+    R->stats.nodes_explored += p.stats[S_EXPLORED];
+    R->stats.nodes_ignored += p.stats[S_IGNORED];
+    R->stats.peak_queue_size = std::max(R->stats.peak_queue_size, p.stats[S_PEAKQ]);
+  }
+  R->stats.kernel_ms = kernel_ms;
+  R->stats.launches = launches;
+  R->stats.wall_ms = wall_ms;
+}
+
+// consensus.rs:345 — single results sorted by sequence
+void build_single(const EngineOut& E, int mode, ProbRes& pr) {
+  for (int s = 0; s < S_NSTAT; ++s) pr.stats[s] = E.stats[s];
+  pr.status = E.status;
+  pr.error = E.error;
+  if (pr.status != WC_OK) return;
+  for (const RawRecord& rr : E.recs) {
+    ConsRec c;
+    c.seq = rr.con[0];
+    for (auto e : rr.fe[0]) c.scores.push_back(cost_of_h(e, mode));
+    pr.single.push_back(std::move(c));
+  }
+  std::stable_sort(pr.single.begin(), pr.single.end(), [](const ConsRec& a, const ConsRec& b) { return a.seq < b.seq; });
+}
+
+// DualConsensus::from_node (dual_consensus.rs:102-150) on a finalized record
+bool dual_from_record(const RawRecord& rr, uint32_t n, int mode, DualRec& d) {
+  std::vector<uint64_t> sc[2];
+  const bool swap = rr.dual && (rr.con[1] < rr.con[0]);
+  d.is_c1.clear();
+  for (uint32_t r = 0; r < n; ++r) {
+    const uint32_t e1 = rr.fe[0][r], e2 = rr.dual ? rr.fe[1][r] : kInactive;
+    int idx = -1;
+    uint64_t best = UINT64_MAX;
+    if (e1 != kInactive) {
+      best = cost_of_h(e1, mode);
+      idx = 0;
+    }
+    if (e2 != kInactive && cost_of_h(e2, mode) < best) {
+      best = cost_of_h(e2, mode);
+      idx = 1;
+    }
+    if (idx < 0) return false;  // assert!(best_con_index <= 1)
+    d.is_c1.push_back((uint8_t)((idx == 0) ^ swap));
+    sc[idx].push_back(best);
+  }
+  ConsRec c1{rr.con[0], sc[0]}, c2{rr.dual ? rr.con[1] : std::vector<uint8_t>(), sc[1]};
+  std::vector<int64_t> s1(n), s2(n);
+  for (uint32_t r = 0; r < n; ++r) {
+    s1[r] = rr.fe[0][r] == kInactive ? -1 : (int64_t)cost_of_h(rr.fe[0][r], mode);
+    uint32_t e2 = rr.dual ? rr.fe[1][r] : kInactive;
+    s2[r] = e2 == kInactive ? -1 : (int64_t)cost_of_h(e2, mode);
+  }
+  if (swap) {
+    d.c1 = c2;
+    d.c2 = c1;
+    d.has_c2 = true;
+    d.s1 = s2;
+    d.s2 = s1;
+  } else {
+    d.c1 = c1;
+    d.has_c2 = rr.dual;
+    if (rr.dual) d.c2 = c2;
+    d.s1 = s1;
+    d.s2 = s2;
+  }
+  return true;
+}
+
+void build_dual(const EngineOut& E, uint32_t n, int mode, ProbRes& pr) {
+  for (int s = 0; s < S_NSTAT; ++s) pr.stats[s] = E.stats[s];
+  pr.status = E.status;
+  pr.error = E.error;
+  if (pr.status != WC_OK) return;
+  for (const RawRecord& rr : E.recs) {
+    DualRec d;
+    if (!dual_from_record(rr, n, mode, d)) {
+      pr.status = WC_E_INVARIANT;
+      pr.error = "read without a tracked consensus in a result";
+      return;
+    }
+    pr.dual.push_back(std::move(d));
+  }
+  if (pr.dual.size() > 1) {
+    // dual_consensus.rs:744-766
+    std::stable_sort(pr.dual.begin(), pr.dual.end(), [](const DualRec& a, const DualRec& b) {
+      static const std::vector<uint8_t> empty;
+      const auto& a2 = a.has_c2 ? a.c2.seq : empty;
+      const auto& b2 = b.has_c2 ? b.c2.seq : empty;
+      if (a.c1.seq != b.c1.seq) return a.c1.seq < b.c1.seq;
+      return a2 < b2;
+    });
+  }
+  if (pr.dual.empty()) {
+    // dual_consensus.rs:772-779: fallback to the root (every read active, empty consensus)
+    RawRecord root;
+    root.fe[0].assign(n, 0);
+    DualRec d;
+    dual_from_record(root, n, mode, d);
+    pr.dual.push_back(std::move(d));
+  }
+}
+
+}  // namespace wch

@@ -88,6 +88,7 @@ struct EngineArgs {
   uint64_t out_stride;
   uint32_t* status;      // per problem
   uint64_t* stats;       // per problem x S_NSTAT
+  uint32_t* done;        // per problem completion flag (host-mapped; set after status, stats, out)
   uint32_t* work_counter;
   uint32_t* trace;       // debug: per-pop records of problem 0 (nullptr = off)
   uint32_t trace_cap;    // records (4 u32 each); trace[0] = count
@@ -95,7 +96,29 @@ struct EngineArgs {
   uint64_t* act_scr;     // offset activation scratch: per workgroup act_stride u64
   uint64_t act_stride;
   unsigned long long* phases;  // debug (WC_PHASE_PROF builds): shader cycles per phase, kPhases
+  // stream mode (1): one persistent launch fed by the host (engine_host.cpp
+  // priority_stream). `problems` and roff/rlen/ractivate are host-mapped
+  // rings (qcap problems, qslots read entries) published up to sctl->tail;
+  // workgroups claim sequence numbers from *qhead, copy the claimed problem's
+  // read table into their workspace, and write results to one of their two
+  // output slots (blockIdx * 2 + b), flagged done[slot] = seq + 1.
+  uint32_t stream;
+  uint32_t qcap, qslots;
+  struct StreamCtl* sctl;
+  uint32_t* qhead;
+  uint64_t idle_ticks;   // wall-clock ticks without a host heartbeat before a waiting workgroup gives up
 };
+// host-mapped control words of a stream launch (16-byte aligned)
+struct alignas(16) StreamCtl {  // tail and stop form one 8-byte word (read together by the device)
+  uint32_t tail;   // problems published (host)
+  uint32_t stop;   // host: nothing more will be published (set after the final tail)
+  uint32_t abort;  // device: a workgroup gave up waiting (no heartbeat for idle_ticks)
+  uint32_t heartbeat;  // host: bumped on every pass of its event loop (liveness)
+};
+// per-workgroup copy of the claimed problem's read table (stream mode): roff | ract | rlen
+__host__ __device__ inline uint64_t rtab_bytes(uint32_t nmax) {
+  return ((uint64_t)nmax * 8 + 15) / 16 * 16 * 2 + ((uint64_t)nmax * 4 + 15) / 16 * 16;
+}
 constexpr int kPhases = 32;
 // offset-activation scratch per workgroup (u64): per wave two lane-interleaved pair arrays of m entries
 __host__ __device__ inline uint64_t act_scr_u64(uint32_t m) { return (uint64_t)kWaves * 2 * m * 64; }  // 0..15 block phases, 16..31 wave-0 sub-phases

@@ -1,0 +1,191 @@
+// Host-side types shared by the C ABI (host.cpp) and the engine scheduler
+// (engine_host.cpp). Not part of the public interface.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/waffle_con.h"
+#include "engine_shared.hpp"
+
+namespace wc {
+void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+int engine_blocks_per_cu(uint32_t sides, size_t lds);
+void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s);
+void launch_wfa_ed_batch(const EdDevJob* jobs, uint32_t n, const uint8_t* seqs, uint64_t* scratch, int wc,
+                         uint32_t both, uint64_t* out, hipStream_t s);
+}  // namespace wc
+
+// device buffer, grown on demand (never shrinks)
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    release();
+    size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+    if (hipMalloc(&p, want) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// pinned host buffer. `mapped`: fine-grained, coherent and device-visible (the
+// engine writes results and completion flags straight into it)
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes, bool mapped = false) {
+    if (bytes <= cap) return true;
+    release();
+    size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+    const unsigned flags = mapped ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault;
+    if (hipHostMalloc(&p, want, flags) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+namespace wch {
+struct Launch;
+}
+
+struct wc_ctx {
+  int device = 0;
+  int n_cu = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+  DevBuf jobs;
+  HostBuf upstage;  // pinned staging of batch uploads (reused across batches)
+  // engine launch slots (engine_host.cpp): each has its own stream and buffers
+  std::vector<wch::Launch*> launches;
+};
+
+struct BatchProblem {
+  uint32_t read_begin = 0;
+  uint32_t n_reads = 0;
+  uint32_t max_len = 0;
+  uint64_t work = 0;             // sum of read lengths (scheduling order)
+  std::vector<int64_t> offsets;  // raw add_sequence_offset values (-1 = None)
+};
+
+struct wc_batch {
+  wc_ctx* ctx = nullptr;
+  std::vector<BatchProblem> probs;
+  std::vector<uint32_t> rlen_h;
+  std::vector<uint64_t> roff_h;
+  DevBuf reads, roff, rlen;
+  uint64_t bytes = 0;
+  ~wc_batch() {
+    reads.release();
+    roff.release();
+    rlen.release();
+  }
+};
+
+struct ConsRec {
+  std::vector<uint8_t> seq;
+  std::vector<uint64_t> scores;
+};
+struct DualRec {
+  ConsRec c1, c2;
+  bool has_c2 = false;
+  std::vector<uint8_t> is_c1;
+  std::vector<int64_t> s1, s2;
+};
+struct ProbRes {
+  int status = WC_OK;
+  std::string error;
+  std::vector<ConsRec> single;
+  std::vector<DualRec> dual;
+  std::vector<std::vector<ConsRec>> chains;
+  std::vector<uint64_t> indices;
+  uint64_t stats[wc::S_NSTAT] = {0};
+};
+struct wc_results {
+  int kind = 0;  // 0 single, 1 dual, 2 priority
+  std::vector<ProbRes> probs;
+  wc_stats stats;
+};
+
+struct RawRecord {
+  uint32_t len[2] = {0, 0};
+  bool dual = false;
+  std::vector<uint8_t> con[2];
+  std::vector<uint32_t> fe[2];
+};
+
+namespace wch {
+std::string err_msg(int code);
+int set_err(wc_ctx* ctx, int code, const std::string& msg);
+wc::DevConfig to_dev(const wc_config& c);
+inline uint64_t cost_of_h(uint32_t e, int mode) { return mode == 0 ? (uint64_t)e : (uint64_t)e * (uint64_t)e; }
+int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* b);
+
+// One engine problem as the host schedules it: global read ids into a batch
+// arena and each read's activation length (-1 = active at the root).
+struct SubProb {
+  std::vector<uint32_t> gid;
+  std::vector<int64_t> act;
+  uint32_t n_active = 0, max_act = 0, max_len = 0;
+  uint64_t work = 0;
+  // capacity growth earned by ST_RETRY outcomes (log2 multipliers)
+  uint8_t wcap_x = 0, pcap_x = 0, lcap_x = 0, rmax_x = 0;
+  uint32_t attempts = 0;
+};
+// auto_shift_offsets + activation points (consensus.rs:151-202) of one
+// problem; fills sp.act / n_active / max_act or returns an error code.
+int activation_plan(const wc_config& cfg, const std::vector<int64_t>& offsets, SubProb& sp, std::string& err);
+
+// Outcome of one engine problem.
+struct EngineOut {
+  int status = WC_OK;
+  std::string error;
+  std::vector<RawRecord> recs;
+  std::array<uint64_t, wc::S_NSTAT> stats{};
+};
+
+// Runs `items` (all reads in batch `b`) to completion on the device, with
+// capacity retries; out[i] is item i's outcome.
+int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, std::vector<SubProb>& items,
+               std::vector<EngineOut>& out, double& kernel_ms, uint64_t& launches);
+
+// PriorityConsensusDWFA over many problems, streamed (engine_host.cpp).
+int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chain_problem* problems,
+                    wc_results* R);
+
+void destroy_launches(wc_ctx* ctx);
+bool dual_from_record(const RawRecord& rr, uint32_t n, int mode, DualRec& d);
+void build_single(const EngineOut& E, int mode, ProbRes& pr);
+void build_dual(const EngineOut& E, uint32_t n, int mode, ProbRes& pr);
+void fill_stats(wc_results* R, double kernel_ms, uint64_t launches, double wall_ms);
+}  // namespace wch
+
+#define HIPCHK(call)                                                                                      \
+  do {                                                                                                    \
+    hipError_t _e = (call);                                                                               \
+    if (_e != hipSuccess)                                                                                 \
+      return wch::set_err(ctx, WC_E_HIP, std::string(#call) + ": " + hipGetErrorString(_e));              \
+  } while (0)
