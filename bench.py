@@ -372,11 +372,13 @@ class Cfg5:
 
     def cpu(self, threads, target_s):
         o = orc()
+        # the rank's loci are in queue order (heaviest first): estimate the mean
+        # per-locus time from a few loci spread over that order, sample evenly
+        probe = [int(k * len(self.loci) / 4) for k in range(4)]
         t0 = time.perf_counter()
-        o.priority_consensus(self.loci[-1], wildcard=ord("*"))
-        one = time.perf_counter() - t0
-        # the rank's loci are in queue order (heaviest first): sample evenly
-        n = sample_size(one * 2, threads, target_s, len(self.loci))
+        cpu_pool_run(lambda i: o.priority_consensus(self.loci[i], wildcard=ord("*")), probe, min(4, threads))
+        one = (time.perf_counter() - t0) * min(4, threads) / len(probe)
+        n = sample_size(one, threads, target_s, len(self.loci))
         idx = [int(k * len(self.loci) / n) for k in range(n)]
         dt, outs = cpu_pool_run(lambda i: o.priority_consensus(self.loci[i], counters=True, wildcard=ord("*")), idx,
                                 threads)
@@ -460,7 +462,13 @@ def main():
     from waffle_con_amd import shard
 
     ctx = w.Context(local_rank)
+
+    def note(msg):  # progress on stderr (long workloads must not look hung)
+        print("[bench rank %d] %s" % (rank, msg), file=sys.stderr, flush=True)
+
+    note("generating %s" % a.workload)
     W = WORKLOADS[a.workload](a, rank, world, ctx)
+    note("generated in %.1f s; warmup" % W.gen_s)
 
     def sync():
         torch.cuda.synchronize()
@@ -471,6 +479,7 @@ def main():
     # so a full collection inside the timed region does not traverse it
     gc.collect()
     gc.freeze()
+    note("timed steps")
     kernel_ms, upd, wout, cmp, loci, launches = 0.0, 0, 0, 0, 0, 0
     step_ms = []
     with shard.Timer(dist, sync) as tm:
@@ -487,6 +496,7 @@ def main():
     elapsed, total_upd, total_loci = shard.reduce_run(
         dist, tm.elapsed, upd, loci, device="cuda" if dist is not None else None)
 
+    note("timed region done: %.2f s" % tm.elapsed)
     e2e = None
     if world == 1 and not a.no_e2e:
         e2e = W.e2e(max(3, a.steps))
@@ -546,6 +556,7 @@ def main():
         line["e2e_note"] = ("fresh batch every step: Python marshalling + pinned staging + H2D of the reads, "
                             "double-buffered against the previous batch's compute")
     if world == 1 and not a.no_cpu:
+        note("CPU baseline")
         cores, aff, quota = usable_cpus()
         threads = a.cpu_threads or cores
         cb = W.cpu(threads, a.cpu_seconds)

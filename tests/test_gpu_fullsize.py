@@ -123,3 +123,25 @@ def test_thousand_reads_dual_vs_oracle():
     got, gc = hip.dual_consensus(reads, counters=True)
     assert got == exp
     _counters_equal(gc, ec)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_global_state_engine_vs_oracle(seed, monkeypatch):
+    """The global-state build (engine_gstate.hip: heap, slot metadata and
+    nominations in HBM instead of LDS), forced with WC_GSTATE=1, is bit-exact
+    on the single, dual and priority engines."""
+    import waffle_con_amd as w
+    from waffle_con_amd import synth
+    monkeypatch.setenv("WC_GSTATE", "1")
+    seqs = w.generate_test(4, 1500, 20, 0.01, 40 + seed)[1]
+    exp, ec = orc.consensus(seqs, counters=True, min_count=5)
+    got, gc = hip.consensus(seqs, counters=True, min_count=5)
+    assert got == exp
+    _counters_equal(gc, ec)
+    reads = synth.cfg3_locus(50 + seed, length=400, reads=8, err=0.01)
+    exp, ec = orc.dual_consensus(reads, counters=True)
+    got, gc = hip.dual_consensus(reads, counters=True)
+    assert got == exp
+    _counters_equal(gc, ec)
+    chains = synth.cfg5_locus(60 + seed, len_range=(300, 600), reads_range=(5, 8), err=0.01)
+    assert hip.priority_consensus(chains, wildcard=ord("*")) == orc.priority_consensus(chains, wildcard=ord("*"))

@@ -21,7 +21,8 @@ PHASES = {0: "pop-broadcast", 1: "analyze", 2: "finalize", 3: "votes+select", 4:
           6: "push-heavy", 7: "heap-insert", 8: "chain-prepare", 9: "chain-walk", 10: "chain-votes",
           11: "chain-accept", 12: "votes-wave", 13: "pop-logic", 14: "chain-total"}
 # the dual engine marks the same ids: 10 = activation, 11 = prune + cost
-DUAL_PHASES = dict(PHASES, **{10: "activate", 11: "prune+cost"})
+DUAL_PHASES = dict(PHASES)
+DUAL_PHASES.update({10: "activate", 11: "prune+cost"})
 
 
 def main():

@@ -1,18 +1,38 @@
 #!/bin/bash
-# Profiles the bench workload on the GPU box (run through gpurun):
-#   1. kernel trace + stats (per-kernel durations)
-#   2. PMC pass FETCH_SIZE, 3. PMC pass WRITE_SIZE (separate passes: TCC slots)
-# Outputs under gpurun_out/prof_<tag>/; tools/pmc_summary.py condenses them.
+# Profiles one bench workload on the GPU box (run through gpurun):
+#   kt     kernel trace + stats (per-kernel durations)
+#   fetch  PMC FETCH_SIZE            } separate passes: TCC slots
+#   write  PMC WRITE_SIZE            }
+#   sq1    PMC issue view: wave cycles, busy/wait split, VALU/SALU instructions
+#   sq2    PMC LDS view: LDS instructions, bank conflicts, LDS issue stalls, memory instructions
+# Every pass is its own timeout-bounded run. Outputs under gpurun_out/prof_<tag>/;
+# tools/pmc_summary.py condenses them into profiles/.
+#   bash tools/profile_round.sh <tag> [bench args...]
 set -e
-TAG=${1:-r01}
-LOCI=${LOCI:-1000}
+TAG=${1:-r02}
+shift || true
+ARGS="$@"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
-  python3 bench.py --loci $LOCI --steps 3 --warmup 1 --no-cpu > $OUT/kt_bench.json
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
-  python3 bench.py --loci $LOCI --steps 1 --warmup 0 --no-cpu > $OUT/fetch_bench.json
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
-  python3 bench.py --loci $LOCI --steps 1 --warmup 0 --no-cpu > $OUT/write_bench.json
+  python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e $ARGS > $OUT/kt_bench.json
+echo "kt done"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/fetch_bench.json
+echo "fetch done"
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/write_bench.json
+echo "write done"
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+  SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $OUT/sq1 -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/sq1_bench.json
+echo "sq1 done"
+timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SMEM \
+  SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/sq2 -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/sq2_bench.json
+echo "sq2 done"
+timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum \
+  --output-format csv -d $OUT/tcc -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/tcc_bench.json
 echo "profile $TAG done"

@@ -73,7 +73,7 @@ __device__ __forceinline__ double wave_max_f64(double v) {
 
 // (B) backup wavefront rows to slot S, stage read windows in LDS, prefetch
 // capacities, predict symbols.
-__device__ inline void chain_prepare(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
+__device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int tid = threadIdx.x, lane = lane_id();
   SideView v = E.sv(top, 0);
   SUB_T0(ta);
@@ -298,7 +298,7 @@ static_assert(kF == 8, "vote_unit covers split <= 8");
 // written lazily (thread_push<kLazy>): only when a diagonal leaves the
 // frontier, plus one flush of the final frontier.
 template <bool kFirst>
-__device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
+__device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int lane = lane_id(), wave = wave_id();
   // reads are dealt round-robin over the waves (read = lane * kWaves + wave):
   // every wave walks a quarter of the reads, so the edit-distance increases,
@@ -489,7 +489,7 @@ __device__ inline void chain_walk(Eng& E, Sh<Ctl>& ctl, uint32_t top, uint32_t L
 // walk's exact rational vote totals (prediction vs everything else) decide
 // almost every step; the rest take the exact path (per-key f64 sums in read
 // order, hashbrown key order).
-__device__ inline void chain_votes(Eng& E, Sh<Ctl>& ctl, uint32_t K) {
+__device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t K) {
   const int lane = lane_id();
   const DevConfig& cfg = E.cfg;
   for (uint32_t j = 1 + wave_id(); j < K; j += kWaves) {
@@ -540,7 +540,7 @@ __device__ inline void chain_votes(Eng& E, Sh<Ctl>& ctl, uint32_t K) {
 // The step-local tests (max_err, capacity, reached_end, one passing candidate)
 // are evaluated by lanes over j at once; only the PQueueTracker threshold walk
 // is sequential, on registers.
-__device__ inline uint32_t chain_accept(Eng& E, Sh<Ctl>& ctl, uint32_t L0, uint32_t Keff) {
+__device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint32_t Keff) {
   const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
   const uint32_t lane = (uint32_t)lane_id();
@@ -591,7 +591,7 @@ __device__ inline uint32_t chain_accept(Eng& E, Sh<Ctl>& ctl, uint32_t L0, uint3
 // otherwise empty) whose single child symbol is s1. Returns j* (uniform); for
 // j* > 0 the chain node N_j* is in slot `top`/LDS, queued, with its
 // nominations cached; j* == 0 leaves everything as it was.
-__device__ __noinline__ uint32_t run_chain(Eng& Eref, Sh<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
+__device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
   Eng E = eng_uniform(Eref);  // scalar-register copy of the caller's context
   const int tid = threadIdx.x;
   if (tid == 0) {

@@ -20,7 +20,15 @@
 
 #include "engine_common.hip.hpp"
 
-namespace wc {
+namespace WC_ENGINE_NS {
+
+// WC_SPLIT builds (A/B experiments): the per-pop block phases are separate
+// functions with their own register allocation instead of being inlined
+#ifdef WC_SPLIT
+#define WC_PHASE_FN __device__ __noinline__
+#else
+#define WC_PHASE_FN __device__ inline
+#endif
 
 // minimum waves per SIMD the engine kernels are register-allocated for
 // (4 = 4 workgroups of 4 waves per CU, 128 VGPRs)
@@ -190,7 +198,7 @@ __device__ inline bool prio_less(const A& a, const B& b) {
   if (a.cost != b.cost) return a.cost > b.cost;  // Reverse(cost)
   return a.len < b.len;
 }
-__device__ inline void heap_push(Sh<HeapEntry>* h, Sh<uint32_t>& n, HeapEntry e) {
+__device__ inline void heap_push(Sh<HeapEntry>* h, Lo<uint32_t>& n, HeapEntry e) {
   uint32_t pos = n++;
   while (pos > 0) {
     uint32_t parent = (pos - 1) / 2;
@@ -200,7 +208,7 @@ __device__ inline void heap_push(Sh<HeapEntry>* h, Sh<uint32_t>& n, HeapEntry e)
   }
   h[pos] = e;
 }
-__device__ inline HeapEntry heap_pop(Sh<HeapEntry>* h, Sh<uint32_t>& n) {
+__device__ inline HeapEntry heap_pop(Sh<HeapEntry>* h, Lo<uint32_t>& n) {
   HeapEntry top = h[0];
   n--;
   h[0] = h[n];
@@ -226,8 +234,8 @@ __device__ inline HeapEntry heap_pop(Sh<HeapEntry>* h, Sh<uint32_t>& n) {
 struct TrackerRef {
   Gm<uint32_t>* lc;
   Gm<uint32_t>* pc;
-  Sh<uint64_t>* total;
-  Sh<uint64_t>* thr;
+  Lo<uint64_t>* total;
+  Lo<uint64_t>* thr;
   uint64_t cap;
   __device__ void insert(uint32_t v) {
     lc[v]++;
@@ -267,7 +275,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 // wave-uniform counters (lane 0 holds them)
-__device__ inline void flush_counters(Sh<Ctl>& ctl, const WaveCounters& wc) {
+__device__ inline void flush_counters(Lo<Ctl>& ctl, const WaveCounters& wc) {
   if (lane_id() == 0) {
     if (wc.updates) atomicAdd((unsigned long long*)&ctl.cnt[S_UPDATES], (unsigned long long)wc.updates);
     if (wc.w_out) atomicAdd((unsigned long long*)&ctl.cnt[S_WOUT], (unsigned long long)wc.w_out);
@@ -277,7 +285,7 @@ __device__ inline void flush_counters(Sh<Ctl>& ctl, const WaveCounters& wc) {
   }
 }
 // per-thread counters (every lane its own): wave-reduce, then lane 0 adds
-__device__ inline void flush_thread_counters(Sh<Ctl>& ctl, WaveCounters c) {
+__device__ inline void flush_thread_counters(Lo<Ctl>& ctl, WaveCounters c) {
   c.updates = wave_sum_u32(c.updates);
   c.w_out = wave_sum_u32(c.w_out);
   c.compares = wave_sum_u32(c.compares);
@@ -314,7 +322,7 @@ struct Eng {
   }
   __device__ const Gm<uint8_t>* read(uint32_t r) const { return rbytes + roff[P.read_begin + r]; }
   __device__ uint32_t rlen(uint32_t r) const { return rlenp[P.read_begin + r]; }
-  __device__ TrackerRef tracker(Sh<Ctl>& ctl, int k) const {
+  __device__ TrackerRef tracker(Lo<Ctl>& ctl, int k) const {
     const uint64_t L2 = lcap + 2;
     return TrackerRef{trk + 2 * k * L2, trk + (2 * k + 1) * L2, &ctl.trk_total[k], &ctl.trk_thr[k],
                       cfg.max_capacity_per_size};
@@ -379,7 +387,7 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
 // workgroup's next output slot has been consumed; then copy the problem's
 // descriptor and read table into the workgroup's workspace. Returns the
 // problem (sequence number), or ~0u to exit; `oslot` = output slot index.
-__device__ inline uint32_t claim_problem(const EngineArgs& A, Sh<Ctl>& ctl, Eng& E, uint32_t& oslot) {
+__device__ inline uint32_t claim_problem(const EngineArgs& A, Lo<Ctl>& ctl, Eng& E, uint32_t& oslot) {
   const int tid = threadIdx.x;
   if (!A.stream) {
     if (tid == 0) ctl.prob = atomicAdd(A.work_counter, 1u);
@@ -464,8 +472,18 @@ __device__ inline uint32_t claim_problem(const EngineArgs& A, Sh<Ctl>& ctl, Eng&
   return seq;
 }
 
+// Where a workgroup's search state (heap, slot metadata, nominations, chain
+// area) lives: dynamic LDS, or its own HBM region in the global-state build.
+__device__ inline Sh<uint8_t>* state_base(const EngineArgs& A, uint8_t* smem) {
+#ifdef WC_GLOBAL_STATE
+  return (Sh<uint8_t>*)(A.gstate + (uint64_t)blockIdx.x * A.gstate_stride);
+#else
+  return (Sh<uint8_t>*)smem;
+#endif
+}
+
 // ---- per-problem init: free stack, trackers, root node (consensus.rs:384-403) ----
-__device__ inline void init_problem(Eng& E, Sh<Ctl>& ctl) {
+__device__ inline void init_problem(Eng& E, Lo<Ctl>& ctl) {
   const int tid = threadIdx.x;
   const DevConfig& cfg = E.cfg;
   if (tid == 0) {
@@ -528,7 +546,7 @@ __device__ __forceinline__ auto node_rs(Eng& E, uint32_t slot, uint32_t side) {
 }
 
 template <bool kHot>
-__device__ inline void analyze_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t len, Sh<RInfo>* out) {
+WC_PHASE_FN void analyze_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t len, Sh<RInfo>* out) {
   const int tid = threadIdx.x, lane = lane_id();
   SideView v = E.sv(slot, side);
   const auto rs = node_rs<kHot>(E, slot, side);
@@ -573,7 +591,7 @@ __device__ inline void analyze_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32_
 
 // ---- FINALIZE one side on scratch (the node is not modified) ----
 template <bool kHot>
-__device__ inline void finalize_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t len, uint32_t* fe,
+WC_PHASE_FN void finalize_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t len, uint32_t* fe,
                                      WaveCounters& cnt) {
   const int lane = lane_id();
   SideView v = E.sv(slot, side);
@@ -604,7 +622,7 @@ __device__ inline void finalize_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32
 // kSrcHot: the parent's RStates are the LDS copy (else the slot's own);
 // kDstHot: the child's RStates go to the LDS copy (else to the slot).
 template <bool kSrcHot, bool kDstHot>
-__device__ inline void push_sides(Eng& E, Sh<Ctl>& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
+WC_PHASE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
                                   bool want_cost, Sh<RInfo>* info) {
   const int tid = threadIdx.x, lane = lane_id();
   const DevConfig& cfg = E.cfg;
@@ -749,7 +767,7 @@ __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t d
 // cache) and counts their ends/multi. ctl.ovf: 4 wavefront capacity, 2 offset
 // scratch, 16 an already active read (the reference's assert).
 template <bool kHot>
-__device__ inline void activate_side(Eng& E, Sh<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t clen, uint32_t alen,
+WC_PHASE_FN void activate_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t clen, uint32_t alen,
                                      bool want_cost, Sh<RInfo>* info) {
   const int tid = threadIdx.x, lane = lane_id();
   if (tid == 0) ctl.nheavy = 0;
@@ -996,7 +1014,7 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
 }
 
 
-__device__ inline bool wave_votes(Sh<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, const Sh<RInfo>* r0, const Sh<RInfo>* r1,
+WC_PHASE_FN bool wave_votes(Lo<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, const Sh<RInfo>* r0, const Sh<RInfo>* r1,
                                   uint32_t n, bool weighted, bool is_dual, bool multi, int wc) {
   const int lane = lane_id();
   const bool side1 = side == 0;
@@ -1018,7 +1036,7 @@ __device__ inline bool wave_votes(Sh<Ctl>& ctl, uint32_t side, const Sh<RInfo>* 
 #include "chain.hip.hpp"
 
 // ---- write one result record (finalized node) ----
-__device__ inline void store_record(Eng& E, Sh<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t slot, uint32_t nsides,
+WC_PHASE_FN void store_record(Eng& E, Lo<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t slot, uint32_t nsides,
                                     const uint32_t* lens, bool is_dual) {
   const int tid = threadIdx.x;
   const uint64_t rb = result_bytes(E.sides, E.nmax, E.lcap);
@@ -1053,7 +1071,7 @@ __device__ inline void trace_pop(const EngineArgs& A, uint32_t prob, const HeapE
   A.trace[0] = k + 1;
 }
 
-__device__ inline void finish_problem(const EngineArgs& A, Sh<Ctl>& ctl, uint8_t* outp, uint32_t prob, uint32_t oslot) {
+__device__ inline void finish_problem(const EngineArgs& A, Lo<Ctl>& ctl, uint8_t* outp, uint32_t prob, uint32_t oslot) {
   // every wave's result-record stores complete (system scope) before the flag
   __threadfence_system();
   __syncthreads();
@@ -1083,12 +1101,12 @@ __device__ inline void finish_problem(const EngineArgs& A, Sh<Ctl>& ctl, uint8_t
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) single_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
-  Sh<Ctl>& ctl = *(Sh<Ctl>*)&ctl_lds;
+  Lo<Ctl>& ctl = *(Lo<Ctl>*)&ctl_lds;
   const int tid = threadIdx.x;
   const int lane = lane_id();
   const DevConfig& cfg = A.cfg;
   const bool early = cfg.early != 0;
-  Eng E = make_eng(A, (Sh<uint8_t>*)smem);
+  Eng E = make_eng(A, state_base(A, smem));
 
   if (tid == 0) ctl.obuf = 1;
   for (;;) {
@@ -1336,13 +1354,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
-  Sh<Ctl>& ctl = *(Sh<Ctl>*)&ctl_lds;
+  Lo<Ctl>& ctl = *(Lo<Ctl>*)&ctl_lds;
   const int tid = threadIdx.x;
   const int lane = lane_id();
   const DevConfig& cfg = A.cfg;
   const bool early = cfg.early != 0;
   const bool weighted = cfg.weighted != 0;
-  Eng E = make_eng(A, (Sh<uint8_t>*)smem);
+  Eng E = make_eng(A, state_base(A, smem));
   Sh<RInfo>* R0 = E.L.rinfo;
   Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
 
@@ -1565,8 +1583,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
             nc++;
           }
           // split children from every pair of sorted candidates (:682-734)
-          Sh<double>* cv = ctl.srt_v;
-          Sh<uint8_t>* cs = ctl.srt_s;
+          Lo<double>* cv = ctl.srt_v;
+          Lo<uint8_t>* cs = ctl.srt_s;
           uint32_t ns = 0, passing = 0;
           for (uint32_t k = 0; k < ctl.nkeys[0]; ++k) {
             if (cfg.wildcard >= 0 && ctl.keys[0][k] == (uint8_t)cfg.wildcard) continue;
@@ -1726,6 +1744,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
   }
 }
 
+#ifndef WC_GLOBAL_STATE
 // =====================================================================
 // standalone DWFALite jobs (dynamic_wfa.rs:48-265): one wave per job
 // =====================================================================
@@ -1763,7 +1782,7 @@ __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
     }
   } else {
     __shared__ RInfo ri_lds;
-    Sh<RInfo>& ri = *(Sh<RInfo>*)&ri_lds;
+    Lo<RInfo>& ri = *(Lo<RInfo>*)&ri_lds;
     if (!wave_analyze_read(wf, e, j.offset, base, j.blen, j.olen, &ri)) status = WC_E_LIMIT_CODE;
     __builtin_amdgcn_wave_barrier();
     if (lane == 0 && status == 0) {
@@ -1780,6 +1799,8 @@ __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
   }
 }
 
+#endif
+
 void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(single_engine_kernel, dim3(grid), dim3(kBlock), lds, s, a);
 }
@@ -1792,8 +1813,10 @@ int engine_blocks_per_cu(uint32_t sides, size_t lds) {
                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kBlock, lds);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
+#ifndef WC_GLOBAL_STATE
 void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s) {
   hipLaunchKernelGGL(dwfa_jobs_kernel, dim3(n), dim3(64), 0, s, jobs);
 }
+#endif
 
-}  // namespace wc
+}  // namespace WC_ENGINE_NS

@@ -11,18 +11,34 @@
 
 #include "engine_shared.hpp"
 
-namespace wc {
+// The engine is compiled twice: normally (namespace wc, per-problem search
+// state in LDS) and as engine_gstate.hip (namespace wcg, WC_GLOBAL_STATE: the
+// same state in a per-workgroup HBM region) for problems whose state does not
+// fit one workgroup's 160 KiB of LDS (many reads, deep queues).
+#ifndef WC_ENGINE_NS
+#define WC_ENGINE_NS wc
+#endif
+
+namespace WC_ENGINE_NS {
+using namespace ::wc;
 
 // Explicit address spaces: HBM (global) and LDS pointers compile to global_* /
 // ds_* instructions instead of flat_* (which wait on both counters and take
-// the slower path). The engines keep every pointer in one of these types.
-// (The host pass of this single-source file only parses device code; it sees
-// plain types.)
+// the slower path). The engines keep every pointer in one of these types:
+// Gm = HBM, Lo = LDS, Sh = the search state (LDS, or HBM in the global-state
+// build). (The host pass of this single-source file only parses device code;
+// it sees plain types.)
 #if defined(__HIP_DEVICE_COMPILE__)
 template <class T> using Gm = __attribute__((address_space(1))) T;
+template <class T> using Lo = __attribute__((address_space(3))) T;
+#ifdef WC_GLOBAL_STATE
+template <class T> using Sh = __attribute__((address_space(1))) T;
+#else
 template <class T> using Sh = __attribute__((address_space(3))) T;
+#endif
 #else
 template <class T> using Gm = T;
+template <class T> using Lo = T;
 template <class T> using Sh = T;
 #endif
 
@@ -135,7 +151,7 @@ __device__ __forceinline__ RRaw rstate_load(const Gm<RState>* p) {
   const Gm<uint4>* q = (const Gm<uint4>*)p;
   return RRaw{q[0], q[1], q[2], q[3]};
 }
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(WC_GLOBAL_STATE)
 __device__ __forceinline__ RRaw rstate_load(const Sh<RState>* p) {
   const Sh<uint4>* q = (const Sh<uint4>*)p;
   return RRaw{q[0], q[1], q[2], q[3]};
@@ -148,7 +164,7 @@ __device__ __forceinline__ void rstate_store(Gm<RState>* p, const RRaw& s) {
   q[2] = s.c;
   q[3] = s.d;
 }
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(WC_GLOBAL_STATE)
 __device__ __forceinline__ void rstate_store(Sh<RState>* p, const RRaw& s) {
   Sh<uint4>* q = (Sh<uint4>*)p;
   q[0] = s.a;
@@ -986,4 +1002,4 @@ __device__ inline int wave_activate(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* 
   return 0;
 }
 
-}  // namespace wc
+}  // namespace WC_ENGINE_NS

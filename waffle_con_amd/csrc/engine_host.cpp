@@ -43,9 +43,11 @@ uint64_t hbm_share(uint64_t cached, double share) {
 
 struct Caps {
   uint32_t sides = 1, pcap = 16, wcap = 64, lcap = 64, nmax = 1, chain = 0, rmax = 1, act_m = 0;
-  size_t lds = 0;
+  size_t lds = 0;   // dynamic LDS per workgroup (0 in the global-state build)
   int per_cu = 1;
   uint64_t wsb = 0, ob = 0;
+  bool gstate = false;  // search state in HBM (engine_gstate.hip): it does not fit LDS
+  uint64_t gsb = 0;     // its bytes per workgroup
 };
 
 // Capacities of one launch over items[ids] (SURVEY §8(a) sizes): wavefront row
@@ -86,19 +88,24 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
   const uint64_t budget = sides == 1 ? (16ull << 20) : std::min<uint64_t>(256ull << 20, per_wg);
   const uint32_t pmax = sides == 1 ? 256u : 1024u;
   const uint64_t lmax = sides == 1 ? 40 * 1024 : 48 * 1024;
+  // WC_GSTATE=1 (test hook) forces the global-state build for every launch
+  bool gstate = getenv("WC_GSTATE") != nullptr;
   uint32_t pcap = 16;
-  while (pcap < pmax && (uint64_t)(pcap * 2) * sb <= budget && lds_bytes(sides, pcap * 2, nmax, chain) <= lmax)
+  while (pcap < pmax && (uint64_t)(pcap * 2) * sb <= budget &&
+         (gstate || lds_bytes(sides, pcap * 2, nmax, chain) <= lmax))
     pcap *= 2;
-  // a retried (pool-exhausted) item gets 4x per retry, as HBM and LDS allow
+  // a retried (pool-exhausted) item gets 4x per retry, as HBM allows; past
+  // what LDS holds, the search state moves to HBM
   for (uint32_t k = 0; k < px; ++k) {
     const uint32_t np = pcap * 2;
-    if ((uint64_t)np * sb > std::max<uint64_t>(budget, per_wg) || lds_bytes(sides, np, nmax, chain) > kLdsMax) break;
+    if ((uint64_t)np * sb > std::max<uint64_t>(budget, per_wg)) break;
     pcap = np;
   }
+  if (lds_bytes(sides, pcap, nmax, chain) > kLdsMax) gstate = true;
   // longer chains amortise the per-chain work (prediction, acceptance, the
   // literal pop between chains); take the longest one whose LDS still gives
   // the workgroups per CU of the default length (results do not depend on it)
-  if (!chain_env && chain > 0) {
+  if (!chain_env && chain > 0 && !gstate) {
     const int occ = engine_blocks_per_cu(sides, (size_t)lds_bytes(sides, pcap, nmax, chain));
     for (uint32_t k = chain + 1; k <= kChainMax; ++k) {
       const uint64_t l = lds_bytes(sides, pcap, nmax, k);
@@ -131,12 +138,10 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
     }
     c.act_m = (uint32_t)m;
   }
-  c.lds = (size_t)lds_bytes(sides, pcap, nmax, chain);
-  if (c.lds > kLdsMax) {
-    err = "problem needs more LDS than one workgroup has (reads x node pool)";
-    return WC_E_LIMIT;
-  }
-  c.per_cu = engine_blocks_per_cu(sides, c.lds);
+  c.gstate = gstate;
+  c.gsb = align16(lds_bytes(sides, pcap, nmax, chain));
+  c.lds = gstate ? 0 : (size_t)c.gsb;
+  c.per_cu = gstate ? wcg::engine_blocks_per_cu(sides, 0) : engine_blocks_per_cu(sides, c.lds);
   c.wsb = ws_bytes(sides, pcap, nmax, c.wcap, c.lcap);
   c.ob = out_bytes(sides, c.rmax, nmax, c.lcap);
   return WC_OK;
@@ -146,7 +151,7 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
 struct Launch {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  DevBuf probs, sroff, srlen, ract, ws, counter, act, phases;
+  DevBuf probs, sroff, srlen, ract, ws, counter, act, phases, gst;
   HostBuf host;  // mapped: done[P] | status[P] | stats[P][S_NSTAT] | out[P]
   HostBuf ring;  // mapped (stream launches): StreamCtl | problem ring | read-table rings
   Caps caps;
@@ -167,7 +172,7 @@ struct Launch {
   const uint64_t* stats() const { return (const uint64_t*)((const uint8_t*)host.p + off_stats); }
   const uint8_t* out(uint32_t k) const { return (const uint8_t*)host.p + off_out + (uint64_t)k * caps.ob; }
   ~Launch() {
-    for (DevBuf* b : {&probs, &sroff, &srlen, &ract, &ws, &counter, &act, &phases}) b->release();
+    for (DevBuf* b : {&probs, &sroff, &srlen, &ract, &ws, &counter, &act, &phases, &gst}) b->release();
     host.release();
     ring.release();
     if (ev0) (void)hipEventDestroy(ev0);
@@ -179,6 +184,26 @@ struct Launch {
 void destroy_launches(wc_ctx* ctx) {
   for (Launch* L : ctx->launches) delete L;
   ctx->launches.clear();
+}
+
+// launches the engine of `caps` (LDS or global-state build) on L's stream
+static int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
+  if (caps.gstate) {
+    if (!L.gst.ensure(caps.gsb * L.grid)) return set_err(ctx, WC_E_HIP, "device allocation failed (search state)");
+    a.gstate = (uint8_t*)L.gst.p;
+    a.gstate_stride = caps.gsb;
+  }
+  HIPCHK(hipEventRecord(L.ev0, L.stream));
+  if (caps.gstate) {
+    if (caps.sides == 1) wcg::launch_single_engine(a, L.grid, 0, L.stream);
+    else wcg::launch_dual_engine(a, L.grid, 0, L.stream);
+  } else {
+    if (caps.sides == 1) launch_single_engine(a, L.grid, caps.lds, L.stream);
+    else launch_dual_engine(a, L.grid, caps.lds, L.stream);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(L.ev1, L.stream));
+  return WC_OK;
 }
 
 static Launch* launch_slot(wc_ctx* ctx, size_t k) {
@@ -280,15 +305,12 @@ static int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
     a.phases = (unsigned long long*)L.phases.p;
     HIPCHK(hipMemsetAsync(L.phases.p, 0, kPhases * 8, L.stream));
   }
-  HIPCHK(hipEventRecord(L.ev0, L.stream));
-  if (caps.sides == 1) launch_single_engine(a, L.grid, caps.lds, L.stream);
-  else launch_dual_engine(a, L.grid, caps.lds, L.stream);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(L.ev1, L.stream));
+  const int krc = launch_kernel(ctx, L, a, caps);
+  if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
-            caps.sides, P, L.grid, caps.per_cu, caps.lds, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
+    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
+            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
   return WC_OK;
 }
 
@@ -497,10 +519,8 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.sctl = (StreamCtl*)dr;
   a.qhead = (uint32_t*)L.counter.p;
   a.idle_ticks = (uint64_t)clk * 1000ull * 30ull;  // 30 s without a host heartbeat: the host is gone
-  HIPCHK(hipEventRecord(L.ev0, L.stream));
-  launch_dual_engine(a, L.grid, caps.lds, L.stream);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(L.ev1, L.stream));
+  const int krc = launch_kernel(ctx, L, a, caps);
+  if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
     fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u\n", L.grid,
@@ -515,9 +535,16 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   volatile uint32_t* done = L.done();
   int rc = WC_OK;
   auto t_idle = std::chrono::steady_clock::now();
-  uint32_t beat = 0;
+  uint32_t beat = 0, finished = 0;
+  const bool log = getenv("WC_LAUNCH_LOG") != nullptr;
+  auto t_log = std::chrono::steady_clock::now();
   for (;;) {
     bool progress = false;
+    if (log && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_log).count() > 10.0) {
+      t_log = std::chrono::steady_clock::now();
+      fprintf(stderr, "[wc] stream: %u published, %u finished, %u outstanding, %zu waiting\n",
+              (uint32_t)seq_item.size(), finished, outstanding, ready.size());
+    }
     __atomic_store_n(&sc->heartbeat, ++beat, __ATOMIC_RELAXED);
     // publish (largest first within what is ready now)
     if (!ready.empty()) {
@@ -570,6 +597,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
       __atomic_store_n(&done[slot], 0u, __ATOMIC_RELEASE);  // the slot may be reused
       seq_done[seq] = 1;
       outstanding--;
+      finished++;
       while (oldest < seq_item.size() && seq_done[oldest]) oldest++;
       on_done(id, st);
       progress = true;

@@ -107,6 +107,10 @@ struct EngineArgs {
   struct StreamCtl* sctl;
   uint32_t* qhead;
   uint64_t idle_ticks;   // wall-clock ticks without a host heartbeat before a waiting workgroup gives up
+  // global-state build (engine_gstate.hip): per-workgroup HBM region holding
+  // what lds_bytes() describes
+  uint8_t* gstate;
+  uint64_t gstate_stride;
 };
 // host-mapped control words of a stream launch (16-byte aligned)
 struct alignas(16) StreamCtl {  // tail and stop form one 8-byte word (read together by the device)

@@ -20,6 +20,11 @@ void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s);
 void launch_wfa_ed_batch(const EdDevJob* jobs, uint32_t n, const uint8_t* seqs, uint64_t* scratch, int wc,
                          uint32_t both, uint64_t* out, hipStream_t s);
 }  // namespace wc
+namespace wcg {  // engine_gstate.hip: search state in HBM
+void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+int engine_blocks_per_cu(uint32_t sides, size_t lds);
+}  // namespace wcg
 
 // device buffer, grown on demand (never shrinks)
 struct DevBuf {
