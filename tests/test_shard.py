@@ -83,3 +83,59 @@ def test_gloo_world2_sharded_loci():
     for s, seqs in merged.items():
         exp = [x["sequence"] for x in orc.consensus(w.generate_test(4, 200, 6, 0.02, s)[1], min_count=2)]
         assert seqs == exp
+
+
+def test_cost_sorted_assignment_is_a_partition():
+    costs = [5, 1, 9, 9, 3, 7, 2, 8, 4, 6, 10, 1]
+    for world in (1, 2, 3, 8):
+        parts = shard.cost_sorted_assignment(costs, world)
+        flat = sorted(i for p in parts for i in p)
+        assert flat == list(range(len(costs)))
+        # each rank's list is in queue order (non-increasing cost)
+        for p in parts:
+            assert all(costs[a] >= costs[b] for a, b in zip(p, p[1:]))
+        loads = [sum(costs[i] for i in p) for p in parts]
+        # LPT bound: max load <= mean + largest item
+        assert max(loads) <= sum(costs) / world + max(costs)
+
+
+def _queue_worker(rank, world, port, n_items, chunk, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from waffle_con_amd import synth
+        costs = [synth.cfg5_cost(s) for s in range(n_items)]
+        static = shard.cost_sorted_assignment(costs, world)[rank]
+        store = dist.distributed_c10d._get_default_store()
+        sq = shard.SharedQueue(store, n_items, chunk)
+        got = []
+        while True:
+            c = sq.next_chunk()
+            if c is None:
+                break
+            got.extend(range(*c))
+        dist.barrier()
+        q.put((rank, static, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_cost_sorted_queue():
+    """bench.py --workload cfg5 at world size 2: the static cost-sorted (LPT)
+    assignment and the store-backed shared queue both hand every locus to
+    exactly one rank, with no collective on the data path."""
+    world, n, chunk = 2, 37, 4
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_queue_worker, args=(r, world, port, n, chunk, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    static = [o[1] for o in out]
+    dyn = [o[2] for o in out]
+    assert sorted(static[0] + static[1]) == list(range(n)) and not set(static[0]) & set(static[1])
+    assert sorted(dyn[0] + dyn[1]) == list(range(n)) and not set(dyn[0]) & set(dyn[1])

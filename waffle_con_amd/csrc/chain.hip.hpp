@@ -94,12 +94,12 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     if (lo == kInactive) lo = 0;
     const uint32_t wb = lo & ~15u;
     const Gm<uint4>* g = (const Gm<uint4>*)(E.read(r) + wb);
-    Sh<uint4>* w = (Sh<uint4>*)(E.L.cwin + (uint64_t)r * 64);
+    Sh<uint32_t>* w = (Sh<uint32_t>*)(E.L.cwin + (uint64_t)win_slot(r, win_m4(E.n)) * kWinStride);
     const uint4 a0 = g[0], a1 = g[1], a2 = g[2], a3 = g[3];
-    w[0] = a0;
-    w[1] = a1;
-    w[2] = a2;
-    w[3] = a3;
+    w[0] = a0.x, w[1] = a0.y, w[2] = a0.z, w[3] = a0.w;
+    w[4] = a1.x, w[5] = a1.y, w[6] = a1.z, w[7] = a1.w;
+    w[8] = a2.x, w[9] = a2.y, w[10] = a2.z, w[11] = a2.w;
+    w[12] = a3.x, w[13] = a3.y, w[14] = a3.z, w[15] = a3.w;
     E.L.cwb[r] = wb;
   }
   const Gm<uint32_t>* pc = E.trk + (E.lcap + 2);  // PQueueTracker processed counts
@@ -112,7 +112,7 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     // predicts the steps t = 1 + wave (mod kWaves)
     const uint32_t wave = (uint32_t)wave_id();
     uint32_t bo_tip = kInactive, blen = 0, wb = 0;
-    const Sh<uint8_t>* win = E.L.cwin + (uint64_t)min((uint32_t)lane, E.n - 1) * 64;
+    const Sh<uint8_t>* win = E.L.cwin + (uint64_t)win_slot(min((uint32_t)lane, E.n - 1), win_m4(E.n)) * kWinStride;
     if ((uint32_t)lane < E.n) {
       Front f;
       front_load(rstate_load(&E.L.hot[lane]), f);
@@ -290,6 +290,27 @@ __device__ __forceinline__ uint32_t vote_unit(uint32_t split) {
 }
 static_assert(kF == 8, "vote_unit covers split <= 8");
 
+// The ED-increase step of one read inside the chain walk (rare: ~0.5% of the
+// updates at cfg2) as a call, so its registers do not add to the walk's
+// per-step register pressure (the walk keeps a frontier per lane in registers).
+// Arguments and result by value (no stack objects): returns the new edit
+// distance, or kInactive on wavefront capacity overflow; the work counters go
+// straight to the chain totals.
+__device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
+                                             const Gm<uint8_t>* con, uint32_t olen, uint32_t sym, int wc, bool early,
+                                             uint32_t wcap, Lo<uint64_t>* tot) {
+  WaveCounters cnt = {0, 0, 0, 0, 0};
+  uint32_t e_out = 0;
+  const bool ok = wave_heavy(tmp, wf, rd, blen, con, olen, (uint8_t)sym, wc, early, wcap, cnt, e_out);
+  if (lane_id() == 0) {
+    atomicAdd((unsigned long long*)&tot[0], (unsigned long long)cnt.updates);
+    atomicAdd((unsigned long long*)&tot[1], (unsigned long long)cnt.w_out);
+    atomicAdd((unsigned long long*)&tot[2], (unsigned long long)cnt.compares);
+    atomicAdd((unsigned long long*)&tot[3], (unsigned long long)cnt.edinc);
+  }
+  return ok ? e_out : kInactive;
+}
+
 // (C) push the K predicted symbols through every read, thread per read.
 // kFirst: speculative pass; stores each step's nominations and aggregates,
 // leaves the final RStates in slot S. Replay pass: writes the final RStates to
@@ -315,7 +336,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   f.off = f.maxb = f.nscmp = f.mask = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) f.fi[k] = f.fd[k] = 0;
-  Win W{E.L.cwin + (uint64_t)min(r, E.n - 1) * 64, 0};
+  Win W{E.L.cwin + (uint64_t)win_slot(min(r, E.n - 1), win_m4(E.n)) * kWinStride, 0};
   uint32_t blen = 0;
   if (has) {
     front_load(rstate_load(&E.L.hot[r]), f);
@@ -326,7 +347,6 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   Gm<uint32_t>* wf_row = v.wf + (uint64_t)r * E.wcap;
   Sh<RState>* tmp = &E.L.ctmp[wave];
   uint32_t t_upd = 0, t_wout = 0, t_cmp = 0;
-  WaveCounters cnt = {0, 0, 0, 0, 0};
   uint64_t bak = 0;  // lanes whose row was backed up (wave-uniform)
   // this wave's share of the node cost; changes only when an edit distance grows
   uint64_t wcost = kFirst ? wave_sum_u64(active ? cost_of(f.e, cfg.cost_mode) : 0ull) : 0ull;
@@ -376,10 +396,10 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
         bak |= 1ull << l;
         __threadfence_block();
       }
-      uint32_t e_out = 0;
       const uint32_t e_in = uni(tmp->e);
-      const bool ok = wave_heavy(tmp, v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, olen,
-                                 (uint8_t)sym, wc, early, E.wcap, cnt, e_out);
+      const uint32_t e_out = chain_heavy(tmp, v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, olen,
+                                         sym, wc, early, E.wcap, ctl.chain_tot);
+      const bool ok = e_out != kInactive;
       wave_lds_sync();
       if (!ok && lane == 0) atomicMin(&ctl.chain_stop, j - 1);
       if (ok) wcost += cost_of(uni(e_out), cfg.cost_mode) - cost_of(e_in, cfg.cost_mode);
@@ -473,14 +493,13 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     if (kFirst) front_store(&E.sv(S, 0).rs[r], f);
     else front_store(&E.L.hot[r], f);
   }
-  const uint32_t s_upd = wave_sum_u32(t_upd) + cnt.updates;
-  const uint32_t s_wout = wave_sum_u32(t_wout) + cnt.w_out;
-  const uint32_t s_cmp = wave_sum_u32(t_cmp) + cnt.compares;
+  const uint32_t s_upd = wave_sum_u32(t_upd);
+  const uint32_t s_wout = wave_sum_u32(t_wout);
+  const uint32_t s_cmp = wave_sum_u32(t_cmp);
   if (lane == 0) {
     atomicAdd((unsigned long long*)&ctl.chain_tot[0], (unsigned long long)s_upd);
     atomicAdd((unsigned long long*)&ctl.chain_tot[1], (unsigned long long)s_wout);
     atomicAdd((unsigned long long*)&ctl.chain_tot[2], (unsigned long long)s_cmp);
-    atomicAdd((unsigned long long*)&ctl.chain_tot[3], (unsigned long long)cnt.edinc);
   }
 }
 

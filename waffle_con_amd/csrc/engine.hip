@@ -136,7 +136,7 @@ struct Lds {
   Sh<ChainOvf>* covf;
   Sh<RState>* ctmp;      // [kWaves]
   Sh<uint16_t>* cnom;    // [K+1][nmax]
-  Sh<uint8_t>* cwin;     // [nmax][64]
+  Sh<uint8_t>* cwin;     // read windows, slot win_slot(r) of kWinStride bytes
   Sh<uint32_t>* cwb;     // [nmax]
   Sh<uint32_t>* cpc;     // [K+1]
   Sh<uint8_t>* cpred;    // [K+2]
@@ -170,7 +170,7 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
     l.cnom = (Sh<uint16_t>*)p;
     p += align16((uint64_t)(K + 1) * nmax * 2);
     l.cwin = p;
-    p += (uint64_t)nmax * 64;
+    p += align16((uint64_t)4 * win_m4(nmax) * kWinStride);
     l.cwb = (Sh<uint32_t>*)p;
     p += align16((uint64_t)nmax * 4);
     l.cpc = (Sh<uint32_t>*)p;

@@ -210,15 +210,23 @@ struct ChainOvf {  // nominations of a read with >= 2 distinct tip symbols
   uint64_t sym, occ;  // bytes in iteration order
   uint32_t split, n;
 };
+// Read windows of the chain walk: 64 bytes of each read in LDS. The walk reads
+// them per step, one read per lane (read r = 4 * lane + wave), so they are laid
+// out for the LDS banks: read r's window is slot (r & 3) * m4 + (r >> 2)
+// (m4 = ceil(nmax / 4)) of kWinStride bytes (17 dwords, odd), which puts the 32
+// lanes of a wave's half on 32 different banks when they read the same offset.
+constexpr uint32_t kWinStride = 68;
+__host__ __device__ inline uint32_t win_m4(uint32_t nmax) { return (nmax + 3) / 4; }
+__host__ __device__ inline uint32_t win_slot(uint32_t r, uint32_t m4) { return (r & 3u) * m4 + (r >> 2); }
 // chain LDS: steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[K+1][nmax] u16 |
-//            win[nmax][64] (read windows) | wb[nmax] u32 | pc[K+1] u32 | pred[K+2] u8
+//            win[4*m4][68 B] (read windows) | wb[nmax] u32 | pc[K+1] u32 | pred[K+2] u8
 __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K) {
   if (K == 0) return 0;
   uint64_t t = align16((uint64_t)(K + 1) * sizeof(ChainStep));
   t += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
   t += (uint64_t)kWaves * 64;
   t += align16((uint64_t)(K + 1) * nmax * 2);
-  t += (uint64_t)nmax * 64;
+  t += align16((uint64_t)4 * win_m4(nmax) * kWinStride);
   t += align16((uint64_t)nmax * 4);
   t += align16((uint64_t)(K + 1) * 4);
   t += align16((uint64_t)(K + 2));
