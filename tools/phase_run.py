@@ -60,7 +60,7 @@ def main():
     if a.workload == "cfg2":
         res, st = batch.consensus(cfg, per_problem=True)
     else:
-        res, st = batch.dual_consensus(cfg)
+        res, st = batch.dual_consensus(cfg, per_problem=True)
     wall = time.perf_counter() - t0
     del os.environ["WC_PHASES"]
     rep = {"loci": a.loci, "kernel_ms": st["kernel_ms"], "wall_s": wall, "updates": st["updates"],
@@ -74,6 +74,18 @@ def main():
     rep["workload"] = a.workload
     if a.workload != "cfg2":
         rep["cycles_per_pop_per_wg"] = round(tot / max(1, st["pops"]), 1)
+        pp = st.get("per_problem")
+        if pp:
+            # is the launch bound by its heaviest locus (all loci run at once)?
+            pops = sorted(p["pops"] for p in pp)
+            rep["pops_min_med_p90_max"] = [pops[0], pops[len(pops) // 2], pops[(9 * len(pops)) // 10], pops[-1]]
+            heavy = max(range(len(pp)), key=lambda i: pp[i]["pops"])
+            one = w.ResidentBatch([loci[heavy]])
+            one.dual_consensus(cfg)
+            _, s1 = one.dual_consensus(cfg)
+            rep["heaviest_alone_kernel_ms"] = s1["kernel_ms"]
+            rep["heaviest_alone_us_per_pop"] = 1000.0 * s1["kernel_ms"] / max(1, pp[heavy]["pops"])
+            rep["heaviest_id"] = heavy
         print(json.dumps(rep, indent=1))
         with open(os.path.join(a.out, "report.json"), "w") as f:
             json.dump(rep, f, indent=1)

@@ -71,7 +71,7 @@ class ResidentBatch:
         finally:
             L.wc_results_free(res)
 
-    def dual_consensus(self, config=None, return_errors=True, context=None):
+    def dual_consensus(self, config=None, return_errors=True, context=None, per_problem=False):
         config = config or CdwfaConfig()
         ctx = context or self.ctx
         L = _lib.lib()
@@ -81,7 +81,7 @@ class ResidentBatch:
         if rc != _lib.WC_OK:
             raise _lib.WaffleConError("wc_batch_dual_consensus failed: " + ctx.last_error(), rc)
         try:
-            return _dual_results(res, self._batch, config, L, return_errors), _stats(res, L)
+            return _dual_results(res, self._batch, config, L, return_errors), _stats(res, L, per_problem)
         finally:
             L.wc_results_free(res)
 

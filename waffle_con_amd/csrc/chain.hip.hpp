@@ -103,7 +103,7 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     E.L.cwb[r] = wb;
   }
   const Gm<uint32_t>* pc = E.trk + (E.lcap + 2);  // PQueueTracker processed counts
-  for (uint32_t j = tid; j <= K; j += kBlock) E.L.cpc[j] = (j >= 1) ? pc[L0 + j] : 0u;
+  for (uint32_t j = tid; j <= K; j += kBlock) E.L.cpc[j] = (j >= 1) ? trk_load(&pc[L0 + j]) : 0u;
   __syncthreads();
   SUB_T1(23, ta);
   SUB_T0(tb);

@@ -35,11 +35,17 @@ namespace WC_ENGINE_NS {
 #ifndef WC_WAVES_PER_EU
 #define WC_WAVES_PER_EU 4
 #endif
+#ifndef WC_DUAL_WAVES_PER_EU
+#define WC_DUAL_WAVES_PER_EU WC_WAVES_PER_EU
+#endif
 
 constexpr int kMaxChild = 64;
+constexpr uint32_t kNCB = 4;  // dual engine: children built together (engine_shared list_entries)
 constexpr uint32_t WC_E_COVERAGE_GAP_CODE = 3;  // include/waffle_con.h
 constexpr uint32_t WC_E_INVARIANT_CODE = 10;  // include/waffle_con.h
 constexpr uint32_t WC_E_LIMIT_CODE = 11;
+// WC_E_LIMIT with the overflow reasons (engine_shared LIM_*) in bits 16+
+__device__ inline uint32_t limit_status(uint32_t why) { return WC_E_LIMIT_CODE | (why << 16); }
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 struct Ctl {
@@ -59,7 +65,6 @@ struct Ctl {
   uint32_t fin[2];
   uint32_t nheavy;
   uint64_t cost_acc;
-  uint32_t some_acc[2];
   uint64_t max_err;
   uint64_t farthest[2], last_constraint[2];
   uint64_t trk_total[2], trk_thr[2];
@@ -86,6 +91,7 @@ struct Ctl {
   uint32_t ch_slot[kMaxChild];
   uint64_t ch_cost[kMaxChild];
   uint32_t ch_len[kMaxChild];
+  uint32_t ch_some[kNCB][2];  // Some(dwfa) counts per side of the children being built
   uint32_t cur_slot;
   uint64_t cnt[S_NSTAT];
 #ifdef WC_PHASE_PROF
@@ -231,6 +237,12 @@ __device__ inline HeapEntry heap_pop(Sh<HeapEntry>* h, Lo<uint32_t>& n) {
 }
 
 // ---- PQueueTracker (pqueue_tracker.rs:10-144), thread 0 only ----
+// The count arrays live in HBM (lcap + 2 entries each). The updates are
+// no-return atomics, so thread 0 never waits on a read-modify-write; the few
+// reads bypass the per-CU L1 (which an atomic does not update).
+__device__ __forceinline__ uint32_t trk_load(const Gm<uint32_t>* p) {
+  return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 struct TrackerRef {
   Gm<uint32_t>* lc;
   Gm<uint32_t>* pc;
@@ -238,21 +250,21 @@ struct TrackerRef {
   Lo<uint64_t>* thr;
   uint64_t cap;
   __device__ void insert(uint32_t v) {
-    lc[v]++;
+    atomicAdd((uint32_t*)&lc[v], 1u);
     if (v >= *thr) (*total)++;
   }
   __device__ void remove(uint32_t v) {
-    lc[v]--;
+    atomicSub((uint32_t*)&lc[v], 1u);
     if (v >= *thr) (*total)--;
   }
   __device__ void increment_threshold() {
-    *total -= lc[*thr];
+    *total -= trk_load(&lc[*thr]);
     (*thr)++;
   }
-  __device__ bool at_capacity(uint32_t v) const { return pc[v] >= cap; }
+  __device__ bool at_capacity(uint32_t v) const { return trk_load(&pc[v]) >= cap; }
   __device__ bool process(uint32_t v) {
-    if (pc[v] >= cap) return false;
-    pc[v]++;
+    if (trk_load(&pc[v]) >= cap) return false;
+    atomicAdd((uint32_t*)&pc[v], 1u);
     return true;
   }
 };
@@ -1095,6 +1107,193 @@ __device__ inline void finish_problem(const EngineArgs& A, Lo<Ctl>& ctl, uint8_t
   __syncthreads();
 }
 
+// ---- DualConsensusDWFA: build every child of the popped node ----
+// (dual_consensus.rs:554-734: per child a clone, activate_dual :957-976, the
+// pushes :915-946, activation :633-639, prune_dwfa :1030-1045 and the
+// priority :1092-1168.) The children of one node are independent: each has
+// its own slot, and the clones copy the parent before the in-place child (the
+// last one) changes it. So each step runs over up to kNCB children in one
+// block-wide pass, and a group of children costs the latency of one.
+__device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, const SlotMeta& tm, bool tdual,
+                                           uint32_t nc) {
+  const int tid = threadIdx.x, lane = lane_id();
+  const DevConfig& cfg = E.cfg;
+  const bool early = cfg.early != 0;
+  const uint32_t n = E.n;
+  for (uint32_t c0 = 0; c0 < nc; c0 += kNCB) {
+    const uint32_t cn = min(kNCB, nc - c0);
+    // slots in the reference's child order: clones first, the last child in place
+    if (tid == 0) {
+      for (uint32_t c = c0; c < c0 + cn; ++c) {
+        uint32_t slot = top;
+        if (c + 1 < nc) {
+          if (ctl.nfree == 0) {
+            ctl.status = ST_RETRY | ST_RETRY_PCAP;
+            break;
+          }
+          slot = E.L.freestack[--ctl.nfree];
+        }
+        ctl.ch_slot[c] = slot;
+        ctl.ch_cost[c] = 0;
+        ctl.ch_some[c - c0][0] = ctl.ch_some[c - c0][1] = 0;
+      }
+      ctl.nheavy = 0;
+    }
+    __syncthreads();
+    if (uni(ctl.status) != ST_OK) return;
+    // clones copy the parent (every side it has)
+    for (uint32_t c = c0; c < c0 + cn; ++c) {
+      const uint32_t slot = uni(ctl.ch_slot[c]);
+      if (slot == top) continue;
+      copy_side<false>(E, top, 0, slot, 0, tm.len[0]);
+      if (tdual) copy_side<false>(E, top, 1, slot, 1, tm.len[1]);
+    }
+    __syncthreads();
+    // activate_dual: side 2 := side 1
+    bool split = false;
+    for (uint32_t c = c0; c < c0 + cn; ++c) {
+      if (uni((uint32_t)ctl.ch_kind[c]) != 2) continue;
+      const uint32_t slot = uni(ctl.ch_slot[c]);
+      copy_side<false>(E, slot, 0, slot, 1, tm.len[0]);
+      split = true;
+    }
+    if (split) __syncthreads();
+    // new symbols, locks, lengths
+    if (tid == 0) {
+      for (uint32_t c = c0; c < c0 + cn; ++c) {
+        const uint32_t slot = ctl.ch_slot[c];
+        const uint32_t kind = ctl.ch_kind[c];
+        SlotMeta m = tm;
+        if (kind == 2) {
+          m.flags |= 1u;
+          m.len[1] = m.len[0];
+          m.nsome[1] = m.nsome[0];
+        }
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+          const int sym = ctl.ch_s[c][sd];
+          if (sym >= 0) {
+            E.sv(slot, sd).con[m.len[sd]] = (uint8_t)sym;
+            m.len[sd]++;
+          } else if (kind == 0) {
+            m.flags |= (sd == 0 ? 2u : 4u);  // lock_sequence
+          }
+        }
+        E.L.meta[slot] = m;
+      }
+    }
+    __syncthreads();
+    PH_MARK(4);
+    // pushes: every (child, side) that appends a symbol, thread per read
+    WaveCounters tc = {0, 0, 0, 0, 0};
+    for (uint32_t q = 0; q < 2 * cn; ++q) {
+      const uint32_t c = c0 + q / 2, sd = q & 1u;
+      const int sym = uni((int32_t)ctl.ch_s[c][sd]);
+      if (sym < 0) continue;
+      const uint32_t slot = uni(ctl.ch_slot[c]);
+      const uint32_t olen = uni(E.L.meta[slot].len[sd]);
+      SideView v = E.sv(slot, sd);
+      for (uint32_t r = tid; r < n; r += kBlock) {
+        const RRaw s = rstate_load(&v.rs[r]);
+        if (rraw_e(s) == kInactive) continue;
+        if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
+          E.L.list[atomicAdd(&ctl.nheavy, 1u)] = q * n + r;
+          continue;
+        }
+        Front f;
+        front_load(s, f);
+        uint32_t cmp = 0;
+        const bool heavy = thread_push(f, GlobalBytes{E.read(r)}, E.rlen(r), olen - 1, (uint8_t)sym, cfg.wildcard,
+                                       early, v.wf + (uint64_t)r * E.wcap, cmp);
+        tc.compares += cmp;
+        front_store(&v.rs[r], f);
+        if (heavy) {
+          E.L.list[atomicAdd(&ctl.nheavy, 1u)] = q * n + r;
+          continue;
+        }
+        tc.updates++;
+        tc.w_out += 2 * f.e + 1;
+      }
+    }
+    flush_thread_counters(ctl, tc);
+    __syncthreads();
+    PH_MARK(5);
+    // the ED-increase loop of every heavy (child, side, read), one wave each
+    const uint32_t nh = uni(ctl.nheavy);
+    WaveCounters cnt = {0, 0, 0, 0, 0};
+    for (uint32_t k = wave_id(); k < nh; k += kWaves) {
+      const uint32_t it = uni(E.L.list[k]);
+      const uint32_t q = it / n, r = it - q * n;
+      const uint32_t c = c0 + q / 2, sd = q & 1u;
+      const uint32_t slot = uni(ctl.ch_slot[c]);
+      SideView v = E.sv(slot, sd);
+      uint32_t e = 0;
+      if (!wave_heavy(&v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
+                      uni(E.L.meta[slot].len[sd]), (uint8_t)uni((int32_t)ctl.ch_s[c][sd]), cfg.wildcard, early,
+                      E.wcap, cnt, e)) {
+        if (lane == 0) atomicOr(&ctl.ovf, 4u);
+      }
+    }
+    flush_counters(ctl, cnt);
+    __syncthreads();
+    PH_MARK(6);
+    // reads whose offset activates at a child's new max length
+    // (dual_consensus.rs:633-639): consensus 1 always, consensus 2 too when dual
+    for (uint32_t c = c0; c < c0 + cn; ++c) {
+      const uint32_t slot = uni(ctl.ch_slot[c]);
+      const uint32_t nl0 = uni(E.L.meta[slot].len[0]), nl1 = uni(E.L.meta[slot].len[1]);
+      if (max(nl0, nl1) > E.P.max_act) continue;
+      activate_side<false>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
+      if (uni(E.L.meta[slot].flags) & 1u) activate_side<false>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
+    }
+    PH_MARK(10);
+    // prune + priority of every child of the group in one pass
+    for (uint32_t c = c0; c < c0 + cn; ++c) {
+      const uint32_t slot = uni(ctl.ch_slot[c]);
+      const bool cdual = (uni(E.L.meta[slot].flags) & 1u) != 0;
+      SideView a = E.sv(slot, 0), b = E.sv(slot, 1);
+      uint64_t cost = 0;
+      uint32_t n0 = 0, n1 = 0;
+      for (uint32_t r = tid; r < n; r += kBlock) {
+        uint32_t e1 = a.rs[r].e, e2 = cdual ? b.rs[r].e : kInactive;
+        if (cdual && e1 != kInactive && e2 != kInactive) {
+          if ((uint64_t)e1 + cfg.dual_max_ed_delta < (uint64_t)e2) {
+            b.rs[r].e = kInactive;
+            e2 = kInactive;
+          } else if ((uint64_t)e2 + cfg.dual_max_ed_delta < (uint64_t)e1) {
+            a.rs[r].e = kInactive;
+            e1 = kInactive;
+          }
+        }
+        uint64_t best = ~0ull;
+        if (e1 != kInactive) best = cost_of(e1, cfg.cost_mode);
+        if (e2 != kInactive && cost_of(e2, cfg.cost_mode) < best) best = cost_of(e2, cfg.cost_mode);
+        if (best != ~0ull) cost += best;
+        n0 += e1 != kInactive;
+        n1 += e2 != kInactive;
+      }
+      if (cost) atomicAdd((unsigned long long*)&ctl.ch_cost[c], (unsigned long long)cost);
+      if (n0) atomicAdd(&ctl.ch_some[c - c0][0], n0);
+      if (n1) atomicAdd(&ctl.ch_some[c - c0][1], n1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;
+      else if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
+      else if (ctl.ovf) ctl.status = limit_status(ctl.ovf);
+      for (uint32_t c = c0; c < c0 + cn; ++c) {
+        auto& m = E.L.meta[ctl.ch_slot[c]];
+        m.nsome[0] = ctl.ch_some[c - c0][0];
+        m.nsome[1] = ctl.ch_some[c - c0][1];
+        ctl.ch_len[c] = max(m.len[0], m.len[1]);
+      }
+    }
+    __syncthreads();
+    PH_MARK(11);
+    if (uni(ctl.status) != ST_OK) return;
+  }
+}
+
 // =====================================================================
 // ConsensusDWFA engine (consensus.rs:139-351)
 // =====================================================================
@@ -1187,7 +1386,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       if (tid == 0) {
         const uint32_t ne = ctl.n_end[0];
         ctl.reached = early ? (ne == E.n) : (ne > 0);  // consensus.rs:516-532
-        if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
+        if (ctl.ovf) ctl.status = limit_status(ctl.ovf);
       }
       __syncthreads();
       if (uni(ctl.status) != ST_OK) break;
@@ -1238,7 +1437,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
             wave_votes(ctl, 0, E.L.rinfo, E.L.rinfo, E.L.rinfo, E.n, false, false, ctl.multi[0] != 0, cfg.wildcard);
         if (lane == 0) {
           if (!ok) {
-            ctl.status = WC_E_LIMIT_CODE;
+            ctl.status = limit_status(LIM_VOTES);
           } else {
             double max_obs = 0.0;
             bool have = false;
@@ -1321,7 +1520,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (tid == 0) {
           if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;
           else if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
-          else if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
+          else if (ctl.ovf) ctl.status = limit_status(ctl.ovf);
           ctl.ch_cost[c] = ctl.cost_acc;
           ctl.ch_slot[c] = slot;
           E.L.meta[slot].len[0] = len + 1;
@@ -1351,7 +1550,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
 // =====================================================================
 // DualConsensusDWFA engine (dual_consensus.rs:240-787)
 // =====================================================================
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
   Lo<Ctl>& ctl = *(Lo<Ctl>*)&ctl_lds;
@@ -1445,7 +1644,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         // reached_consensus_end (dual_consensus.rs:1203-1233); inactive counts as require_all
         ctl.fin[0] = early ? (ctl.n_end[0] == tm.nsome[0]) : (ctl.n_end[0] > 0);
         ctl.fin[1] = !tdual ? 0u : (early ? (ctl.n_end[1] == tm.nsome[1]) : (ctl.n_end[1] > 0));
-        if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
+        if (ctl.ovf) ctl.status = limit_status(ctl.ovf);
       }
       __syncthreads();
       PH_MARK(1);
@@ -1528,11 +1727,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         const uint32_t side = wave_id();
         const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, E.n, weighted, tdual,
                                    ctl.multi[side] != 0, cfg.wildcard);
-        if (!ok && lane == 0) atomicOr(&ctl.ovf, 1u);
+        if (!ok && lane == 0) atomicOr(&ctl.ovf, (uint32_t)LIM_VOTES);
       }
       __syncthreads();
       if (tid == 0) {
-        if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
+        if (ctl.ovf) ctl.status = limit_status(ctl.ovf);
         double thr[2] = {0.0, 0.0};
         uint64_t mc[2] = {0, 0};
         for (uint32_t s = 0; s < (tdual ? 2u : 1u); ++s) {
@@ -1613,7 +1812,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
                 nc++;
               }
         }
-        if (overflow) ctl.status = WC_E_LIMIT_CODE;
+        if (overflow) ctl.status = limit_status(LIM_CHILDREN);
         ctl.nchild = nc;
       }
       __syncthreads();
@@ -1632,103 +1831,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       }
 
       // ---- build every child: clones first, the last child in place ----
-      for (uint32_t c = 0; c < nc; ++c) {
-        if (tid == 0) {
-          uint32_t slot = top;
-          if (c + 1 < nc) {
-            if (ctl.nfree == 0) ctl.status = ST_RETRY | ST_RETRY_PCAP;
-            else slot = E.L.freestack[--ctl.nfree];
-          }
-          ctl.cur_slot = slot;
-          ctl.cost_acc = 0;
-          ctl.some_acc[0] = ctl.some_acc[1] = 0;
-        }
-        __syncthreads();
-        if (uni(ctl.status) != ST_OK) break;
-        const uint32_t slot = uni(ctl.cur_slot);
-        const uint8_t kind = (uint8_t)uni((uint32_t)ctl.ch_kind[c]);
-        const int s0 = uni((int32_t)ctl.ch_s[c][0]), s1 = uni((int32_t)ctl.ch_s[c][1]);
-        if (slot != top) {
-          copy_side<false>(E, top, 0, slot, 0, tlens[0]);
-          if (tdual) copy_side<false>(E, top, 1, slot, 1, tlens[1]);
-          __syncthreads();
-        }
-        PH_MARK(4);
-        // activate_dual (dual_consensus.rs:957-976): side 2 := side 1
-        if (kind == 2) copy_side<false>(E, slot, 0, slot, 1, tlens[0]);
-        if (tid == 0) {
-          SlotMeta m = tm;
-          if (kind == 2) {
-            m.flags |= 1u;
-            m.len[1] = m.len[0];
-            m.nsome[1] = m.nsome[0];
-          }
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const int sym = s == 0 ? s0 : s1;
-            if (sym >= 0) {
-              E.sv(slot, s).con[m.len[s]] = (uint8_t)sym;
-              m.len[s]++;
-            } else if (kind == 0) {
-              m.flags |= (s == 0 ? 2u : 4u);  // lock_sequence
-            }
-          }
-          E.L.meta[slot] = m;
-        }
-        __syncthreads();
-        const uint32_t nl0 = E.L.meta[slot].len[0], nl1 = E.L.meta[slot].len[1];
-        push_sides<false, false>(E, ctl, slot, s0, s1, nl0, nl1, false, nullptr);
-        const bool cdual = (E.L.meta[slot].flags & 1u) != 0;
-        // reads whose offset activates at the new max length (dual_consensus.rs:633-639):
-        // consensus 1 always, consensus 2 too when dual (:866-906)
-        if (max(nl0, nl1) <= E.P.max_act) {
-          activate_side<false>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
-          if (cdual) activate_side<false>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
-        }
-        PH_MARK(10);
-        // prune (dual_consensus.rs:1030-1045) + priority (:1092-1168)
-        {
-          SideView a = E.sv(slot, 0), b = E.sv(slot, 1);
-          uint64_t cost = 0;
-          uint32_t n0 = 0, n1 = 0;
-          for (uint32_t r = tid; r < E.n; r += kBlock) {
-            uint32_t e1 = a.rs[r].e, e2 = cdual ? b.rs[r].e : kInactive;
-            if (cdual && e1 != kInactive && e2 != kInactive) {
-              if ((uint64_t)e1 + cfg.dual_max_ed_delta < (uint64_t)e2) {
-                b.rs[r].e = kInactive;
-                e2 = kInactive;
-              } else if ((uint64_t)e2 + cfg.dual_max_ed_delta < (uint64_t)e1) {
-                a.rs[r].e = kInactive;
-                e1 = kInactive;
-              }
-            }
-            uint64_t best = ~0ull;
-            if (e1 != kInactive) best = cost_of(e1, cfg.cost_mode);
-            if (e2 != kInactive && cost_of(e2, cfg.cost_mode) < best) best = cost_of(e2, cfg.cost_mode);
-            if (best != ~0ull) cost += best;
-            n0 += e1 != kInactive;
-            n1 += e2 != kInactive;
-          }
-          if (cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);
-          if (n0) atomicAdd(&ctl.some_acc[0], n0);
-          if (n1) atomicAdd(&ctl.some_acc[1], n1);
-        }
-        __syncthreads();
-        if (tid == 0) {
-          if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;
-          else if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
-          else if (ctl.ovf) ctl.status = WC_E_LIMIT_CODE;
-          auto& m = E.L.meta[slot];
-          m.nsome[0] = ctl.some_acc[0];
-          m.nsome[1] = ctl.some_acc[1];
-          ctl.ch_cost[c] = ctl.cost_acc;
-          ctl.ch_slot[c] = slot;
-          ctl.ch_len[c] = max(m.len[0], m.len[1]);
-        }
-        __syncthreads();
-        PH_MARK(11);
-        if (uni(ctl.status) != ST_OK) break;
-      }
+      dual_build_children(E, ctl, top, tm, tdual, nc);
       if (uni(ctl.status) != ST_OK) break;
       if (tid == 0) {
         for (uint32_t c = 0; c < nc; ++c) {

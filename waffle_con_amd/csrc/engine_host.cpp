@@ -48,6 +48,8 @@ struct Caps {
   uint64_t wsb = 0, ob = 0;
   bool gstate = false;  // search state in HBM (engine_gstate.hip): it does not fit LDS
   uint64_t gsb = 0;     // its bytes per workgroup
+  uint32_t conc = 0;    // workgroups the HBM share was planned for
+  bool pool_short = false;  // a retried item's node pool did not get its full growth
 };
 
 // Capacities of one launch over items[ids] (SURVEY §8(a) sizes): wavefront row
@@ -96,9 +98,13 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
     pcap *= 2;
   // a retried (pool-exhausted) item gets 4x per retry, as HBM allows; past
   // what LDS holds, the search state moves to HBM
+  c.pool_short = false;
   for (uint32_t k = 0; k < px; ++k) {
     const uint32_t np = pcap * 2;
-    if ((uint64_t)np * sb > std::max<uint64_t>(budget, per_wg)) break;
+    if ((uint64_t)np * sb > std::max<uint64_t>(budget, per_wg)) {
+      c.pool_short = true;
+      break;
+    }
     pcap = np;
   }
   if (lds_bytes(sides, pcap, nmax, chain) > kLdsMax) gstate = true;
@@ -138,6 +144,7 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
     }
     c.act_m = (uint32_t)m;
   }
+  c.conc = (uint32_t)conc;
   c.gstate = gstate;
   c.gsb = align16(lds_bytes(sides, pcap, nmax, chain));
   c.lds = gstate ? 0 : (size_t)c.gsb;
@@ -324,6 +331,11 @@ static uint32_t harvest(const Launch& L, uint32_t k, const SubProb& s, EngineOut
   o.error.clear();
   if (st & ST_RETRY) return st;
   const uint8_t* base = L.out(k);
+  if ((st & 0xFFFFu) == WC_E_LIMIT) {
+    o.status = WC_E_LIMIT;
+    o.error = limit_msg(st >> 16);
+    return WC_E_LIMIT;
+  }
   if (st != ST_OK) {
     o.error = err_msg((int)st);
     if (st == WC_E_COVERAGE_GAP)  // consensus.rs:305 / dual_consensus.rs message
@@ -427,7 +439,7 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
         bump(items[id], st);
         if (items[id].attempts >= kMaxAttempts) {
           out[id].status = WC_E_LIMIT;
-          out[id].error = err_msg(WC_E_LIMIT);
+          out[id].error = retry_msg(st, items[id].attempts);
         } else {
           retry.push_back(id);
         }
@@ -449,7 +461,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   constexpr uint32_t kQcap = 1u << 16;   // published, unfinished problems
   constexpr uint32_t kQslots = 1u << 23; // their read-table entries
   L.caps = caps;
-  L.grid = (uint32_t)std::max(1, caps.per_cu) * (uint32_t)ctx->n_cu;
+  L.grid = std::min<uint32_t>((uint32_t)std::max(1, caps.per_cu) * (uint32_t)ctx->n_cu, std::max(1u, caps.conc));
   L.P = 2 * L.grid;  // two output slots per workgroup
   L.kernel_ms = 0;
   const uint32_t P = L.P;
@@ -854,10 +866,20 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     }
     Launch* L = launch_slot(ctx, 0);
     if (!L) return set_err(ctx, WC_E_HIP, "stream creation failed");
-    std::vector<uint32_t> ids(4 * ctx->n_cu, 0);  // the pool share is planned for a full chip of workgroups
+    // the pool share is planned for a full chip of workgroups; when a retried
+    // item's node pool outgrows that share, the epoch runs fewer workgroups
+    // (halving, down to one per retried item) so that each gets more HBM
+    const size_t nretry = std::count_if(ready.begin(), ready.end(), [&](uint32_t id) { return subs[id].attempts > 0; });
+    size_t conc = 4 * ctx->n_cu;
     Caps caps;
     std::string err;
-    int prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(L->ws.cap, 0.8), caps, err);
+    int prc = WC_OK;
+    for (;;) {
+      std::vector<uint32_t> ids(conc, 0);
+      prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(L->ws.cap, 0.8), caps, err);
+      if (prc != WC_OK || !caps.pool_short || conc <= std::max<size_t>(1, nretry)) break;
+      conc = std::max<size_t>(std::max<size_t>(1, nretry), conc / 2);
+    }
     if (prc != WC_OK) {
       for (uint32_t id : ready) {
         pool[id]->res.reset(new ProbRes());
@@ -884,7 +906,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
           return;
         }
         o.status = WC_E_LIMIT;
-        o.error = err_msg(WC_E_LIMIT);
+        o.error = retry_msg(st, subs[id].attempts);
       }
       w.res.reset(new ProbRes());
       build_dual(o, (uint32_t)subs[id].gid.size(), cfg.consensus_cost, *w.res);

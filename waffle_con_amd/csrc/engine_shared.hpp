@@ -21,6 +21,11 @@ enum : uint32_t {
   ST_RETRY_LCAP = 0x4,       // consensus outgrew lcap
   ST_RETRY_HEAP = 0x8,       // priority queue outgrew pcap
   ST_RETRY_RMAX = 0x10,      // more tied results than result records
+  // WC_E_LIMIT from the engines carries what overflowed in bits 16+:
+  LIM_TIPS = 0x1,       // more than 8 distinct symbols at one read's wavefront tips
+  LIM_OFFSET = 0x2,     // offset activation scratch
+  LIM_VOTES = 0x8,      // more than 14 voted symbols at one node side
+  LIM_CHILDREN = 0x20,  // more than 64 children of one node
 };
 
 enum StatIdx : int {
@@ -233,6 +238,11 @@ __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K) {
   return t;
 }
 
+// work list entries (u32): heavy (side, read) items; the dual engine builds up
+// to 4 children at once (engine.hip kNCB), so 2 sides x 4 children x nmax
+__host__ __device__ inline uint64_t list_entries(uint32_t sides, uint32_t nmax) {
+  return (uint64_t)(sides == 2 ? 8 : 2) * nmax;
+}
 // sides whose expanded node's RStates are held in LDS (single engine only)
 __host__ __device__ inline uint32_t hot_sides(uint32_t sides) { return sides == 1 ? 1u : 0u; }
 // LDS: hot RStates[hot_sides][nmax] | chain area | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
@@ -245,7 +255,7 @@ __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uin
   t += (uint64_t)pcap * sizeof(SlotMeta);
   t += (uint64_t)sides * nmax * sizeof(RInfo);
   t += align16((uint64_t)sides * nmax * 4);
-  t += align16((uint64_t)2 * nmax * 4);
+  t += align16((uint64_t)list_entries(sides, nmax) * 4);
   return align16(t);
 }
 

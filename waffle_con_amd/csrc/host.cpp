@@ -50,6 +50,30 @@ std::string err_msg(int code) {
   }
 }
 
+// WC_E_LIMIT from an engine: what overflowed (engine_shared.hpp LIM_*)
+std::string limit_msg(uint32_t why) {
+  std::string m = "device capacity limit exceeded:";
+  if (why & LIM_TIPS) m += " more than 8 distinct symbols at one read's wavefront tips;";
+  if (why & LIM_VOTES) m += " more than 14 distinct symbols voted at one node side;";
+  if (why & LIM_CHILDREN) m += " more than 64 children of one node;";
+  if (why & LIM_OFFSET) m += " offset activation scratch (offset_window + offset_compare_length);";
+  if (!(why & (LIM_TIPS | LIM_VOTES | LIM_CHILDREN | LIM_OFFSET))) return err_msg(WC_E_LIMIT);
+  m.pop_back();
+  return m;
+}
+
+// a problem still asking for more capacity after the last retry
+std::string retry_msg(uint32_t st, uint32_t attempts) {
+  std::string m = "device capacity limit exceeded: still too small after " + std::to_string(attempts) + " retries:";
+  if (st & ST_RETRY_WCAP) m += " wavefront rows (edit distance);";
+  if (st & ST_RETRY_PCAP) m += " node pool;";
+  if (st & ST_RETRY_HEAP) m += " priority queue;";
+  if (st & ST_RETRY_LCAP) m += " consensus length;";
+  if (st & ST_RETRY_RMAX) m += " result records;";
+  m.pop_back();
+  return m;
+}
+
 int set_err(wc_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return code;

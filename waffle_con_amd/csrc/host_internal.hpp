@@ -144,6 +144,8 @@ struct RawRecord {
 
 namespace wch {
 std::string err_msg(int code);
+std::string limit_msg(uint32_t why);
+std::string retry_msg(uint32_t st, uint32_t attempts);
 int set_err(wc_ctx* ctx, int code, const std::string& msg);
 wc::DevConfig to_dev(const wc_config& c);
 inline uint64_t cost_of_h(uint32_t e, int mode) { return mode == 0 ? (uint64_t)e : (uint64_t)e * (uint64_t)e; }
