@@ -83,9 +83,24 @@ def main():
             one = w.ResidentBatch([loci[heavy]])
             one.dual_consensus(cfg)
             _, s1 = one.dual_consensus(cfg)
+            os.environ["WC_PHASES"] = ph_file
+            _, s1 = one.dual_consensus(cfg)
+            del os.environ["WC_PHASES"]
+            with open(ph_file) as f:
+                c1 = [int(x) for x in f.read().strip().splitlines()[-1].split()[2:]]
+            t1 = sum(c1[k] for k in names if k not in (12, 14)) or 1
             rep["heaviest_alone_kernel_ms"] = s1["kernel_ms"]
             rep["heaviest_alone_us_per_pop"] = 1000.0 * s1["kernel_ms"] / max(1, pp[heavy]["pops"])
+            rep["heaviest_alone_cycles_per_pop"] = round(t1 / max(1, pp[heavy]["pops"]), 1)
+            rep["heaviest_alone_phase_cycles_per_pop"] = {names[k]: round(c1[k] / max(1, pp[heavy]["pops"]), 1)
+                                                          for k in names if c1[k]}
             rep["heaviest_id"] = heavy
+        # dual sub-phase counters (engine.hip dual_build_children; wave 0's view)
+        np_ = max(1, st["pops"])
+        DSUB = {16: "group_items", 17: "wave_items", 18: "row_resumes(w0)", 19: "group_loop_cycles(w0)",
+                20: "wave_loop_cycles(w0)", 21: "children", 28: "votes-insertion-order(w0)", 29: "votes-fx-order(w0)",
+                30: "votes-sums(w0)", 31: "active-min-growth(t0)"}
+        rep["dual_sub_per_pop"] = {DSUB[k]: round(cyc[k] / np_, 2) for k in DSUB if k < len(cyc)}
         print(json.dumps(rep, indent=1))
         with open(os.path.join(a.out, "report.json"), "w") as f:
             json.dump(rep, f, indent=1)

@@ -63,7 +63,7 @@ struct Ctl {
   uint32_t ovf;
   uint32_t reached;
   uint32_t fin[2];
-  uint32_t nheavy;
+  uint32_t nheavy, nwide;
   uint64_t cost_acc;
   uint64_t max_err;
   uint64_t farthest[2], last_constraint[2];
@@ -754,19 +754,29 @@ __device__ inline void hot_fetch(Eng& E, uint32_t slot, uint32_t side) {
 // (the clone's push writes the child's RStates straight into its slot).
 template <bool kSrcHot>
 __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t dst, uint32_t sdst, uint32_t len) {
-  const int tid = threadIdx.x, lane = lane_id();
   SideView a = E.sv(src, ssrc), b = E.sv(dst, sdst);
   const auto ars = node_rs<kSrcHot>(E, src, ssrc);
   copy_bytes(b.con, a.con, len);
-  if (!kSrcHot)
-    for (uint32_t r = tid; r < E.n; r += kBlock) rstate_store(&b.rs[r], rstate_load(&ars[r]));
-  for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
-    const uint32_t e = ars[r].e;
+  // thread per read: its RState, then its wavefront row in 16-byte moves with
+  // eight loads in flight, so the reads' copies overlap instead of queueing
+  // behind one wave per read (rows are 16-byte aligned: wcap % 64 == 0)
+  for (uint32_t r = threadIdx.x; r < E.n; r += kBlock) {
+    const RRaw st = rstate_load(&ars[r]);
+    if (!kSrcHot) rstate_store(&b.rs[r], st);
+    const uint32_t e = rraw_e(st);
     if (e == kInactive) continue;
-    const uint32_t W = 2 * e + 1;
-    const Gm<uint32_t>* wa = a.wf + (uint64_t)r * E.wcap;
-    Gm<uint32_t>* wb = b.wf + (uint64_t)r * E.wcap;
-    for (uint32_t i = lane; i < W; i += 64) wb[i] = wa[i];
+    const uint32_t n4 = (2 * e + 1 + 3) >> 2;
+    const Gm<uint4>* wa = (const Gm<uint4>*)(a.wf + (uint64_t)r * E.wcap);
+    Gm<uint4>* wb = (Gm<uint4>*)(b.wf + (uint64_t)r * E.wcap);
+    for (uint32_t i = 0; i < n4; i += 8) {
+      uint4 t[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k)
+        if (i + k < n4) t[k] = wa[i + k];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k)
+        if (i + k < n4) wb[i + k] = t[k];
+    }
   }
 }
 
@@ -912,8 +922,24 @@ struct SymSet {
 // its f64 vote. Returns false when more than kKout distinct symbols occur.
 template <class Load, class Weight>
 __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, bool weighted, bool multi, int wc,
-                                       uint32_t& m_out, uint32_t& key_out, double& val_out) {
+                                       uint32_t& m_out, uint32_t& key_out, double& val_out,
+                                       Lo<uint64_t>* ph = nullptr) {
   const int lane = lane_id();
+#ifdef WC_PHASE_PROF
+  uint64_t vt = __builtin_amdgcn_s_memtime();
+#define VOTE_T(k)                                              \
+  do {                                                         \
+    if (ph && threadIdx.x == 0) {                              \
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();        \
+      ph[k] += t1 - vt;                                        \
+      vt = t1;                                                 \
+    }                                                          \
+  } while (0)
+#else
+#define VOTE_T(k) \
+  do {            \
+  } while (0)
+#endif
   // 1. outer-map insertion order: first appearance over (read, inner order)
   uint64_t ins_lo = 0, ins_hi = 0;
   uint32_t nk = 0;
@@ -946,6 +972,7 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
       known.add(s);
     }
   }
+  VOTE_T(28);
   // 2. hashbrown iteration order, wildcard removed (consensus.rs:556-561)
   const uint64_t ord = fx_order_packed(nk, ins_at);
   uint64_t k_lo = 0, k_hi = 0;
@@ -959,6 +986,7 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
     m++;
   }
   auto key_at = [&](uint32_t j) { return j < 8 ? byte_at(k_lo, j) : byte_at(k_hi, j - 8); };
+  VOTE_T(29);
   // 3. per-key sums; lane k keeps key k's running sum
   double accv = 0.0;
   if (!weighted && !multi) {
@@ -1019,6 +1047,8 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
       }
     }
   }
+  VOTE_T(30);
+#undef VOTE_T
   m_out = m;
   key_out = (uint32_t)lane < m ? key_at(lane) : 0u;
   val_out = accv;
@@ -1034,7 +1064,13 @@ WC_PHASE_FN bool wave_votes(Lo<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, co
   double val = 0.0;
   const bool ok = wave_votes_core([&](uint32_t r) { return rinfo_load(&ri[r]); },
                                   [&](uint32_t r) { return vote_weight(r0, r1, r, is_dual, side1); }, n, weighted,
-                                  multi, wc, m, key, val);
+                                  multi, wc, m, key, val,
+#ifdef WC_PHASE_PROF
+                                  ctl.ph
+#else
+                                  nullptr
+#endif
+  );
   if (!ok) return false;
   if ((uint32_t)lane < m) {
     ctl.keys[side][lane] = (uint8_t)key;
@@ -1138,6 +1174,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         ctl.ch_some[c - c0][0] = ctl.ch_some[c - c0][1] = 0;
       }
       ctl.nheavy = 0;
+      ctl.nwide = 0;
     }
     __syncthreads();
     if (uni(ctl.status) != ST_OK) return;
@@ -1184,7 +1221,11 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     }
     __syncthreads();
     PH_MARK(4);
-    // pushes: every (child, side) that appends a symbol, thread per read
+    // pushes: every (child, side) that appends a symbol, thread per read.
+    // Reads that need the ED-increase loop go to the group list (rows that fit
+    // kRow16, four reads per wave) or, for wide frontiers and long rows, to
+    // the wave list (filled from the top of E.L.list)
+    const uint32_t lend = (uint32_t)list_entries(2, E.nmax) - 1;
     WaveCounters tc = {0, 0, 0, 0, 0};
     for (uint32_t q = 0; q < 2 * cn; ++q) {
       const uint32_t c = c0 + q / 2, sd = q & 1u;
@@ -1197,7 +1238,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         const RRaw s = rstate_load(&v.rs[r]);
         if (rraw_e(s) == kInactive) continue;
         if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
-          E.L.list[atomicAdd(&ctl.nheavy, 1u)] = q * n + r;
+          E.L.list[lend - atomicAdd(&ctl.nwide, 1u)] = q * n + r;
           continue;
         }
         Front f;
@@ -1208,7 +1249,8 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         tc.compares += cmp;
         front_store(&v.rs[r], f);
         if (heavy) {
-          E.L.list[atomicAdd(&ctl.nheavy, 1u)] = q * n + r;
+          if (2 * f.e + 3 <= kRow16) E.L.list[atomicAdd(&ctl.nheavy, 1u)] = q * n + r;
+          else E.L.list[lend - atomicAdd(&ctl.nwide, 1u)] = q * n + r;
           continue;
         }
         tc.updates++;
@@ -1218,11 +1260,56 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     flush_thread_counters(ctl, tc);
     __syncthreads();
     PH_MARK(5);
-    // the ED-increase loop of every heavy (child, side, read), one wave each
-    const uint32_t nh = uni(ctl.nheavy);
+    // the ED-increase loops: four reads per wave in 16-lane groups ...
+    const uint32_t nh = uni(ctl.nheavy), nw = uni(ctl.nwide);
+    SUB_CNT(16, nh);
+    SUB_CNT(17, nw);
+    SUB_T0(tg);
     WaveCounters cnt = {0, 0, 0, 0, 0};
-    for (uint32_t k = wave_id(); k < nh; k += kWaves) {
-      const uint32_t it = uni(E.L.list[k]);
+    GroupCnt gc = {0, 0, 0, 0};
+    // (up to one item per wave the 64-lane path is quicker: it goes to the wave loop)
+    const uint32_t ng = nh > (uint32_t)kWaves ? nh : 0u;
+    for (uint32_t b0 = wave_id() * 4u; b0 < ng; b0 += kWaves * 4u) {
+      const uint32_t k = b0 + ((uint32_t)lane >> 4);
+      const bool act = k < ng;
+      const uint32_t it = act ? E.L.list[k] : 0u;
+      const uint32_t q = it / n, r = it - q * n;
+      const uint32_t c = c0 + q / 2, sd = q & 1u;
+      const uint32_t slot = ctl.ch_slot[c];
+      SideView v = E.sv(slot, sd);
+      uint32_t e = 0;
+      const uint32_t g = group_edinc(act, &v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
+                                     E.L.meta[slot].len[sd], cfg.wildcard, early, E.wcap, gc, e);
+      if (act && (lane & 15) == 0 && g == kG_WCAP) atomicOr(&ctl.ovf, 4u);
+      // ... a row that outgrew the group finishes with the whole wave
+      uint64_t mem = ballot(act && (lane & 15) == 0 && g == kG_MEM);
+      while (mem) {
+        const int src = __builtin_ctzll(mem);
+        mem &= mem - 1;
+        const uint32_t it2 = (uint32_t)__builtin_amdgcn_readlane((int)it, src);
+        const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)e, src);
+        const uint32_t q2 = it2 / n, r2 = it2 - q2 * n;
+        const uint32_t c2 = c0 + q2 / 2, sd2 = q2 & 1u;
+        SUB_CNT(18, 1);
+        const uint32_t slot2 = uni(ctl.ch_slot[c2]);
+        SideView v2 = E.sv(slot2, sd2);
+        uint32_t eo = 0;
+        if (!wave_edinc_mem(&v2.rs[r2], v2.wf + (uint64_t)r2 * E.wcap, e2, E.read(r2), E.rlen(r2), v2.con,
+                            uni(E.L.meta[slot2].len[sd2]), cfg.wildcard, early, E.wcap, cnt, eo)) {
+          if (lane == 0) atomicOr(&ctl.ovf, 4u);
+        }
+      }
+    }
+    SUB_T1(19, tg);
+    SUB_T0(tw);
+    cnt.edinc += wave_sum_u32(gc.edinc);
+    cnt.updates += wave_sum_u32(gc.updates);
+    cnt.w_out += wave_sum_u32(gc.w_out);
+    cnt.compares += wave_sum_u32(gc.cmp);
+    // ... and wide frontiers / long rows (and a few group items) one read per wave
+    const uint32_t nsolo = nw + (nh - ng);
+    for (uint32_t k = wave_id(); k < nsolo; k += kWaves) {
+      const uint32_t it = uni(k < nw ? E.L.list[lend - k] : E.L.list[k - nw]);
       const uint32_t q = it / n, r = it - q * n;
       const uint32_t c = c0 + q / 2, sd = q & 1u;
       const uint32_t slot = uni(ctl.ch_slot[c]);
@@ -1234,6 +1321,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         if (lane == 0) atomicOr(&ctl.ovf, 4u);
       }
     }
+    SUB_T1(20, tw);
     flush_counters(ctl, cnt);
     __syncthreads();
     PH_MARK(6);
@@ -1247,34 +1335,52 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       if (uni(E.L.meta[slot].flags) & 1u) activate_side<false>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
     }
     PH_MARK(10);
-    // prune + priority of every child of the group in one pass
-    for (uint32_t c = c0; c < c0 + cn; ++c) {
-      const uint32_t slot = uni(ctl.ch_slot[c]);
-      const bool cdual = (uni(E.L.meta[slot].flags) & 1u) != 0;
-      SideView a = E.sv(slot, 0), b = E.sv(slot, 1);
-      uint64_t cost = 0;
-      uint32_t n0 = 0, n1 = 0;
-      for (uint32_t r = tid; r < n; r += kBlock) {
-        uint32_t e1 = a.rs[r].e, e2 = cdual ? b.rs[r].e : kInactive;
-        if (cdual && e1 != kInactive && e2 != kInactive) {
-          if ((uint64_t)e1 + cfg.dual_max_ed_delta < (uint64_t)e2) {
-            b.rs[r].e = kInactive;
-            e2 = kInactive;
-          } else if ((uint64_t)e2 + cfg.dual_max_ed_delta < (uint64_t)e1) {
-            a.rs[r].e = kInactive;
-            e1 = kInactive;
+    // prune + priority of every child of the group in one pass; every
+    // child's edit distances are loaded before any is used
+    uint32_t cslot[kNCB], cdual = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kNCB; ++k) {
+      cslot[k] = k < cn ? uni(ctl.ch_slot[c0 + k]) : 0u;
+      if (k < cn && (uni(E.L.meta[cslot[k]].flags) & 1u)) cdual |= 1u << k;
+    }
+    uint64_t ccost[kNCB] = {0, 0, 0, 0};
+    uint32_t cn0[kNCB] = {0, 0, 0, 0}, cn1[kNCB] = {0, 0, 0, 0};
+    for (uint32_t r = tid; r < n; r += kBlock) {
+      uint32_t e1[kNCB], e2[kNCB];
+#pragma unroll
+      for (uint32_t k = 0; k < kNCB; ++k) {
+        e1[k] = e2[k] = kInactive;
+        if (k < cn) {
+          e1[k] = E.sv(cslot[k], 0).rs[r].e;
+          if (cdual & (1u << k)) e2[k] = E.sv(cslot[k], 1).rs[r].e;
+        }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kNCB; ++k) {
+        if (k >= cn) continue;
+        if ((cdual & (1u << k)) && e1[k] != kInactive && e2[k] != kInactive) {
+          if ((uint64_t)e1[k] + cfg.dual_max_ed_delta < (uint64_t)e2[k]) {
+            E.sv(cslot[k], 1).rs[r].e = kInactive;
+            e2[k] = kInactive;
+          } else if ((uint64_t)e2[k] + cfg.dual_max_ed_delta < (uint64_t)e1[k]) {
+            E.sv(cslot[k], 0).rs[r].e = kInactive;
+            e1[k] = kInactive;
           }
         }
         uint64_t best = ~0ull;
-        if (e1 != kInactive) best = cost_of(e1, cfg.cost_mode);
-        if (e2 != kInactive && cost_of(e2, cfg.cost_mode) < best) best = cost_of(e2, cfg.cost_mode);
-        if (best != ~0ull) cost += best;
-        n0 += e1 != kInactive;
-        n1 += e2 != kInactive;
+        if (e1[k] != kInactive) best = cost_of(e1[k], cfg.cost_mode);
+        if (e2[k] != kInactive && cost_of(e2[k], cfg.cost_mode) < best) best = cost_of(e2[k], cfg.cost_mode);
+        if (best != ~0ull) ccost[k] += best;
+        cn0[k] += e1[k] != kInactive;
+        cn1[k] += e2[k] != kInactive;
       }
-      if (cost) atomicAdd((unsigned long long*)&ctl.ch_cost[c], (unsigned long long)cost);
-      if (n0) atomicAdd(&ctl.ch_some[c - c0][0], n0);
-      if (n1) atomicAdd(&ctl.ch_some[c - c0][1], n1);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kNCB; ++k) {
+      if (k >= cn) continue;
+      if (ccost[k]) atomicAdd((unsigned long long*)&ctl.ch_cost[c0 + k], (unsigned long long)ccost[k]);
+      if (cn0[k]) atomicAdd(&ctl.ch_some[k][0], cn0[k]);
+      if (cn1[k]) atomicAdd(&ctl.ch_some[k][1], cn1[k]);
     }
     __syncthreads();
     if (tid == 0) {
@@ -1706,6 +1812,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       }
 
       // ---- active_min_count growth (dual_consensus.rs:497-513) ----
+      SUB_T0(tam);
       uint32_t nadd = 0;  // reads activating at tlen
       if (tlen <= E.P.max_act && uni(ctl.am_len) == tlen + 1) {
         if (tid == 0) ctl.act_cnt = 0;
@@ -1721,6 +1828,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         E.active_min[tlen + 1] = (uint32_t)max(cfg.min_count, ceil_u64(cfg.min_af * (double)nt));
         ctl.am_len++;
       }
+      SUB_T1(31, tam);
 
       // ---- votes on both sides (waves 0 and 1 in parallel) ----
       if (wave_id() < (tdual ? 2 : 1)) {
@@ -1831,6 +1939,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       }
 
       // ---- build every child: clones first, the last child in place ----
+      SUB_CNT(21, nc);
       dual_build_children(E, ctl, top, tm, tdual, nc);
       if (uni(ctl.status) != ST_OK) break;
       if (tid == 0) {

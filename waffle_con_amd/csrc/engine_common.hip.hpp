@@ -45,23 +45,39 @@ template <class T> using Sh = T;
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
-}
-// Wave64 sum through DPP lane moves (VALU, no LDS round trips): quad swaps,
-// half-row and row mirrors leave every lane with its 16-lane row sum; the four
-// row sums are read into scalar registers. Returns the (uniform) total.
+// Wave64 reductions through DPP lane moves (VALU, no LDS round trips): quad
+// swaps, half-row and row mirrors leave every lane with its 16-lane row
+// result; the four row results are read into scalar registers. Lanes outside
+// exec read as 0 (bound_ctrl), the identity of max and sum.
 template <int kCtrl>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xf, 0xf, true);
 }
+__device__ __forceinline__ uint32_t row_max_u32(uint32_t v) {
+  v = max(v, dpp_u32<0xb1>(v));   // quad_perm [1,0,3,2]
+  v = max(v, dpp_u32<0x4e>(v));   // quad_perm [2,3,0,1]
+  v = max(v, dpp_u32<0x141>(v));  // row_half_mirror
+  v = max(v, dpp_u32<0x140>(v));  // row_mirror
+  return v;
+}
+__device__ __forceinline__ uint32_t row_sum_u32(uint32_t v) {
+  v += dpp_u32<0xb1>(v);
+  v += dpp_u32<0x4e>(v);
+  v += dpp_u32<0x141>(v);
+  v += dpp_u32<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = row_max_u32(v);
+  return max(max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+             max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+}
+// lane i reads lane i-1 (row_ror: within its 16-lane row, wave_ror: of the wave), cyclically
+__device__ __forceinline__ uint32_t row_ror1(uint32_t v) { return dpp_u32<0x121>(v); }
+__device__ __forceinline__ uint32_t row_ror2(uint32_t v) { return dpp_u32<0x122>(v); }
+__device__ __forceinline__ uint32_t wave_ror1(uint32_t v) { return dpp_u32<0x13c>(v); }
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-  v += dpp_u32<0xb1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_u32<0x4e>(v);   // quad_perm [2,3,0,1]
-  v += dpp_u32<0x141>(v);  // row_half_mirror
-  v += dpp_u32<0x140>(v);  // row_mirror
+  v = row_sum_u32(v);
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
          (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
@@ -263,31 +279,23 @@ constexpr int kRegQ = 2;
 // increase_edit_distance on the register row: W -> W + 2,
 // new[j] = max(old[j] (j < W), old[j-1] + 1 (1 <= j <= W), old[j-2] + 1 (2 <= j <= W+1)).
 __device__ __forceinline__ void regs_grow(uint32_t (&v)[kRegQ], uint32_t W) {
-  const int lane = lane_id();
-  uint32_t nv[kRegQ];
+  const uint32_t lane = (uint32_t)lane_id();
+  // descending q: v[q - 1] is still the old row when entry q is rebuilt.
+  // Entry j - 1 is lane - 1 of v[q] (lane 0: lane 63 of v[q - 1]), entry
+  // j - 2 is lane - 2 (lanes 0, 1: lanes 62, 63 of v[q - 1]): one wave
+  // rotation of a per-lane selection of the two registers.
 #pragma unroll
-  for (int q = 0; q < kRegQ; ++q) {
-    const uint32_t j = (uint32_t)lane + 64u * q;
-    uint32_t m1 = (uint32_t)__shfl_up((int)v[q], 1, 64);
-    uint32_t m2 = (uint32_t)__shfl_up((int)v[q], 2, 64);
-    if (q > 0) {
-      const uint32_t p63 = (uint32_t)__builtin_amdgcn_readlane((int)v[q - 1], 63);
-      const uint32_t p62 = (uint32_t)__builtin_amdgcn_readlane((int)v[q - 1], 62);
-      if (lane == 0) {
-        m1 = p63;
-        m2 = p62;
-      } else if (lane == 1) {
-        m2 = p63;
-      }
-    }
+  for (int q = kRegQ - 1; q >= 0; --q) {
+    const uint32_t j = lane + 64u * q;
+    const uint32_t prev = q > 0 ? v[q > 0 ? q - 1 : 0] : 0u;
+    const uint32_t m1 = wave_ror1(lane == 63 ? prev : v[q]);
+    const uint32_t m2 = wave_ror1(wave_ror1(lane >= 62 ? prev : v[q]));
     uint32_t x = 0;
     if (j < W) x = v[q];
     if (j >= 1 && j <= W) x = max(x, m1 + 1);
     if (j >= 2 && j <= W + 1) x = max(x, m2 + 1);
-    nv[q] = x;
+    v[q] = x;
   }
-#pragma unroll
-  for (int q = 0; q < kRegQ; ++q) v[q] = nv[q];
 }
 
 // extend every diagonal of the register row (wave_extend_all semantics)
@@ -871,6 +879,189 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
     __builtin_amdgcn_wave_barrier();
     wave_rebuild(wf, e, off, blen, olen, rsp);
   }
+  e_out = e;
+  return true;
+}
+
+// ---- the ED-increase loop for four reads per wave (16-lane groups) ----
+// A push's ED-increase work (dynamic_wfa.rs:84-91) is a short chain of
+// dependent memory round trips per read (RState, row, the extend's read and
+// consensus bytes), so one read per wave leaves the wave waiting on one chain
+// at a time. Here each 16-lane group of a wave runs its own read's loop, the
+// row held lane-strided (entry 16 q + gl in v[q]) for W <= kRow16, so four
+// reads' chains overlap. Same arithmetic as wave_heavy's register path.
+constexpr int kQ16 = 8;
+constexpr uint32_t kRow16 = 16u * kQ16;
+
+__device__ __forceinline__ uint32_t grp_max(uint32_t v) { return row_max_u32(v); }
+__device__ __forceinline__ uint32_t grp_sum(uint32_t v) { return row_sum_u32(v); }
+
+// Outcome per group: kG_DONE (RState rebuilt), kG_WCAP (wavefront capacity),
+// kG_MEM (the row outgrew kRow16: stored back with e = `e_out`, the loop goes
+// on in wave_edinc_mem). Counters are per lane (wave-sum them).
+constexpr uint32_t kG_DONE = 0, kG_WCAP = 1, kG_MEM = 2, kG_RUN = 3;
+struct GroupCnt {
+  uint32_t edinc, updates, w_out, cmp;
+};
+__device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd,
+                                       uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc, bool early,
+                                       uint32_t wcap, GroupCnt& gc, uint32_t& e_out) {
+  const int lane = lane_id();
+  const uint32_t gl = (uint32_t)lane & 15u, gb = (uint32_t)lane & ~15u;
+  uint32_t e = 0, off = 0;
+  if (act) {
+    e = rsp->e;
+    off = rsp->off;
+  }
+  uint32_t W = 2 * e + 1;
+  uint32_t v[kQ16];
+#pragma unroll
+  for (int q = 0; q < kQ16; ++q) {
+    const uint32_t j = 16u * q + gl;
+    v[q] = (act && j < W) ? wf[j] : 0u;
+  }
+  uint32_t st = act ? kG_RUN : kG_DONE;
+  uint32_t mb = 0, cmp = 0;
+  while (ballot(st == kG_RUN)) {
+    if (st == kG_RUN && W + 2 > wcap) st = kG_WCAP;
+    else if (st == kG_RUN && W + 2 > kRow16) st = kG_MEM;
+    const bool go = st == kG_RUN;  // group-uniform
+    // increase_edit_distance: W -> W + 2 (lane moves run on every lane).
+    // Descending q keeps v[q - 1] old; entries j - 1 and j - 2 are row
+    // rotations of per-lane selections of v[q] and v[q - 1] (row_ror).
+#pragma unroll
+    for (int q = kQ16 - 1; q >= 0; --q) {
+      const uint32_t j = 16u * q + gl;
+      const uint32_t prev = q > 0 ? v[q > 0 ? q - 1 : 0] : 0u;
+      const uint32_t m1 = row_ror1(gl == 15 ? prev : v[q]);
+      const uint32_t m2 = row_ror2(gl >= 14 ? prev : v[q]);
+      uint32_t x = 0;
+      if (j < W) x = v[q];
+      if (j >= 1 && j <= W) x = max(x, m1 + 1);
+      if (j >= 2 && j <= W + 1) x = max(x, m2 + 1);
+      if (go) v[q] = x;
+    }
+    if (go) {
+      W += 2;
+      e += 1;
+      gc.edinc += gl == 0;
+    }
+    // extend every diagonal: the first 8-byte step of every entry is issued
+    // before any is used; runs that go on past it finish in match_run
+    const uint64_t wcb = 0x0101010101010101ull * (uint64_t)(uint8_t)wc;
+    uint64_t xa[kQ16], ya[kQ16];
+#pragma unroll
+    for (int q = 0; q < kQ16; ++q) {
+      const uint32_t j = 16u * q + gl;
+      const uint32_t bo = v[q] + e - j, oo = v[q] + off;
+      xa[q] = ya[q] = 0;
+      if (go && j < W && bo < blen && oo < olen) {
+        xa[q] = load8(rd, bo);
+        ya[q] = load8(con, oo);
+      }
+    }
+    uint32_t lmo = 0, lmb = 0;
+#pragma unroll
+    for (int q = 0; q < kQ16; ++q) {
+      const uint32_t j = 16u * q + gl;
+      if (!(go && j < W)) continue;
+      uint32_t d = v[q];
+      const uint32_t bo = d + e - j, oo = d + off;
+      if (bo < blen && oo < olen) {
+        const uint32_t rem = min(blen - bo, olen - oo);
+        uint64_t mm = nz_bytes(xa[q] ^ ya[q]);
+        if (wc >= 0) mm &= nz_bytes(xa[q] ^ wcb);
+        const uint32_t k = mm ? (uint32_t)__builtin_ctzll(mm) >> 3 : 8u;
+        if (k >= rem) {
+          d += rem;
+          cmp += rem;
+        } else if (k < 8) {
+          d += k;
+          cmp += k + 1;
+        } else {
+          cmp += 8;
+          d += 8 + match_run(rd, blen, con, olen, bo + 8, oo + 8, wc, cmp);
+        }
+      }
+      v[q] = d;
+      lmo = max(lmo, d);
+      lmb = max(lmb, d + e - j);
+    }
+    lmo = grp_max(lmo);
+    lmb = grp_max(lmb);
+    if (go) {
+      mb = lmb;
+      if (!(lmo + off < olen && !(early && lmb == blen))) st = kG_DONE;
+    }
+  }
+  gc.cmp += cmp;
+  e_out = e;
+  if (!act || st == kG_WCAP) return st;
+  // the row back to memory
+#pragma unroll
+  for (int q = 0; q < kQ16; ++q) {
+    const uint32_t j = 16u * q + gl;
+    if (j < W) wf[j] = v[q];
+  }
+  if (st == kG_MEM) return st;
+  gc.updates += gl == 0;
+  gc.w_out += gl == 0 ? W : 0u;
+  // RState from the register row (regs_rebuild semantics, group-wide)
+  uint32_t nf = 0, mbx = 0, nsc = 0;
+#pragma unroll
+  for (int q = 0; q < kQ16; ++q) {
+    const uint32_t j = 16u * q + gl;
+    const bool valid = j < W;
+    const uint32_t d = v[q];
+    const uint32_t bo = d + e - j;
+    const bool inF = valid && d + off >= olen;
+    const uint32_t m = (uint32_t)(ballot(inF) >> gb) & 0xFFFFu;
+    const uint32_t pos = nf + (uint32_t)__popc(m & ((1u << gl) - 1u));
+    if (inF && pos < (uint32_t)kF) {
+      rsp->fi[pos] = (uint16_t)j;
+      rsp->fd[pos] = d;
+    }
+    nf += (uint32_t)__popc(m);
+    if (valid && !inF) {
+      mbx = max(mbx, bo);
+      nsc += bo < blen;
+    }
+  }
+  (void)mb;
+  mbx = grp_max(mbx);
+  nsc = grp_sum(nsc);
+  if (gl == 0) {
+    rsp->e = e;
+    rsp->maxb = mbx;
+    rsp->nscmp = (uint16_t)min(nsc, 65535u);
+    rsp->nf = (uint8_t)min(nf, (uint32_t)kF);
+    rsp->flags = (nf > (uint32_t)kF || nsc > 65535u) ? kWide : 0;
+  }
+  return kG_DONE;
+}
+
+// Continue an ED-increase loop whose row (W = 2 e + 1 entries, post-extend, not
+// yet done) is in memory: one wave, lanes over diagonals (wave_heavy's memory
+// path). Returns false on wavefront capacity overflow.
+template <class P>
+__device__ inline bool wave_edinc_mem(P rsp, Gm<uint32_t>* wf, uint32_t e, const Gm<uint8_t>* rd, uint32_t blen,
+                                      const Gm<uint8_t>* con, uint32_t olen, int wc, bool early, uint32_t wcap,
+                                      WaveCounters& cnt, uint32_t& e_out) {
+  const uint32_t off = rsp->off;
+  uint32_t W = 2 * e + 1, mo, mb, cmp = 0;
+  do {
+    if (W + 2 > wcap) return false;
+    wave_grow(wf, W);
+    W += 2;
+    e += 1;
+    wave_extend_all(wf, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
+    cnt.edinc++;
+  } while (mo + off < olen && !(early && mb == blen));
+  cnt.updates++;
+  cnt.w_out += W;
+  cnt.compares += wave_sum_u32(cmp);
+  __builtin_amdgcn_wave_barrier();
+  wave_rebuild(wf, e, off, blen, olen, rsp);
   e_out = e;
   return true;
 }
