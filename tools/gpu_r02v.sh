@@ -1,0 +1,11 @@
+set -o pipefail
+O=gpurun_out/r02v
+mkdir -p $O
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread -k "not cfg4_full" > $O/tests.log 2>&1
+echo "tests rc=$?"
+tail -2 $O/tests.log
+timeout -k 10 200 python -u bench.py --workload cfg3 --loci 768 --steps 1 --warmup 1 --no-cpu --no-e2e > $O/cfg3.json 2> $O/cfg3.err || { echo "cfg3 failed"; exit 1; }
+python -c "import json; d=json.load(open('$O/cfg3.json')); print('cfg3 loci/s', d['loci_per_s'], 'kernel ms', d['kernel_ms_per_step'])"
+timeout -k 10 300 python -u tools/priority_bench.py --loci 1024 --cpu-loci 4 > $O/prio.json 2> $O/prio.err || { echo "prio failed"; exit 1; }
+cat $O/prio.json
+WAFFLE_CON_LIB=$PWD/waffle_con_amd/libwaffle_con_prof.so timeout -k 10 200 python -u tools/phase_run.py --workload cfg3 --loci 768 --out $O/ph_cfg3 > $O/ph_cfg3.log 2>&1; echo "ph cfg3 rc=$?"

@@ -99,7 +99,8 @@ def main():
         np_ = max(1, st["pops"])
         DSUB = {16: "group_items", 17: "wave_items", 18: "row_resumes(w0)", 19: "group_loop_cycles(w0)",
                 20: "wave_loop_cycles(w0)", 21: "children", 28: "votes-insertion-order(w0)", 29: "votes-fx-order(w0)",
-                30: "votes-sums(w0)", 31: "active-min-growth(t0)"}
+                30: "votes-sums(w0)", 31: "active-min-growth(t0)", 22: "prune-setup(t0)", 23: "prune-loop(t0)",
+                24: "prune-atomics(t0)", 25: "prune-barrier1(t0)", 26: "prune-tail(t0)"}
         rep["dual_sub_per_pop"] = {DSUB[k]: round(cyc[k] / np_, 2) for k in DSUB if k < len(cyc)}
         print(json.dumps(rep, indent=1))
         with open(os.path.join(a.out, "report.json"), "w") as f:

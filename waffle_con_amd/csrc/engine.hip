@@ -81,6 +81,7 @@ struct Ctl {
   uint32_t nkeys[2];
   uint8_t keys[2][kKout];
   double vals[2][kKout];
+  uint64_t fxc[2][3];  // per side: the last votes' insertion-ordered keys (lo, hi | nk << 56) and their fx order
   // thread-0 scratch for child enumeration (kept in LDS, not private memory)
   int16_t opt[2][kKout + 1];
   double srt_v[kKout];
@@ -261,12 +262,10 @@ struct TrackerRef {
     *total -= trk_load(&lc[*thr]);
     (*thr)++;
   }
-  __device__ bool at_capacity(uint32_t v) const { return trk_load(&pc[v]) >= cap; }
-  __device__ bool process(uint32_t v) {
-    if (trk_load(&pc[v]) >= cap) return false;
-    atomicAdd((uint32_t*)&pc[v], 1u);
-    return true;
-  }
+  __device__ uint32_t processed(uint32_t v) const { return trk_load(&pc[v]); }
+  // process() of a length whose processed() count is below capacity (the pop
+  // just checked it; only this workgroup's thread 0 touches the tracker)
+  __device__ void process_unchecked(uint32_t v) { atomicAdd((uint32_t*)&pc[v], 1u); }
 };
 
 __device__ inline uint64_t ceil_u64(double x) {
@@ -276,14 +275,47 @@ __device__ inline uint64_t ceil_u64(double x) {
   return (uint64_t)c;
 }
 
+template <int kCtrl>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = dpp_u32<kCtrl>((uint32_t)v), hi = dpp_u32<kCtrl>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+// (uniform) wave sum of u64 values: DPP row sums, four scalar reads
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  v += dpp_u64<0xb1>(v);
+  v += dpp_u64<0x4e>(v);
+  v += dpp_u64<0x141>(v);
+  v += dpp_u64<0x140>(v);
+  uint64_t t = 0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
-    uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
-    v += ((uint64_t)hi << 32) | lo;
-  }
-  return v;
+  for (int l = 0; l < 64; l += 16)
+    t += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  return t;
+}
+
+// ---- wave-aggregated LDS updates (call with the whole wave converged) ----
+// Same-address LDS atomics from many lanes serialize lane by lane; here one
+// lane adds the wave's total.
+__device__ __forceinline__ void agg_add(Lo<uint32_t>* p, uint32_t v) {
+  const uint32_t t = wave_sum_u32(v);
+  if (lane_id() == 0 && t) atomicAdd((uint32_t*)p, t);
+}
+__device__ __forceinline__ void agg_add64(Lo<uint64_t>* p, uint64_t v) {
+  const uint64_t t = wave_sum_u64(v);
+  if (lane_id() == 0 && t) atomicAdd((unsigned long long*)p, (unsigned long long)t);
+}
+__device__ __forceinline__ void agg_or(Lo<uint32_t>* p, bool cond, uint32_t bits) {
+  if (ballot(cond) && lane_id() == 0) atomicOr((uint32_t*)p, bits);
+}
+// a slot of the list counted by `counter` for every lane with `take`
+__device__ __forceinline__ uint32_t agg_append(Lo<uint32_t>* counter, bool take) {
+  const uint64_t m = ballot(take);
+  if (!m) return 0;
+  uint32_t base = 0;
+  if (lane_id() == 0) base = atomicAdd((uint32_t*)counter, (uint32_t)__popcll((unsigned long long)m));
+  base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+  return base + (uint32_t)__popcll((unsigned long long)(m & ((1ull << lane_id()) - 1ull)));
 }
 
 // wave-uniform counters (lane 0 holds them)
@@ -514,6 +546,7 @@ __device__ inline void init_problem(Eng& E, Lo<Ctl>& ctl) {
     ctl.cache_slot = kNoSlot;
     ctl.hot_slot = kNoSlot;
     ctl.hot_load = 0;
+    ctl.fxc[0][1] = ctl.fxc[1][1] = ~0ull;  // no cached fx order (nk <= 14)
     for (int s = 0; s < S_NSTAT; ++s) ctl.cnt[s] = 0;
 #ifdef WC_PHASE_PROF
     for (int k = 0; k < kPhases; ++k) ctl.ph[k] = 0;
@@ -557,48 +590,74 @@ __device__ __forceinline__ auto node_rs(Eng& E, uint32_t slot, uint32_t side) {
   else return E.sv(slot, side).rs;
 }
 
+// ---- ANALYZE the nominations of every read on up to two sides of one node ----
+// Work items are (side, read): thread step from the RState frontier, the
+// wave path for wide frontiers. ctl.nheavy must be 0 on entry.
 template <bool kHot>
-WC_PHASE_FN void analyze_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t side, uint32_t len, Sh<RInfo>* out) {
+WC_PHASE_FN void analyze_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t nsides, uint32_t len0, uint32_t len1,
+                               Sh<RInfo>* out0, Sh<RInfo>* out1) {
   const int tid = threadIdx.x, lane = lane_id();
-  SideView v = E.sv(slot, side);
-  const auto rs = node_rs<kHot>(E, slot, side);
-  if (tid == 0) ctl.nheavy = 0;
-  __syncthreads();
-  uint32_t ends = 0, multi = 0;
-  for (uint32_t r = tid; r < E.n; r += kBlock) {
-    const RRaw s = rstate_load(&rs[r]);
-    if (rraw_e(s) == kInactive) {
-      out[r].e = kInactive;
-      out[r].n = 0;
-      out[r].end = 0;
-      continue;
+  const uint32_t n = E.n, items = nsides * n;
+  uint32_t ends0 = 0, ends1 = 0;
+  bool multi0 = false, multi1 = false;
+  for (uint32_t base = 0; base < items; base += kBlock) {
+    const uint32_t it = base + tid;
+    bool wide = false;
+    if (it < items) {
+      const uint32_t side = it >= n ? 1u : 0u, r = it - side * n;
+      Sh<RInfo>* out = (side ? out1 : out0) + r;
+      const RRaw s = rstate_load(&node_rs<kHot>(E, slot, side)[r]);
+      if (rraw_e(s) == kInactive) {
+        out->e = kInactive;
+        out->n = 0;
+        out->end = 0;
+      } else if (rraw_flags(s) & kWide) {
+        wide = true;
+      } else {
+        Front f;
+        front_load(s, f);
+        bool m;
+        thread_analyze(f, E.read(r), E.rlen(r), side ? len1 : len0, out, m);
+        if (side) {
+          ends1 += out->end;
+          multi1 |= m;
+        } else {
+          ends0 += out->end;
+          multi0 |= m;
+        }
+      }
     }
-    if (rraw_flags(s) & kWide) {
-      E.L.list[atomicAdd(&ctl.nheavy, 1u)] = r;
-      continue;
-    }
-    Front f;
-    front_load(s, f);
-    bool m;
-    thread_analyze(f, E.read(r), E.rlen(r), len, &out[r], m);
-    ends += out[r].end;
-    multi |= m;
+    const uint32_t k = agg_append(&ctl.nheavy, wide);
+    if (wide) E.L.list[k] = it;
   }
-  if (ends) atomicAdd(&ctl.n_end[side], ends);
-  if (multi) atomicOr(&ctl.multi[side], 1u);
+  agg_add(&ctl.n_end[0], ends0);
+  agg_add(&ctl.n_end[1], ends1);
+  agg_or(&ctl.multi[0], multi0, 1u);
+  agg_or(&ctl.multi[1], multi1, 1u);
   __syncthreads();
   const uint32_t nh = uni(ctl.nheavy);
   for (uint32_t k = wave_id(); k < nh; k += kWaves) {
-    const uint32_t r = E.L.list[k];
+    const uint32_t it = uni(E.L.list[k]);
+    const uint32_t side = it >= n ? 1u : 0u, r = it - side * n;
+    Sh<RInfo>* out = (side ? out1 : out0) + r;
+    const auto rs = node_rs<kHot>(E, slot, side);
     const uint32_t e = rs[r].e, off = rs[r].off;
-    const bool ok = wave_analyze_read(v.wf + (uint64_t)r * E.wcap, e, off, E.read(r), E.rlen(r), len, &out[r]);
+    const bool ok = wave_analyze_read(E.sv(slot, side).wf + (uint64_t)r * E.wcap, e, off, E.read(r), E.rlen(r),
+                                      side ? len1 : len0, out);
     if (lane == 0) {
       if (!ok) atomicOr(&ctl.ovf, 1u);
-      if (out[r].end) atomicAdd(&ctl.n_end[side], 1u);
-      if (out[r].n > 1) atomicOr(&ctl.multi[side], 1u);
+      if (out->end) atomicAdd(&ctl.n_end[side], 1u);
+      if (out->n > 1) atomicOr(&ctl.multi[side], 1u);
     }
   }
   __syncthreads();
+}
+// side 0 only (the single engine)
+template <bool kHot>
+WC_PHASE_FN void analyze_side0(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t len, Sh<RInfo>* out) {
+  if (threadIdx.x == 0) ctl.nheavy = 0;
+  __syncthreads();
+  analyze_sides<kHot>(E, ctl, slot, 1, len, 0, out, out);
 }
 
 // ---- FINALIZE one side on scratch (the node is not modified) ----
@@ -647,8 +706,12 @@ WC_PHASE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1,
   // work items over the pushed sides only: (side, read) with side >= first
   const uint32_t first = s0 >= 0 ? 0u : 1u;
   const uint32_t items = ((s0 >= 0 ? 1u : 0u) + (s1 >= 0 ? 1u : 0u)) * E.n;
-  for (uint32_t it = tid; it < items; it += kBlock) {
+  for (uint32_t base = 0; base < items; base += kBlock) {
+    const uint32_t it = base + tid;
     const uint32_t hi = it >= E.n ? 1u : 0u, r = it - hi * E.n, side = first + hi;
+    bool heavy_item = false;
+    do {
+    if (it >= items) break;
     const int sym = side == 0 ? s0 : s1;
     SideView v = E.sv(slot, side);
     const auto dst = node_rs<kDstHot>(E, slot, side);
@@ -661,15 +724,15 @@ WC_PHASE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1,
         out->n = 0;
         out->end = 0;
       }
-      continue;
+      break;
     }
     const uint32_t olen = side == 0 ? len0 : len1;
     const Gm<uint8_t>* rd = E.read(r);
     const uint32_t blen = E.rlen(r);
     if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
       if (kSrcHot != kDstHot) rstate_store(&dst[r], s);
-      E.L.list[atomicAdd(&ctl.nheavy, 1u)] = side * E.n + r;
-      continue;
+      heavy_item = true;
+      break;
     }
     Front f;
     front_load(s, f);
@@ -679,8 +742,8 @@ WC_PHASE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1,
     tc.compares += cmp;
     front_store(&dst[r], f);
     if (heavy) {
-      E.L.list[atomicAdd(&ctl.nheavy, 1u)] = side * E.n + r;
-      continue;
+      heavy_item = true;
+      break;
     }
     tc.updates++;
     tc.w_out += 2 * f.e + 1;
@@ -691,13 +754,16 @@ WC_PHASE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1,
       ends += out->end;
       multi |= m;
     }
+    } while (0);
+    const uint32_t k = agg_append(&ctl.nheavy, heavy_item);
+    if (heavy_item) E.L.list[k] = side * E.n + r;
   }
 
   flush_thread_counters(ctl, tc);
 
-  if (ends) atomicAdd(&ctl.n_end[0], ends);
-  if (multi) atomicOr(&ctl.multi[0], 1u);
-  if (want_cost && cost) atomicAdd((unsigned long long*)&ctl.cost_acc, (unsigned long long)cost);
+  agg_add(&ctl.n_end[0], ends);
+  agg_or(&ctl.multi[0], multi != 0, 1u);
+  if (want_cost) agg_add64(&ctl.cost_acc, cost);
   __syncthreads();
   PH_MARK(5);
   const uint32_t nh = uni(ctl.nheavy);
@@ -923,7 +989,7 @@ struct SymSet {
 template <class Load, class Weight>
 __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, bool weighted, bool multi, int wc,
                                        uint32_t& m_out, uint32_t& key_out, double& val_out,
-                                       Lo<uint64_t>* ph = nullptr) {
+                                       Lo<uint64_t>* ph = nullptr, Lo<uint64_t>* fxc = nullptr) {
   const int lane = lane_id();
 #ifdef WC_PHASE_PROF
   uint64_t vt = __builtin_amdgcn_s_memtime();
@@ -973,8 +1039,21 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
     }
   }
   VOTE_T(28);
-  // 2. hashbrown iteration order, wildcard removed (consensus.rs:556-561)
-  const uint64_t ord = fx_order_packed(nk, ins_at);
+  // 2. hashbrown iteration order, wildcard removed (consensus.rs:556-561);
+  // consecutive pops mostly see the same keys in the same insertion order,
+  // so the last order is kept (fxc) and reused on a match
+  uint64_t ord;
+  const uint64_t tag = ins_hi | ((uint64_t)nk << 56);
+  if (fxc && fxc[0] == ins_lo && fxc[1] == tag) {
+    ord = fxc[2];
+  } else {
+    ord = fx_order_packed(nk, ins_at);
+    if (fxc && lane == 0) {
+      fxc[0] = ins_lo;
+      fxc[1] = tag;
+      fxc[2] = ord;
+    }
+  }
   uint64_t k_lo = 0, k_hi = 0;
   uint32_t m = 0;
   const bool drop_wc = wc >= 0 && nk > 1;
@@ -989,24 +1068,52 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
   VOTE_T(29);
   // 3. per-key sums; lane k keeps key k's running sum
   double accv = 0.0;
-  if (!weighted && !multi) {
-    // every voter has exactly one distinct symbol: each contribution is exactly
-    // 1.0, so the ordered f64 sum is an exact integer count
-    uint32_t c = 0;
-    for (uint32_t base = 0; base < n; base += 64) {
+  // Unweighted votes: a read adds occ/split (tips) to each of its symbols. A
+  // single-symbol read adds exactly 1.0; a read with split in {1, 2, 4, 8}
+  // adds multiples of 1/8. All partial sums of such terms are exact in f64
+  // (< 2^50), so the sum in read order is the exact sum: a count of eighths,
+  // here ballot counts for single-symbol reads plus a serial pass over the
+  // (few) multi-symbol reads. Any other split (3, 5, 6, 7 or more than 8
+  // tips) can round, and then every key takes the ordered fold below.
+  bool fold = weighted;
+  if (!weighted) {
+    uint32_t c8 = 0;
+    for (uint32_t base = 0; base < n && !fold; base += 64) {
       const uint32_t r = base + lane;
-      uint32_t s = 0xFFFF;
-      if (r < n) {
-        const RInfoReg x = load(r);
-        if (x.e != kInactive && x.n == 1) s = byte_at(x.sym, 0);
-      }
+      RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
+      if (r < n) x = load(r);
+      const bool voter = x.e != kInactive;
+      const uint32_t s0 = voter && x.n == 1 ? byte_at(x.sym, 0) : 0x100u;
       for (uint32_t k = 0; k < m; ++k) {
-        const uint32_t pc = (uint32_t)__popcll((unsigned long long)ballot(s == key_at(k)));
-        if (k == (uint32_t)lane) c += pc;
+        const uint32_t cnt = (uint32_t)__popcll((unsigned long long)ballot(s0 == key_at(k)));
+        if ((uint32_t)lane == k) c8 += 8u * cnt;
+      }
+      uint64_t mm = ballot(voter && x.n >= 2);
+      while (mm) {
+        const int l = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        const uint32_t xn = (uint32_t)__builtin_amdgcn_readlane((int)x.n, l);
+        const uint32_t split = (uint32_t)__builtin_amdgcn_readlane((int)x.split, l);
+        if (split > 8u || (split & (split - 1u))) {
+          fold = true;
+          break;
+        }
+        const uint64_t sym = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x.sym >> 32), l) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x.sym, l);
+        const uint4 occ = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)x.occ.x, l),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)x.occ.y, l),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)x.occ.z, l),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)x.occ.w, l));
+        for (uint32_t jj = 0; jj < xn; ++jj) {
+          const uint32_t sj = byte_at(sym, jj);
+          for (uint32_t k = 0; k < m; ++k)  // the dropped wildcard matches no key
+            if (key_at(k) == sj && (uint32_t)lane == k) c8 += occ_at(occ, jj) * (8u / split);
+        }
       }
     }
-    accv = (double)c;
-  } else {
+    if (!fold) accv = (double)c8 * 0.125;
+  }
+  if (fold) {
     // contributions computed lane-parallel (one read per lane), then folded
     // strictly in read order (the reference's f64 summation order); a read
     // without the key adds nothing (x + 0.0 == x, so skipping it is exact)
@@ -1066,11 +1173,11 @@ WC_PHASE_FN bool wave_votes(Lo<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, co
                                   [&](uint32_t r) { return vote_weight(r0, r1, r, is_dual, side1); }, n, weighted,
                                   multi, wc, m, key, val,
 #ifdef WC_PHASE_PROF
-                                  ctl.ph
+                                  ctl.ph,
 #else
-                                  nullptr
+                                  nullptr,
 #endif
-  );
+                                  ctl.fxc[side]);
   if (!ok) return false;
   if ((uint32_t)lane < m) {
     ctl.keys[side][lane] = (uint8_t)key;
@@ -1158,7 +1265,9 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
   const uint32_t n = E.n;
   for (uint32_t c0 = 0; c0 < nc; c0 += kNCB) {
     const uint32_t cn = min(kNCB, nc - c0);
-    // slots in the reference's child order: clones first, the last child in place
+    // slots in the reference's child order (clones first, the last child in
+    // place), then every child's new symbols, locks and lengths: the new
+    // consensus bytes sit past the copied prefix, so they go in before the copies
     if (tid == 0) {
       for (uint32_t c = c0; c < c0 + cn; ++c) {
         uint32_t slot = top;
@@ -1172,36 +1281,9 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         ctl.ch_slot[c] = slot;
         ctl.ch_cost[c] = 0;
         ctl.ch_some[c - c0][0] = ctl.ch_some[c - c0][1] = 0;
-      }
-      ctl.nheavy = 0;
-      ctl.nwide = 0;
-    }
-    __syncthreads();
-    if (uni(ctl.status) != ST_OK) return;
-    // clones copy the parent (every side it has)
-    for (uint32_t c = c0; c < c0 + cn; ++c) {
-      const uint32_t slot = uni(ctl.ch_slot[c]);
-      if (slot == top) continue;
-      copy_side<false>(E, top, 0, slot, 0, tm.len[0]);
-      if (tdual) copy_side<false>(E, top, 1, slot, 1, tm.len[1]);
-    }
-    __syncthreads();
-    // activate_dual: side 2 := side 1
-    bool split = false;
-    for (uint32_t c = c0; c < c0 + cn; ++c) {
-      if (uni((uint32_t)ctl.ch_kind[c]) != 2) continue;
-      const uint32_t slot = uni(ctl.ch_slot[c]);
-      copy_side<false>(E, slot, 0, slot, 1, tm.len[0]);
-      split = true;
-    }
-    if (split) __syncthreads();
-    // new symbols, locks, lengths
-    if (tid == 0) {
-      for (uint32_t c = c0; c < c0 + cn; ++c) {
-        const uint32_t slot = ctl.ch_slot[c];
         const uint32_t kind = ctl.ch_kind[c];
         SlotMeta m = tm;
-        if (kind == 2) {
+        if (kind == 2) {  // activate_dual
           m.flags |= 1u;
           m.len[1] = m.len[0];
           m.nsome[1] = m.nsome[0];
@@ -1218,6 +1300,21 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         }
         E.L.meta[slot] = m;
       }
+      ctl.nheavy = 0;
+      ctl.nwide = 0;
+    }
+    __syncthreads();
+    if (uni(ctl.status) != ST_OK) return;
+    // clones copy the parent (every side it has); activate_dual copies side 1
+    // into side 2, straight from the parent (a split child's parent is single,
+    // so the in-place child's side 2 is not read by any clone)
+    for (uint32_t c = c0; c < c0 + cn; ++c) {
+      const uint32_t slot = uni(ctl.ch_slot[c]);
+      if (slot != top) {
+        copy_side<false>(E, top, 0, slot, 0, tm.len[0]);
+        if (tdual) copy_side<false>(E, top, 1, slot, 1, tm.len[1]);
+      }
+      if (uni((uint32_t)ctl.ch_kind[c]) == 2) copy_side<false>(E, top, 0, slot, 1, tm.len[0]);
     }
     __syncthreads();
     PH_MARK(4);
@@ -1234,27 +1331,35 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t slot = uni(ctl.ch_slot[c]);
       const uint32_t olen = uni(E.L.meta[slot].len[sd]);
       SideView v = E.sv(slot, sd);
-      for (uint32_t r = tid; r < n; r += kBlock) {
-        const RRaw s = rstate_load(&v.rs[r]);
-        if (rraw_e(s) == kInactive) continue;
-        if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
-          E.L.list[lend - atomicAdd(&ctl.nwide, 1u)] = q * n + r;
-          continue;
+      for (uint32_t base = 0; base < n; base += kBlock) {
+        const uint32_t r = base + tid;
+        uint32_t kind = 0;  // 1: group list, 2: wave list
+        if (r < n) {
+          const RRaw s = rstate_load(&v.rs[r]);
+          if (rraw_e(s) != kInactive) {
+            if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
+              kind = 2;
+            } else {
+              Front f;
+              front_load(s, f);
+              uint32_t cmp = 0;
+              const bool heavy = thread_push(f, GlobalBytes{E.read(r)}, E.rlen(r), olen - 1, (uint8_t)sym,
+                                             cfg.wildcard, early, v.wf + (uint64_t)r * E.wcap, cmp);
+              tc.compares += cmp;
+              front_store(&v.rs[r], f);
+              if (heavy) {
+                kind = 2 * f.e + 3 <= kRow16 ? 1u : 2u;
+              } else {
+                tc.updates++;
+                tc.w_out += 2 * f.e + 1;
+              }
+            }
+          }
         }
-        Front f;
-        front_load(s, f);
-        uint32_t cmp = 0;
-        const bool heavy = thread_push(f, GlobalBytes{E.read(r)}, E.rlen(r), olen - 1, (uint8_t)sym, cfg.wildcard,
-                                       early, v.wf + (uint64_t)r * E.wcap, cmp);
-        tc.compares += cmp;
-        front_store(&v.rs[r], f);
-        if (heavy) {
-          if (2 * f.e + 3 <= kRow16) E.L.list[atomicAdd(&ctl.nheavy, 1u)] = q * n + r;
-          else E.L.list[lend - atomicAdd(&ctl.nwide, 1u)] = q * n + r;
-          continue;
-        }
-        tc.updates++;
-        tc.w_out += 2 * f.e + 1;
+        const uint32_t kg = agg_append(&ctl.nheavy, kind == 1);
+        const uint32_t kw = agg_append(&ctl.nwide, kind == 2);
+        if (kind == 1) E.L.list[kg] = q * n + r;
+        if (kind == 2) E.L.list[lend - kw] = q * n + r;
       }
     }
     flush_thread_counters(ctl, tc);
@@ -1337,12 +1442,15 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     PH_MARK(10);
     // prune + priority of every child of the group in one pass; every
     // child's edit distances are loaded before any is used
+    SUB_T0(tp0);
     uint32_t cslot[kNCB], cdual = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kNCB; ++k) {
       cslot[k] = k < cn ? uni(ctl.ch_slot[c0 + k]) : 0u;
       if (k < cn && (uni(E.L.meta[cslot[k]].flags) & 1u)) cdual |= 1u << k;
     }
+    SUB_T1(22, tp0);
+    SUB_T0(tp1);
     uint64_t ccost[kNCB] = {0, 0, 0, 0};
     uint32_t cn0[kNCB] = {0, 0, 0, 0}, cn1[kNCB] = {0, 0, 0, 0};
     for (uint32_t r = tid; r < n; r += kBlock) {
@@ -1375,14 +1483,20 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         cn1[k] += e2[k] != kInactive;
       }
     }
+    SUB_T1(23, tp1);
+    SUB_T0(tp2);
 #pragma unroll
     for (uint32_t k = 0; k < kNCB; ++k) {
       if (k >= cn) continue;
-      if (ccost[k]) atomicAdd((unsigned long long*)&ctl.ch_cost[c0 + k], (unsigned long long)ccost[k]);
-      if (cn0[k]) atomicAdd(&ctl.ch_some[k][0], cn0[k]);
-      if (cn1[k]) atomicAdd(&ctl.ch_some[k][1], cn1[k]);
+      agg_add64(&ctl.ch_cost[c0 + k], ccost[k]);
+      agg_add(&ctl.ch_some[k][0], cn0[k]);
+      agg_add(&ctl.ch_some[k][1], cn1[k]);
     }
+    SUB_T1(24, tp2);
+    SUB_T0(tp3);
     __syncthreads();
+    SUB_T1(25, tp3);
+    SUB_T0(tp4);
     if (tid == 0) {
       if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;
       else if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
@@ -1395,6 +1509,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       }
     }
     __syncthreads();
+    SUB_T1(26, tp4);
     PH_MARK(11);
     if (uni(ctl.status) != ST_OK) return;
   }
@@ -1442,7 +1557,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           ctl.top_slot = top.slot;
           ctl.top_len = top.len;
           ctl.top_cost = top.cost;
-          if (top.cost > ctl.max_err || top.len < ctl.trk_thr[0] || t.at_capacity(top.len)) {
+          const bool at_cap = t.processed(top.len) >= t.cap;
+          if (top.cost > ctl.max_err || top.len < ctl.trk_thr[0] || at_cap) {
             ctl.cnt[S_IGNORED]++;
             E.L.freestack[ctl.nfree++] = top.slot;
             if (top.slot == ctl.hot_slot) ctl.hot_slot = kNoSlot;
@@ -1451,7 +1567,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
             ctl.farthest[0] = max(ctl.farthest[0], (uint64_t)top.len);
             ctl.cnt[S_EXPLORED]++;
             ctl.last_constraint[0]++;
-            if (!t.process(top.len)) ctl.status = 4;  // "Capacity is full"
+            t.process_unchecked(top.len);
             ctl.action = 0;
             ctl.cache_hit = top.slot == ctl.cache_slot;
             // the popped node's RStates move into LDS; the previous LDS
@@ -1487,7 +1603,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (prev != kNoSlot) hot_store(E, prev, 0);
         hot_fetch(E, top, 0);
       }
-      if (!uni(ctl.cache_hit)) analyze_side<true>(E, ctl, top, 0, len, E.L.rinfo);
+      if (!uni(ctl.cache_hit)) analyze_side0<true>(E, ctl, top, len, E.L.rinfo);
       PH_MARK(1);
       if (tid == 0) {
         const uint32_t ne = ctl.n_end[0];
@@ -1707,14 +1823,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           const uint64_t am = top.len < ctl.am_len ? E.active_min[top.len] : 0;
           const bool imbalanced = dual && (m.nsome[0] < am || m.nsome[1] < am);
           if (top.len >= ctl.am_len) ctl.status = WC_E_INVARIANT_CODE;
-          if (top.cost > ctl.max_err || top.len < ctl.trk_thr[dual] || t.at_capacity(top.len) || imbalanced) {
+          const bool at_cap = t.processed(top.len) >= t.cap;
+          if (top.cost > ctl.max_err || top.len < ctl.trk_thr[dual] || at_cap || imbalanced) {
             ctl.cnt[S_IGNORED]++;
             E.L.freestack[ctl.nfree++] = top.slot;
             ctl.action = 1;
           } else {
             ctl.farthest[dual] = max(ctl.farthest[dual], (uint64_t)top.len);
             ctl.last_constraint[dual]++;
-            if (!t.process(top.len)) ctl.status = 4;
+            t.process_unchecked(top.len);
             ctl.cnt[S_EXPLORED]++;
             ctl.action = 0;
           }
@@ -1723,6 +1840,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         ctl.n_end[0] = ctl.n_end[1] = 0;
         ctl.multi[0] = ctl.multi[1] = 0;
         ctl.n_either = 0;
+        ctl.nheavy = 0;
         ctl.ovf = 0;
       }
       __syncthreads();
@@ -1737,12 +1855,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       const SlotMeta tm = E.L.meta[top];
       const uint32_t tlens[2] = {tm.len[0], tm.len[1]};
 
-      analyze_side<false>(E, ctl, top, 0, tlens[0], R0);
-      if (tdual) analyze_side<false>(E, ctl, top, 1, tlens[1], R1);
+      analyze_sides<false>(E, ctl, top, tdual ? 2 : 1, tlens[0], tlens[1], R0, R1);
       // reached_all_end (dual_consensus.rs:1174-1195): per read, either side at its end
-      for (uint32_t r = tid; r < E.n; r += kBlock) {
-        const bool v = (R0[r].e != kInactive && R0[r].end) || (tdual && R1[r].e != kInactive && R1[r].end);
-        if (v) atomicAdd(&ctl.n_either, 1u);
+      {
+        uint32_t ne = 0;
+        for (uint32_t r = tid; r < E.n; r += kBlock)
+          ne += (R0[r].e != kInactive && R0[r].end) || (tdual && R1[r].e != kInactive && R1[r].end);
+        agg_add(&ctl.n_either, ne);
       }
       __syncthreads();
       if (tid == 0) {
@@ -1949,7 +2068,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
           heap_push(E.L.heap, ctl.heap_n, HeapEntry{ctl.ch_cost[c], ctl.ch_len[c], ctl.ch_slot[c]});
         }
       }
-      __syncthreads();
+      // (no barrier: the next pop is thread 0's too, and the block meets after it)
       PH_MARK(7);
     }
     finish_problem(A, ctl, outp, prob, oslot);

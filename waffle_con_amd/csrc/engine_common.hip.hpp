@@ -914,11 +914,19 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
     off = rsp->off;
   }
   uint32_t W = 2 * e + 1;
+  // wave-uniform bound on every group's row length: entry blocks q with
+  // 16 q >= wlim are skipped (scalar branches) instead of predicated
+#ifdef WC_NO_WLIM
+  uint32_t wlim = 1000000u;
+#else
+  uint32_t wlim = wave_max_u32(act ? W : 0u);
+#endif
   uint32_t v[kQ16];
 #pragma unroll
   for (int q = 0; q < kQ16; ++q) {
     const uint32_t j = 16u * q + gl;
-    v[q] = (act && j < W) ? wf[j] : 0u;
+    v[q] = 0u;
+    if (16u * q < wlim && act && j < W) v[q] = wf[j];
   }
   uint32_t st = act ? kG_RUN : kG_DONE;
   uint32_t mb = 0, cmp = 0;
@@ -926,11 +934,13 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
     if (st == kG_RUN && W + 2 > wcap) st = kG_WCAP;
     else if (st == kG_RUN && W + 2 > kRow16) st = kG_MEM;
     const bool go = st == kG_RUN;  // group-uniform
+    wlim += 2;
     // increase_edit_distance: W -> W + 2 (lane moves run on every lane).
     // Descending q keeps v[q - 1] old; entries j - 1 and j - 2 are row
     // rotations of per-lane selections of v[q] and v[q - 1] (row_ror).
 #pragma unroll
     for (int q = kQ16 - 1; q >= 0; --q) {
+      if (16u * q >= wlim) continue;
       const uint32_t j = 16u * q + gl;
       const uint32_t prev = q > 0 ? v[q > 0 ? q - 1 : 0] : 0u;
       const uint32_t m1 = row_ror1(gl == 15 ? prev : v[q]);
@@ -955,6 +965,7 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
       const uint32_t j = 16u * q + gl;
       const uint32_t bo = v[q] + e - j, oo = v[q] + off;
       xa[q] = ya[q] = 0;
+      if (16u * q >= wlim) continue;
       if (go && j < W && bo < blen && oo < olen) {
         xa[q] = load8(rd, bo);
         ya[q] = load8(con, oo);
@@ -964,6 +975,7 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
 #pragma unroll
     for (int q = 0; q < kQ16; ++q) {
       const uint32_t j = 16u * q + gl;
+      if (16u * q >= wlim) continue;
       if (!(go && j < W)) continue;
       uint32_t d = v[q];
       const uint32_t bo = d + e - j, oo = d + off;
@@ -1001,7 +1013,7 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
 #pragma unroll
   for (int q = 0; q < kQ16; ++q) {
     const uint32_t j = 16u * q + gl;
-    if (j < W) wf[j] = v[q];
+    if (16u * q < wlim && j < W) wf[j] = v[q];
   }
   if (st == kG_MEM) return st;
   gc.updates += gl == 0;
@@ -1010,6 +1022,7 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
   uint32_t nf = 0, mbx = 0, nsc = 0;
 #pragma unroll
   for (int q = 0; q < kQ16; ++q) {
+    if (16u * q >= wlim) continue;
     const uint32_t j = 16u * q + gl;
     const bool valid = j < W;
     const uint32_t d = v[q];
