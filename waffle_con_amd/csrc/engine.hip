@@ -199,13 +199,33 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
   return l;
 }
 
+// slot metadata field by field (a struct copy would move the padding through
+// private memory)
+__device__ __forceinline__ void meta_put(Sh<SlotMeta>& d, const SlotMeta& m) {
+  d.len[0] = m.len[0];
+  d.len[1] = m.len[1];
+  d.nsome[0] = m.nsome[0];
+  d.nsome[1] = m.nsome[1];
+  d.flags = m.flags;
+}
+__device__ __forceinline__ SlotMeta meta_get(const Sh<SlotMeta>& d) {
+  SlotMeta m;
+  m.len[0] = d.len[0];
+  m.len[1] = d.len[1];
+  m.nsome[0] = d.nsome[0];
+  m.nsome[1] = d.nsome[1];
+  m.flags = d.flags;
+  m.pad[0] = m.pad[1] = m.pad[2] = 0;
+  return m;
+}
+
 // ---- priority-queue 1.x emulation (thread 0 only) ----
 template <class A, class B>
-__device__ inline bool prio_less(const A& a, const B& b) {
+__device__ __forceinline__ bool prio_less(const A& a, const B& b) {
   if (a.cost != b.cost) return a.cost > b.cost;  // Reverse(cost)
   return a.len < b.len;
 }
-__device__ inline void heap_push(Sh<HeapEntry>* h, Lo<uint32_t>& n, HeapEntry e) {
+__device__ __forceinline__ void heap_push(Sh<HeapEntry>* h, Lo<uint32_t>& n, HeapEntry e) {
   uint32_t pos = n++;
   while (pos > 0) {
     uint32_t parent = (pos - 1) / 2;
@@ -215,25 +235,38 @@ __device__ inline void heap_push(Sh<HeapEntry>* h, Lo<uint32_t>& n, HeapEntry e)
   }
   h[pos] = e;
 }
-__device__ inline HeapEntry heap_pop(Sh<HeapEntry>* h, Lo<uint32_t>& n) {
-  HeapEntry top = h[0];
+__device__ __forceinline__ HeapEntry heap_pop(Sh<HeapEntry>* h, Lo<uint32_t>& n) {
+  const HeapEntry top = h[0];
   n--;
-  h[0] = h[n];
+  // sift the last entry down from the root: the swap-per-level loop of the
+  // reference, with the moving entry kept in registers (same final layout)
+  const HeapEntry x = h[n];
   uint32_t i = 0;
   if (n > 1) {
     for (;;) {
-      uint32_t l = 2 * i + 1, r = 2 * i + 2, largest = i;
+      const uint32_t l = 2 * i + 1, r = 2 * i + 2;
+      uint32_t largest = i;
+      HeapEntry best = x;
       if (l < n) {
-        if (prio_less(h[largest], h[l])) largest = l;
-        if (r < n && prio_less(h[largest], h[r])) largest = r;
+        const HeapEntry hl = h[l];
+        if (prio_less(best, hl)) {
+          largest = l;
+          best = hl;
+        }
+        if (r < n) {
+          const HeapEntry hr = h[r];
+          if (prio_less(best, hr)) {
+            largest = r;
+            best = hr;
+          }
+        }
       }
       if (largest == i) break;
-      HeapEntry t = h[i];
-      h[i] = h[largest];
-      h[largest] = t;
+      h[i] = best;
       i = largest;
     }
   }
+  h[i] = x;
   return top;
 }
 
@@ -250,22 +283,22 @@ struct TrackerRef {
   Lo<uint64_t>* total;
   Lo<uint64_t>* thr;
   uint64_t cap;
-  __device__ void insert(uint32_t v) {
+  __device__ __forceinline__ void insert(uint32_t v) {
     atomicAdd((uint32_t*)&lc[v], 1u);
     if (v >= *thr) (*total)++;
   }
-  __device__ void remove(uint32_t v) {
+  __device__ __forceinline__ void remove(uint32_t v) {
     atomicSub((uint32_t*)&lc[v], 1u);
     if (v >= *thr) (*total)--;
   }
-  __device__ void increment_threshold() {
+  __device__ __forceinline__ void increment_threshold() {
     *total -= trk_load(&lc[*thr]);
     (*thr)++;
   }
-  __device__ uint32_t processed(uint32_t v) const { return trk_load(&pc[v]); }
+  __device__ __forceinline__ uint32_t processed(uint32_t v) const { return trk_load(&pc[v]); }
   // process() of a length whose processed() count is below capacity (the pop
   // just checked it; only this workgroup's thread 0 touches the tracker)
-  __device__ void process_unchecked(uint32_t v) { atomicAdd((uint32_t*)&pc[v], 1u); }
+  __device__ __forceinline__ void process_unchecked(uint32_t v) { atomicAdd((uint32_t*)&pc[v], 1u); }
 };
 
 __device__ inline uint64_t ceil_u64(double x) {
@@ -343,7 +376,6 @@ __device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_read
 
 // per-workgroup engine context (registers)
 struct Eng {
-  const EngineArgs* A;
   DevConfig cfg;  // by value: uniform registers, not loads through A
   uint32_t chain;
   Gm<uint8_t>* ws;
@@ -366,7 +398,7 @@ struct Eng {
   }
   __device__ const Gm<uint8_t>* read(uint32_t r) const { return rbytes + roff[P.read_begin + r]; }
   __device__ uint32_t rlen(uint32_t r) const { return rlenp[P.read_begin + r]; }
-  __device__ TrackerRef tracker(Lo<Ctl>& ctl, int k) const {
+  __device__ __forceinline__ TrackerRef tracker(Lo<Ctl>& ctl, int k) const {
     const uint64_t L2 = lcap + 2;
     return TrackerRef{trk + 2 * k * L2, trk + (2 * k + 1) * L2, &ctl.trk_total[k], &ctl.trk_thr[k],
                       cfg.max_capacity_per_size};
@@ -387,7 +419,6 @@ __device__ inline Eng eng_uniform(const Eng& s) {
 
 __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
   Eng E;
-  E.A = &A;
   E.cfg = A.cfg;
   E.chain = A.chain;
   E.rbytes = (const Gm<uint8_t>*)A.rbytes;
@@ -834,14 +865,18 @@ __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t d
     const uint32_t n4 = (2 * e + 1 + 3) >> 2;
     const Gm<uint4>* wa = (const Gm<uint4>*)(a.wf + (uint64_t)r * E.wcap);
     Gm<uint4>* wb = (Gm<uint4>*)(b.wf + (uint64_t)r * E.wcap);
+    // (rows hold wcap >= 64 entries, a multiple of 32: the eight loads stay inside)
     for (uint32_t i = 0; i < n4; i += 8) {
-      uint4 t[8];
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k)
-        if (i + k < n4) t[k] = wa[i + k];
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k)
-        if (i + k < n4) wb[i + k] = t[k];
+      const uint4 t0 = wa[i], t1 = wa[i + 1], t2 = wa[i + 2], t3 = wa[i + 3];
+      const uint4 t4 = wa[i + 4], t5 = wa[i + 5], t6 = wa[i + 6], t7 = wa[i + 7];
+      wb[i] = t0;
+      if (i + 1 < n4) wb[i + 1] = t1;
+      if (i + 2 < n4) wb[i + 2] = t2;
+      if (i + 3 < n4) wb[i + 3] = t3;
+      if (i + 4 < n4) wb[i + 4] = t4;
+      if (i + 5 < n4) wb[i + 5] = t5;
+      if (i + 6 < n4) wb[i + 6] = t6;
+      if (i + 7 < n4) wb[i + 7] = t7;
     }
   }
 }
@@ -1192,7 +1227,7 @@ WC_PHASE_FN bool wave_votes(Lo<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, co
 
 // ---- write one result record (finalized node) ----
 WC_PHASE_FN void store_record(Eng& E, Lo<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t slot, uint32_t nsides,
-                                    const uint32_t* lens, bool is_dual) {
+                                    uint32_t len0, uint32_t len1, bool is_dual) {
   const int tid = threadIdx.x;
   const uint64_t rb = result_bytes(E.sides, E.nmax, E.lcap);
   Gm<uint8_t>* rec = outp + 16 + (uint64_t)ctl.store_idx * rb;
@@ -1201,14 +1236,14 @@ WC_PHASE_FN void store_record(Eng& E, Lo<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t 
     Gm<uint32_t>* rfe = (Gm<uint32_t>*)(rec + 16 + E.sides * align16(E.lcap) + s * align16((uint64_t)E.nmax * 4));
     if (s < nsides) {
       SideView v = E.sv(slot, s);
-      copy_bytes(rcon, v.con, lens[s]);  // both 16-byte aligned: 16-byte stores
+      copy_bytes(rcon, v.con, s ? len1 : len0);  // both 16-byte aligned: 16-byte stores
     }
     for (uint32_t r = tid; r < E.n; r += kBlock) rfe[r] = s < nsides ? E.L.fe[s * E.nmax + r] : kInactive;
   }
   if (tid == 0) {
     Gm<uint32_t>* h = (Gm<uint32_t>*)rec;
-    h[0] = lens[0];
-    h[1] = nsides > 1 ? lens[1] : 0;
+    h[0] = len0;
+    h[1] = nsides > 1 ? len1 : 0;
     h[2] = is_dual ? 1u : 0u;
   }
 }
@@ -1298,7 +1333,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
             m.flags |= (sd == 0 ? 2u : 4u);  // lock_sequence
           }
         }
-        E.L.meta[slot] = m;
+        meta_put(E.L.meta[slot], m);
       }
       ctl.nheavy = 0;
       ctl.nwide = 0;
@@ -1382,9 +1417,13 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t c = c0 + q / 2, sd = q & 1u;
       const uint32_t slot = ctl.ch_slot[c];
       SideView v = E.sv(slot, sd);
-      uint32_t e = 0;
-      const uint32_t g = group_edinc(act, &v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
-                                     E.L.meta[slot].len[sd], cfg.wildcard, early, E.wcap, gc, e);
+      const GroupOut go = group_edinc(act, &v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
+                                      E.L.meta[slot].len[sd], cfg.wildcard, early, E.wcap);
+      const uint32_t g = go.st, e = go.e;
+      gc.edinc += go.edinc;
+      gc.updates += go.updates;
+      gc.w_out += go.w_out;
+      gc.cmp += go.cmp;
       if (act && (lane & 15) == 0 && g == kG_WCAP) atomicOr(&ctl.ovf, 4u);
       // ... a row that outgrew the group finishes with the whole wave
       uint64_t mem = ballot(act && (lane & 15) == 0 && g == kG_MEM);
@@ -1648,7 +1687,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (uni(ctl.status) != ST_OK) break;
         if (uni(ctl.store_idx) >= 0) {
           const uint32_t lens[2] = {len, 0};
-          store_record(E, ctl, outp, top, 1, lens, false);
+          store_record(E, ctl, outp, top, 1, lens[0], 0, false);
         }
         PH_MARK(2);
       }
@@ -1852,7 +1891,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       const uint32_t top = uni(ctl.top_slot);
       const uint32_t tlen = uni(ctl.top_len);
       const bool tdual = uni(ctl.top_dual) != 0;
-      const SlotMeta tm = E.L.meta[top];
+      const SlotMeta tm = meta_get(E.L.meta[top]);
       const uint32_t tlens[2] = {tm.len[0], tm.len[1]};
 
       analyze_sides<false>(E, ctl, top, tdual ? 2 : 1, tlens[0], tlens[1], R0, R1);
@@ -1926,7 +1965,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         }
         __syncthreads();
         if (uni(ctl.status) != ST_OK) break;
-        if (uni(ctl.store_idx) >= 0) store_record(E, ctl, outp, top, tdual ? 2 : 1, tlens, tdual);
+        if (uni(ctl.store_idx) >= 0) store_record(E, ctl, outp, top, tdual ? 2 : 1, tlens[0], tlens[1], tdual);
         PH_MARK(2);
       }
 
@@ -1961,7 +2000,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (ctl.ovf) ctl.status = limit_status(ctl.ovf);
         double thr[2] = {0.0, 0.0};
         uint64_t mc[2] = {0, 0};
-        for (uint32_t s = 0; s < (tdual ? 2u : 1u); ++s) {
+#pragma unroll
+        for (uint32_t s = 0; s < 2u; ++s) {
+          if (s == 1 && !tdual) break;
           double sum = -0.0, mx = 0.0;
           bool have = false;
           for (uint32_t k = 0; k < ctl.nkeys[s]; ++k) {

@@ -903,9 +903,14 @@ constexpr uint32_t kG_DONE = 0, kG_WCAP = 1, kG_MEM = 2, kG_RUN = 3;
 struct GroupCnt {
   uint32_t edinc, updates, w_out, cmp;
 };
-__device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd,
-                                       uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc, bool early,
-                                       uint32_t wcap, GroupCnt& gc, uint32_t& e_out) {
+// group_edinc's result, by value (registers): outcome, final e, per-lane counters
+struct GroupOut {
+  uint32_t st, e, edinc, updates, w_out, cmp;
+};
+__device__ __noinline__ GroupOut group_edinc(bool act, Gm<RState>* rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd,
+                                             uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc,
+                                             bool early, uint32_t wcap) {
+  GroupOut go_ = {kG_DONE, 0, 0, 0, 0, 0};
   const int lane = lane_id();
   const uint32_t gl = (uint32_t)lane & 15u, gb = (uint32_t)lane & ~15u;
   uint32_t e = 0, off = 0;
@@ -954,7 +959,7 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
     if (go) {
       W += 2;
       e += 1;
-      gc.edinc += gl == 0;
+      go_.edinc += gl == 0;
     }
     // extend every diagonal: the first 8-byte step of every entry is issued
     // before any is used; runs that go on past it finish in match_run
@@ -1006,18 +1011,19 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
       if (!(lmo + off < olen && !(early && lmb == blen))) st = kG_DONE;
     }
   }
-  gc.cmp += cmp;
-  e_out = e;
-  if (!act || st == kG_WCAP) return st;
+  go_.cmp = cmp;
+  go_.e = e;
+  go_.st = st;
+  if (!act || st == kG_WCAP) return go_;
   // the row back to memory
 #pragma unroll
   for (int q = 0; q < kQ16; ++q) {
     const uint32_t j = 16u * q + gl;
     if (16u * q < wlim && j < W) wf[j] = v[q];
   }
-  if (st == kG_MEM) return st;
-  gc.updates += gl == 0;
-  gc.w_out += gl == 0 ? W : 0u;
+  if (st == kG_MEM) return go_;
+  go_.updates = gl == 0;
+  go_.w_out = gl == 0 ? W : 0u;
   // RState from the register row (regs_rebuild semantics, group-wide)
   uint32_t nf = 0, mbx = 0, nsc = 0;
 #pragma unroll
@@ -1050,7 +1056,8 @@ __device__ __noinline__ uint32_t group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
     rsp->nf = (uint8_t)min(nf, (uint32_t)kF);
     rsp->flags = (nf > (uint32_t)kF || nsc > 65535u) ? kWide : 0;
   }
-  return kG_DONE;
+  go_.st = kG_DONE;
+  return go_;
 }
 
 // Continue an ED-increase loop whose row (W = 2 e + 1 entries, post-extend, not
