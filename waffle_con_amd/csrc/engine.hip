@@ -29,6 +29,13 @@ namespace WC_ENGINE_NS {
 #else
 #define WC_PHASE_FN __device__ inline
 #endif
+// The single engine's push and analysis are separate functions: in the
+// kernel body they raise register pressure past the 128-VGPR budget of 4
+// workgroups/CU (spills), out of line they don't (cfg2 -3% kernel time; the
+// dual engine keeps them inline, where the call overhead costs more)
+#ifndef WC_SINGLE_FN
+#define WC_SINGLE_FN __device__ __noinline__
+#endif
 
 // minimum waves per SIMD the engine kernels are register-allocated for
 // (4 = 4 workgroups of 4 waves per CU, 128 VGPRs)
@@ -685,7 +692,7 @@ WC_PHASE_FN void analyze_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t nsi
 }
 // side 0 only (the single engine)
 template <bool kHot>
-WC_PHASE_FN void analyze_side0(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t len, Sh<RInfo>* out) {
+WC_SINGLE_FN void analyze_side0(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t len, Sh<RInfo>* out) {
   if (threadIdx.x == 0) ctl.nheavy = 0;
   __syncthreads();
   analyze_sides<kHot>(E, ctl, slot, 1, len, 0, out, out);
@@ -724,7 +731,7 @@ WC_PHASE_FN void finalize_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t sid
 // kSrcHot: the parent's RStates are the LDS copy (else the slot's own);
 // kDstHot: the child's RStates go to the LDS copy (else to the slot).
 template <bool kSrcHot, bool kDstHot>
-WC_PHASE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
+WC_SINGLE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1, uint32_t len0, uint32_t len1,
                                   bool want_cost, Sh<RInfo>* info) {
   const int tid = threadIdx.x, lane = lane_id();
   const DevConfig& cfg = E.cfg;
@@ -1554,6 +1561,23 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
   }
 }
 
+// single-engine phases out of line (see WC_SINGLE_FN)
+WC_SINGLE_FN WaveCounters single_finalize(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t len) {
+  WaveCounters cnt = {0, 0, 0, 0, 0};
+  finalize_side<true>(E, ctl, top, 0, len, E.L.fe, cnt);
+  return cnt;
+}
+WC_SINGLE_FN bool single_votes(Lo<Ctl>& ctl, Sh<RInfo>* ri, uint32_t n, bool multi, int wc) {
+  return wave_votes(ctl, 0, ri, ri, ri, n, false, false, multi, wc);
+}
+WC_SINGLE_FN void single_store(Eng& E, Lo<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t top, uint32_t len) {
+  store_record(E, ctl, outp, top, 1, len, 0, false);
+}
+WC_SINGLE_FN void single_activate(Eng& E, Lo<Ctl>& ctl, uint32_t slot, bool hot, uint32_t len) {
+  if (hot) activate_side<true>(E, ctl, slot, 0, len, len, true, E.L.rinfo);
+  else activate_side<false>(E, ctl, slot, 0, len, len, true, E.L.rinfo);
+}
+
 // =====================================================================
 // ConsensusDWFA engine (consensus.rs:139-351)
 // =====================================================================
@@ -1654,8 +1678,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
 
       // ---- finalize a clone (consensus.rs:254-279) ----
       if (uni(ctl.reached)) {
-        WaveCounters cnt = {0, 0, 0, 0, 0};
-        finalize_side<true>(E, ctl, top, 0, len, E.L.fe, cnt);
+        const WaveCounters cnt = single_finalize(E, ctl, top, len);
         flush_counters(ctl, cnt);
         __syncthreads();
         if (tid == 0) {
@@ -1687,15 +1710,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         if (uni(ctl.status) != ST_OK) break;
         if (uni(ctl.store_idx) >= 0) {
           const uint32_t lens[2] = {len, 0};
-          store_record(E, ctl, outp, top, 1, lens[0], 0, false);
+          single_store(E, ctl, outp, top, lens[0]);
         }
         PH_MARK(2);
       }
 
       // ---- votes + child selection (consensus.rs:283-321) ----
       if (wave_id() == 0) {
-        const bool ok =
-            wave_votes(ctl, 0, E.L.rinfo, E.L.rinfo, E.L.rinfo, E.n, false, false, ctl.multi[0] != 0, cfg.wildcard);
+        const bool ok = single_votes(ctl, E.L.rinfo, E.n, ctl.multi[0] != 0, cfg.wildcard);
         if (lane == 0) {
           if (!ok) {
             ctl.status = limit_status(LIM_VOTES);
@@ -1775,8 +1797,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
         else push_sides<true, true>(E, ctl, slot, sym, -1, len + 1, 0, true, E.L.rinfo);
         // reads whose offset activates at this length (consensus.rs:327-335)
         if (len + 1 <= E.P.max_act) {
-          if (slot != top) activate_side<false>(E, ctl, slot, 0, len + 1, len + 1, true, E.L.rinfo);
-          else activate_side<true>(E, ctl, slot, 0, len + 1, len + 1, true, E.L.rinfo);
+          single_activate(E, ctl, slot, slot == top, len + 1);
         }
         if (tid == 0) {
           if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;

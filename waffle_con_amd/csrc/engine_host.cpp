@@ -425,10 +425,13 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
       pending.swap(later);
       continue;
     }
+    const auto t0 = std::chrono::steady_clock::now();
     rc = launch_start(ctx, *L, b, cfg, items, run, caps);
     if (rc != WC_OK) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
     rc = launch_finish(ctx, *L);
     if (rc != WC_OK) return rc;
+    const auto t2 = std::chrono::steady_clock::now();
     kernel_ms += L->kernel_ms;
     launches++;
     std::vector<uint32_t> retry;
@@ -445,6 +448,11 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
         }
       }
     }
+    if (getenv("WC_HOST_TIMING"))
+      fprintf(stderr, "[wc] launch: start %.3f ms, to completion %.3f ms (kernel %.3f), harvest %.3f ms\n",
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(), L->kernel_ms,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
     retry.insert(retry.end(), later.begin(), later.end());
     pending.swap(retry);
   }

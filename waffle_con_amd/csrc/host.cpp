@@ -204,13 +204,22 @@ int batch_run(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, wc
   }
   double kms = 0;
   uint64_t nl = 0;
+  const auto t1 = std::chrono::steady_clock::now();
   int rc = run_engine(ctx, b, cfg, sides, items, outs, kms, nl);
   if (rc != WC_OK) return rc;
+  const auto t2 = std::chrono::steady_clock::now();
   for (uint32_t i = 0; i < n; ++i) {
     if (sides == 1) build_single(outs[i], cfg.consensus_cost, R->probs[i]);
     else build_dual(outs[i], b->probs[i].n_reads, cfg.consensus_cost, R->probs[i]);
   }
   double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (getenv("WC_HOST_TIMING")) {
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
+      return std::chrono::duration<double, std::milli>(z - a).count();
+    };
+    fprintf(stderr, "[wc] host: plan %.3f ms, engine %.3f ms (kernel %.3f), results %.3f ms\n", ms(t0, t1), ms(t1, t2),
+            kms, ms(t2, std::chrono::steady_clock::now()));
+  }
   fill_stats(R, kms, nl, wall);
   return WC_OK;
 }
