@@ -130,6 +130,17 @@ uint32_t wc_results_count(const wc_results* r, uint32_t p);
 int wc_results_single(const wc_results* r, uint32_t p, uint32_t k, const uint8_t** seq, uint64_t* seq_len,
                       const uint64_t** scores, uint64_t* n_scores);
 
+/* Every Consensus of a single-consensus result set in one call (a binding
+ * helper for many loci; no reference counterpart: it returns what
+ * wc_results_status/count/single return, in bulk). wc_results_single_sizes
+ * gives the totals over all problems; wc_results_single_pack then fills
+ * status[problems], count[problems], seq[seq_bytes] (all sequences back to
+ * back), seq_off[n_results + 1], scores[n_scores], score_off[n_results + 1],
+ * results in problem order. */
+int wc_results_single_sizes(const wc_results* r, uint64_t* n_results, uint64_t* seq_bytes, uint64_t* n_scores);
+int wc_results_single_pack(const wc_results* r, int32_t* status, uint32_t* count, uint8_t* seq, uint64_t* seq_off,
+                           uint64_t* scores, uint64_t* score_off);
+
 /* DualConsensus (dual_consensus.rs:52-177). scores1/scores2 use -1 for None. */
 typedef struct wc_dual_view {
   const uint8_t* seq1;

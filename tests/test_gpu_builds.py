@@ -1,0 +1,73 @@
+"""GPU parity of every engine build on the same problems: the 256-thread
+build (WC_NARROW=0), the 128-thread build (engine_narrow.hip, the default for
+problems of <= 128 reads) and the global-state build (WC_GSTATE). The build is
+picked per launch from the environment (engine_host.cpp plan_caps), so one
+process exercises all of them. Sequences, scores and every work counter must
+equal the oracle's."""
+import os
+
+import pytest
+
+import oracle_ffi as orc
+
+pytestmark = pytest.mark.gpu
+
+hip = pytest.importorskip("hip_runner")
+
+KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored", "nodes_ignored",
+        "peak_queue_size")
+BUILDS = {"wide": {"WC_NARROW": "0"}, "narrow-single": {"WC_NARROW": "1"}, "narrow": {"WC_NARROW": "2"},
+          "gstate": {"WC_GSTATE": "1"}}
+
+
+@pytest.fixture(params=sorted(BUILDS))
+def build(request):
+    old = {k: os.environ.get(k) for k in ("WC_NARROW", "WC_GSTATE")}
+    for k in old:
+        os.environ.pop(k, None)
+    os.environ.update(BUILDS[request.param])
+    yield request.param
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
+def _gen(L, N, err, seed):
+    import waffle_con_amd as w
+    return w.generate_test(4, L, N, err, seed)[1]
+
+
+@pytest.mark.parametrize("L,N,err,seed", [(1500, 40, 0.01, 5), (800, 128, 0.02, 6), (600, 3, 0.05, 7)])
+def test_single_builds(build, L, N, err, seed):
+    seqs = _gen(L, N, err, seed)
+    cfg = dict(min_count=max(1, N // 4))
+    exp, ec = orc.consensus(seqs, counters=True, **cfg)
+    got, gc = hip.consensus(seqs, counters=True, **cfg)
+    assert got == exp
+    for k in KEYS:
+        assert gc[k] == ec[k], (build, k, gc[k], ec[k])
+
+
+@pytest.mark.parametrize("L,N,err,seeds", [(700, 20, 0.01, (8, 9)), (500, 64, 0.01, (10, 11))])
+def test_dual_builds(build, L, N, err, seeds):
+    a = _gen(L, N, err, seeds[0])
+    b = _gen(L, N, err, seeds[1])
+    mix = [x for pair in zip(a, b) for x in pair]
+    exp, ec = orc.dual_consensus(mix, counters=True, min_count=max(2, N // 4))
+    got, gc = hip.dual_consensus(mix, counters=True, min_count=max(2, N // 4))
+    assert got == exp
+    for k in KEYS:
+        assert gc[k] == ec[k], (build, k, gc[k], ec[k])
+
+
+def test_priority_builds(build):
+    from waffle_con_amd import synth
+    for seed in (6, 2):
+        chains = synth.cfg5_locus(seed)
+        exp, ec = orc.priority_consensus(chains, counters=True, wildcard=ord("*"))
+        got, gc = hip.priority_consensus(chains, counters=True, wildcard=ord("*"))
+        assert got == exp
+        for k in KEYS:
+            assert gc[k] == ec[k], (build, seed, k, gc[k], ec[k])

@@ -5,7 +5,7 @@ import ctypes
 
 from . import _lib
 from .cdwfa_config import CdwfaConfig
-from .consensus import Consensus, _problems, _raise_for, _stats
+from .consensus import _problems, _single_results, _stats
 from .dual_consensus import _dual_results
 
 
@@ -49,24 +49,7 @@ class ResidentBatch:
         if rc != _lib.WC_OK:
             raise _lib.WaffleConError("wc_batch_consensus failed: " + ctx.last_error(), rc)
         try:
-            out = []
-            for p in range(len(self._batch)):
-                try:
-                    _raise_for(res, p, L)
-                except _lib.WaffleConError as e:
-                    if not return_errors:
-                        raise
-                    out.append(e)
-                    continue
-                items = []
-                for k in range(L.wc_results_count(res, p)):
-                    sp, sl = _lib._u8p(), ctypes.c_uint64()
-                    cp, cl = ctypes.POINTER(ctypes.c_uint64)(), ctypes.c_uint64()
-                    L.wc_results_single(res, p, k, ctypes.byref(sp), ctypes.byref(sl), ctypes.byref(cp),
-                                        ctypes.byref(cl))
-                    items.append(Consensus(_lib.u8_bytes(sp, sl.value), config.consensus_cost,
-                                           _lib.u64_list(cp, cl.value)))
-                out.append(items)
+            out = _single_results(res, len(self._batch), config.consensus_cost, L, return_errors)
             return out, _stats(res, L, per_problem)
         finally:
             L.wc_results_free(res)

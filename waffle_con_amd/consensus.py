@@ -6,41 +6,98 @@
 """
 import ctypes
 
+import numpy as np
+
 from . import _lib
 from .cdwfa_config import CdwfaConfig, ConsensusCost
 
 
 class Consensus:
-    """consensus.rs:42-74."""
-    __slots__ = ("_sequence", "_consensus_cost", "_scores")
+    """consensus.rs:42-74. Results of a batch call share one packed host
+    buffer (wc_results_single_pack); each Consensus unpacks its own sequence
+    and scores from it into Python objects on first access."""
+    __slots__ = ("_sequence", "_consensus_cost", "_scores", "_src")
 
     def __init__(self, sequence, consensus_cost, scores):
         self._sequence = bytes(sequence)
         self._consensus_cost = consensus_cost
         self._scores = list(scores)
+        self._src = None
+
+    @classmethod
+    def _packed(cls, pack, j, consensus_cost):
+        """Result j of a packed result set pack = (seq u8 array, seq offsets,
+        scores u64 array, score offsets)."""
+        c = cls.__new__(cls)
+        c._sequence = c._scores = None
+        c._consensus_cost = consensus_cost
+        c._src = (pack, j)
+        return c
+
+    def _unpack(self):
+        (seq, so, sc, co), j = self._src
+        self._sequence = seq[so[j]:so[j + 1]].tobytes()
+        self._scores = sc[co[j]:co[j + 1]].tolist()
+        self._src = None
 
     def sequence(self):
+        if self._src is not None:
+            self._unpack()
         return self._sequence
 
     def consensus_cost(self):
         return self._consensus_cost
 
     def scores(self):
+        if self._src is not None:
+            self._unpack()
         return self._scores
 
     def __eq__(self, other):
-        return (isinstance(other, Consensus) and self._sequence == other._sequence
-                and self._consensus_cost == other._consensus_cost and self._scores == other._scores)
+        return (isinstance(other, Consensus) and self.sequence() == other.sequence()
+                and self._consensus_cost == other._consensus_cost and self.scores() == other.scores())
 
     def __repr__(self):
         return "Consensus(sequence=%r, consensus_cost=%s, scores=%r)" % (
-            self._sequence, self._consensus_cost.name, self._scores)
+            self.sequence(), self._consensus_cost.name, self.scores())
 
 
 def _raise_for(results, p, L):
     st = L.wc_results_status(results, p)
     if st != _lib.WC_OK:
         raise _lib.WaffleConError(L.wc_results_error(results, p).decode(), st)
+
+
+def _single_results(res, n, cost, L, return_errors):
+    """Per problem: a list of Consensus, or its WaffleConError. Everything
+    comes out of the library in one wc_results_single_pack call."""
+    u64 = ctypes.c_uint64
+    nr, sb, ns = u64(), u64(), u64()
+    if L.wc_results_single_sizes(res, ctypes.byref(nr), ctypes.byref(sb), ctypes.byref(ns)) != _lib.WC_OK:
+        raise _lib.WaffleConError("wc_results_single_sizes: not a single-consensus result set", _lib.WC_E_BAD_INPUT)
+    status = np.zeros(max(n, 1), np.int32)
+    count = np.zeros(max(n, 1), np.uint32)
+    seq = np.empty(max(sb.value, 1), np.uint8)
+    soff = np.empty(nr.value + 1, np.uint64)
+    sc = np.empty(max(ns.value, 1), np.uint64)
+    coff = np.empty(nr.value + 1, np.uint64)
+    L.wc_results_single_pack(res, status.ctypes.data, count.ctypes.data, seq.ctypes.data, soff.ctypes.data,
+                             sc.ctypes.data, coff.ctypes.data)
+    so, co, cnt, st = soff.tolist(), coff.tolist(), count.tolist(), status.tolist()
+    pack = (seq, so, sc, co)
+    out, k = [], 0
+    mk = Consensus._packed
+    for p in range(n):
+        if st[p] != _lib.WC_OK:
+            e = _lib.WaffleConError(L.wc_results_error(res, p).decode(), st[p])
+            if not return_errors:
+                raise e
+            out.append(e)
+            k += cnt[p]
+            continue
+        out.append([mk(pack, j, cost) for j in range(k, k + cnt[p])])
+        k += cnt[p]
+    return out
 
 
 def _stats(results, L, per_problem=False):
@@ -89,23 +146,7 @@ def consensus_batch(problems, config=None, context=None, return_errors=False):
     if rc != _lib.WC_OK:
         raise _lib.WaffleConError("wc_consensus_batch failed: " + ctx.last_error(), rc)
     try:
-        out = []
-        for p in range(len(batch)):
-            try:
-                _raise_for(res, p, L)
-            except _lib.WaffleConError as e:
-                if not return_errors:
-                    raise
-                out.append(e)
-                continue
-            items = []
-            for k in range(L.wc_results_count(res, p)):
-                sp, sl = _lib._u8p(), ctypes.c_uint64()
-                cp, cl = ctypes.POINTER(ctypes.c_uint64)(), ctypes.c_uint64()
-                L.wc_results_single(res, p, k, ctypes.byref(sp), ctypes.byref(sl), ctypes.byref(cp), ctypes.byref(cl))
-                items.append(Consensus(_lib.u8_bytes(sp, sl.value), config.consensus_cost,
-                                       _lib.u64_list(cp, cl.value)))
-            out.append(items)
+        out = _single_results(res, len(batch), config.consensus_cost, L, return_errors)
         return out, _stats(res, L)
     finally:
         L.wc_results_free(res)

@@ -60,6 +60,14 @@ __device__ __forceinline__ RInfoReg nom_load(const Sh<uint16_t>* nom, const Sh<C
   return x;
 }
 
+// LDS window slot of read r (the walk deals read r to wave r % kEW, lane
+// r / kEW): the lanes of one wave read consecutive slots (engine_shared.hpp
+// kWinStride). kEW * ceil(n / kEW) <= 4 * win_m4(n) slots, so the carve of
+// win_m4 fits every build's wave count.
+__device__ __forceinline__ uint32_t cwin_slot(uint32_t r, uint32_t n) {
+  return (r % (uint32_t)kEW) * ((n + kEW - 1) / (uint32_t)kEW) + r / (uint32_t)kEW;
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -79,7 +87,7 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
   SUB_T0(ta);
   // windows: 64 bytes from the lowest tip, 16-byte aligned (reads are
   // 16-byte aligned and the read buffer has 64 bytes of tail padding)
-  for (uint32_t r = tid; r < E.n; r += kBlock) {
+  for (uint32_t r = tid; r < E.n; r += kEB) {
     const RRaw h = rstate_load(&E.L.hot[r]);
     if (rraw_e(h) != kInactive && (rraw_flags(h) & kWide)) atomicOr(&ctl.chain_nochain, 1u);
     Front f;
@@ -94,7 +102,7 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     if (lo == kInactive) lo = 0;
     const uint32_t wb = lo & ~15u;
     const Gm<uint4>* g = (const Gm<uint4>*)(E.read(r) + wb);
-    Sh<uint32_t>* w = (Sh<uint32_t>*)(E.L.cwin + (uint64_t)win_slot(r, win_m4(E.n)) * kWinStride);
+    Sh<uint32_t>* w = (Sh<uint32_t>*)(E.L.cwin + (uint64_t)cwin_slot(r, E.n) * kWinStride);
     const uint4 a0 = g[0], a1 = g[1], a2 = g[2], a3 = g[3];
     w[0] = a0.x, w[1] = a0.y, w[2] = a0.z, w[3] = a0.w;
     w[4] = a1.x, w[5] = a1.y, w[6] = a1.z, w[7] = a1.w;
@@ -103,16 +111,16 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     E.L.cwb[r] = wb;
   }
   const Gm<uint32_t>* pc = E.trk + (E.lcap + 2);  // PQueueTracker processed counts
-  for (uint32_t j = tid; j <= K; j += kBlock) E.L.cpc[j] = (j >= 1) ? trk_load(&pc[L0 + j]) : 0u;
+  for (uint32_t j = tid; j <= K; j += kEB) E.L.cpc[j] = (j >= 1) ? trk_load(&pc[L0 + j]) : 0u;
   __syncthreads();
   SUB_T1(23, ta);
   SUB_T0(tb);
   {
     // upcoming bases of each read's first tip (reads 0..63); every wave
-    // predicts the steps t = 1 + wave (mod kWaves)
+    // predicts the steps t = 1 + wave (mod kEW)
     const uint32_t wave = (uint32_t)wave_id();
     uint32_t bo_tip = kInactive, blen = 0, wb = 0;
-    const Sh<uint8_t>* win = E.L.cwin + (uint64_t)win_slot(min((uint32_t)lane, E.n - 1), win_m4(E.n)) * kWinStride;
+    const Sh<uint8_t>* win = E.L.cwin + (uint64_t)cwin_slot(min((uint32_t)lane, E.n - 1), E.n) * kWinStride;
     if ((uint32_t)lane < E.n) {
       Front f;
       front_load(rstate_load(&E.L.hot[lane]), f);
@@ -130,17 +138,17 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     // all of this wave's bytes under one wait; LDS windows only: a read whose
     // next bases lie past its window does not vote (the prediction is a
     // guess, acceptance is exact)
-    constexpr uint32_t kPer = (kChainMax + kWaves - 1) / kWaves;
+    constexpr uint32_t kPer = (kChainMax + kEW - 1) / kEW;
     uint32_t xs[kPer];
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u) {
-      const uint32_t t = 1 + wave + kWaves * u;
+      const uint32_t t = 1 + wave + kEW * u;
       const uint32_t q = bo_tip + t - wb;
       xs[u] = (bo_tip != kInactive && t < K && bo_tip + t < blen && q < 64u) ? (uint32_t)win[q] : 0x100u;
     }
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u) {
-      const uint32_t t = 1 + wave + kWaves * u;
+      const uint32_t t = 1 + wave + kEW * u;
       if (t >= K) break;
       const uint32_t x = xs[u];
       // plurality of x over the wave (ties: the first-seen symbol); a
@@ -321,7 +329,7 @@ __device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, 
 template <bool kFirst>
 __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int lane = lane_id(), wave = wave_id();
-  // reads are dealt round-robin over the waves (read = lane * kWaves + wave):
+  // reads are dealt round-robin over the waves (read = lane * kEW + wave):
   // every wave walks a quarter of the reads, so the edit-distance increases,
   // which a wave handles one read at a time, are spread over all four
   if ((uint32_t)wave >= E.n) return;  // no reads in this wave (no barriers below)
@@ -329,14 +337,14 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   const bool early = cfg.early != 0;
   const int wc = cfg.wildcard;
   SideView v = E.sv(top, 0);
-  const uint32_t r = (uint32_t)lane * kWaves + (uint32_t)wave;
+  const uint32_t r = (uint32_t)lane * kEW + (uint32_t)wave;
   const bool has = r < E.n;
   Front f;
   f.e = kInactive;
   f.off = f.maxb = f.nscmp = f.mask = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) f.fi[k] = f.fd[k] = 0;
-  Win W{E.L.cwin + (uint64_t)win_slot(min(r, E.n - 1), win_m4(E.n)) * kWinStride, 0};
+  Win W{E.L.cwin + (uint64_t)cwin_slot(min(r, E.n - 1), E.n) * kWinStride, 0};
   uint32_t blen = 0;
   if (has) {
     front_load(rstate_load(&E.L.hot[r]), f);
@@ -379,7 +387,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
       hm &= hm - 1;
       if (lane == l) front_store(tmp, f);
       wave_lds_sync();
-      const uint32_t rl = (uint32_t)l * kWaves + (uint32_t)wave;
+      const uint32_t rl = (uint32_t)l * kEW + (uint32_t)wave;
       if (kFirst && !((bak >> l) & 1ull)) {
         // first rewrite of this row in the chain: keep a copy in slot S (the
         // rows are otherwise only touched at frontier diagonals, which a
@@ -511,7 +519,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
 __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t K) {
   const int lane = lane_id();
   const DevConfig& cfg = E.cfg;
-  for (uint32_t j = 1 + wave_id(); j < K; j += kWaves) {
+  for (uint32_t j = 1 + wave_id(); j < K; j += kEW) {
     SUB_T0(ta);
     auto& st = E.L.cstep[j];
     const uint64_t po = st.po, ef = st.ef;
@@ -631,7 +639,7 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
   const uint32_t K = uni(ctl.chain_k);
   if (K == 0) return 0;
   const uint32_t S = uni(ctl.chain_slot);
-  for (uint32_t i = tid; i < (K + 1) * (uint32_t)(sizeof(ChainStep) / 4); i += kBlock)
+  for (uint32_t i = tid; i < (K + 1) * (uint32_t)(sizeof(ChainStep) / 4); i += kEB)
     ((Sh<uint32_t>*)E.L.cstep)[i] = 0;
   chain_prepare(E, ctl, top, L0, K, S);
   __syncthreads();
@@ -667,7 +675,7 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
   SideView v = E.sv(top, 0), b = E.sv(S, 0);
   if (jstar == K && Keff == K) {
     // every step accepted: the speculative final state is the node
-    for (uint32_t r = tid; r < E.n; r += kBlock) {
+    for (uint32_t r = tid; r < E.n; r += kEB) {
       const RRaw t = rstate_load(&b.rs[r]);
       rstate_store(&E.L.hot[r], t);
       RInfoReg x = nom_load(E.L.cnom + K * E.nmax, E.L.covf, r);
@@ -689,14 +697,14 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
     // thread path writes)
     const int lane = lane_id();
     const uint32_t nb = uni(ctl.chain_nbak);
-    for (uint32_t k = wave_id(); k < nb; k += kWaves) {
+    for (uint32_t k = wave_id(); k < nb; k += kEW) {
       const uint32_t r = E.L.list[2 * k], W = E.L.list[2 * k + 1];
       const Gm<uint32_t>* src = b.wf + (uint64_t)r * E.wcap;
       Gm<uint32_t>* dst = v.wf + (uint64_t)r * E.wcap;
       for (uint32_t i = lane; i < W; i += 64) dst[i] = src[i];
     }
     __syncthreads();
-    for (uint32_t r = tid; r < E.n; r += kBlock) {
+    for (uint32_t r = tid; r < E.n; r += kEB) {
       Front f;
       front_load(rstate_load(&E.L.hot[r]), f);
       if (f.e == kInactive) continue;

@@ -148,7 +148,7 @@ struct Lds {
   Sh<RState>* hot;       // [sides][nmax] RStates of the node being expanded (single engine)
   Sh<ChainStep>* cstep;  // chain area (single engine with A.chain > 0)
   Sh<ChainOvf>* covf;
-  Sh<RState>* ctmp;      // [kWaves]
+  Sh<RState>* ctmp;      // [kEW]
   Sh<uint16_t>* cnom;    // [K+1][nmax]
   Sh<uint8_t>* cwin;     // read windows, slot win_slot(r) of kWinStride bytes
   Sh<uint32_t>* cwb;     // [nmax]
@@ -180,7 +180,7 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
     l.covf = (Sh<ChainOvf>*)p;
     p += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
     l.ctmp = (Sh<RState>*)p;
-    p += (uint64_t)kWaves * 64;
+    p += (uint64_t)kEW * 64;
     l.cnom = (Sh<uint16_t>*)p;
     p += align16((uint64_t)(K + 1) * nmax * 2);
     l.cwin = p;
@@ -542,7 +542,7 @@ __device__ inline uint32_t claim_problem(const EngineArgs& A, Lo<Ctl>& ctl, Eng&
   Gm<uint64_t>* lroff = (Gm<uint64_t>*)E.roff;
   Gm<int64_t>* lract = (Gm<int64_t>*)E.ract;
   Gm<uint32_t>* lrlen = (Gm<uint32_t>*)E.rlenp;
-  for (uint32_t r = tid; r < P.n_reads; r += kBlock) {
+  for (uint32_t r = tid; r < P.n_reads; r += kEB) {
     const uint32_t q = (base + r) % A.qslots;
     lroff[r] = A.roff[q];
     lract[r] = A.ractivate[q];
@@ -591,10 +591,10 @@ __device__ inline void init_problem(Eng& E, Lo<Ctl>& ctl) {
     ctl.ph_t = __builtin_amdgcn_s_memtime();
 #endif
   }
-  for (uint32_t i = tid; i < E.pcap; i += kBlock) E.L.freestack[i] = E.pcap - 1 - i;
-  for (uint32_t i = tid; i < 4 * (E.lcap + 2); i += kBlock) E.trk[i] = 0;
+  for (uint32_t i = tid; i < E.pcap; i += kEB) E.L.freestack[i] = E.pcap - 1 - i;
+  for (uint32_t i = tid; i < 4 * (E.lcap + 2); i += kEB) E.trk[i] = 0;
   SideView v = E.sv(0, 0);
-  for (uint32_t r = tid; r < E.n; r += kBlock) {
+  for (uint32_t r = tid; r < E.n; r += kEB) {
     // e = 0 (or None), off = 0, maxb = 0, nscmp = 0, nf = 1: the single
     // diagonal d=0 sits at the (empty) consensus end
     const uint32_t e = E.ract[E.P.read_begin + r] < 0 ? 0u : kInactive;
@@ -638,7 +638,7 @@ WC_PHASE_FN void analyze_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t nsi
   const uint32_t n = E.n, items = nsides * n;
   uint32_t ends0 = 0, ends1 = 0;
   bool multi0 = false, multi1 = false;
-  for (uint32_t base = 0; base < items; base += kBlock) {
+  for (uint32_t base = 0; base < items; base += kEB) {
     const uint32_t it = base + tid;
     bool wide = false;
     if (it < items) {
@@ -674,7 +674,7 @@ WC_PHASE_FN void analyze_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t nsi
   agg_or(&ctl.multi[1], multi1, 1u);
   __syncthreads();
   const uint32_t nh = uni(ctl.nheavy);
-  for (uint32_t k = wave_id(); k < nh; k += kWaves) {
+  for (uint32_t k = wave_id(); k < nh; k += kEW) {
     const uint32_t it = uni(E.L.list[k]);
     const uint32_t side = it >= n ? 1u : 0u, r = it - side * n;
     Sh<RInfo>* out = (side ? out1 : out0) + r;
@@ -705,7 +705,7 @@ WC_PHASE_FN void finalize_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t sid
   const int lane = lane_id();
   SideView v = E.sv(slot, side);
   const auto rs = node_rs<kHot>(E, slot, side);
-  for (uint32_t r = wave_id(); r < E.n; r += kWaves) {
+  for (uint32_t r = wave_id(); r < E.n; r += kEW) {
     const uint32_t e = rs[r].e;
     if (e == kInactive) {
       if (lane == 0) fe[r] = kInactive;
@@ -744,7 +744,7 @@ WC_SINGLE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1
   // work items over the pushed sides only: (side, read) with side >= first
   const uint32_t first = s0 >= 0 ? 0u : 1u;
   const uint32_t items = ((s0 >= 0 ? 1u : 0u) + (s1 >= 0 ? 1u : 0u)) * E.n;
-  for (uint32_t base = 0; base < items; base += kBlock) {
+  for (uint32_t base = 0; base < items; base += kEB) {
     const uint32_t it = base + tid;
     const uint32_t hi = it >= E.n ? 1u : 0u, r = it - hi * E.n, side = first + hi;
     bool heavy_item = false;
@@ -806,7 +806,7 @@ WC_SINGLE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1
   PH_MARK(5);
   const uint32_t nh = uni(ctl.nheavy);
   WaveCounters cnt = {0, 0, 0, 0, 0};
-  for (uint32_t k = wave_id(); k < nh; k += kWaves) {
+  for (uint32_t k = wave_id(); k < nh; k += kEW) {
     const uint32_t it = E.L.list[k];
     const uint32_t side = it >= E.n ? 1u : 0u, r = it - side * E.n;
     SideView v = E.sv(slot, side);
@@ -837,20 +837,20 @@ WC_SINGLE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1
 
 __device__ inline void copy_bytes(Gm<uint8_t>* d, const Gm<uint8_t>* s, uint32_t len) {
   const uint32_t n16 = len >> 4;
-  for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((Gm<uint4>*)d)[i] = ((const Gm<uint4>*)s)[i];
-  for (uint32_t i = (n16 << 4) + threadIdx.x; i < len; i += kBlock) d[i] = s[i];
+  for (uint32_t i = threadIdx.x; i < n16; i += kEB) ((Gm<uint4>*)d)[i] = ((const Gm<uint4>*)s)[i];
+  for (uint32_t i = (n16 << 4) + threadIdx.x; i < len; i += kEB) d[i] = s[i];
 }
 
 // move the RStates of one node side between its slot and the LDS copy
 __device__ inline void hot_store(Eng& E, uint32_t slot, uint32_t side) {
   Gm<RState>* d = E.sv(slot, side).rs;
   const Sh<RState>* h = E.L.hot + side * E.nmax;
-  for (uint32_t r = threadIdx.x; r < E.n; r += kBlock) rstate_store(&d[r], rstate_load(&h[r]));
+  for (uint32_t r = threadIdx.x; r < E.n; r += kEB) rstate_store(&d[r], rstate_load(&h[r]));
 }
 __device__ inline void hot_fetch(Eng& E, uint32_t slot, uint32_t side) {
   const Gm<RState>* d = E.sv(slot, side).rs;
   Sh<RState>* h = E.L.hot + side * E.nmax;
-  for (uint32_t r = threadIdx.x; r < E.n; r += kBlock) rstate_store(&h[r], rstate_load(&d[r]));
+  for (uint32_t r = threadIdx.x; r < E.n; r += kEB) rstate_store(&h[r], rstate_load(&d[r]));
 }
 
 // ---- clone a node: RState records, live wavefront rows, consensus bytes ----
@@ -864,7 +864,7 @@ __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t d
   // thread per read: its RState, then its wavefront row in 16-byte moves with
   // eight loads in flight, so the reads' copies overlap instead of queueing
   // behind one wave per read (rows are 16-byte aligned: wcap % 64 == 0)
-  for (uint32_t r = threadIdx.x; r < E.n; r += kBlock) {
+  for (uint32_t r = threadIdx.x; r < E.n; r += kEB) {
     const RRaw st = rstate_load(&ars[r]);
     if (!kSrcHot) rstate_store(&b.rs[r], st);
     const uint32_t e = rraw_e(st);
@@ -902,14 +902,14 @@ WC_PHASE_FN void activate_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t sid
   const int tid = threadIdx.x, lane = lane_id();
   if (tid == 0) ctl.nheavy = 0;
   __syncthreads();
-  for (uint32_t r = tid; r < E.n; r += kBlock)
+  for (uint32_t r = tid; r < E.n; r += kEB)
     if (E.ract[E.P.read_begin + r] == (int64_t)alen) E.L.list[atomicAdd(&ctl.nheavy, 1u)] = r;
   __syncthreads();
   const uint32_t nh = uni(ctl.nheavy);
   SideView v = E.sv(slot, side);
   const auto dst = node_rs<kHot>(E, slot, side);
   WaveCounters cnt = {0, 0, 0, 0, 0};
-  for (uint32_t k = wave_id(); k < nh; k += kWaves) {
+  for (uint32_t k = wave_id(); k < nh; k += kEW) {
     const uint32_t r = E.L.list[k];
     if (uni(dst[r].e) != kInactive) {
       if (lane == 0) atomicOr(&ctl.ovf, 16u);
@@ -1245,7 +1245,7 @@ WC_PHASE_FN void store_record(Eng& E, Lo<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t 
       SideView v = E.sv(slot, s);
       copy_bytes(rcon, v.con, s ? len1 : len0);  // both 16-byte aligned: 16-byte stores
     }
-    for (uint32_t r = tid; r < E.n; r += kBlock) rfe[r] = s < nsides ? E.L.fe[s * E.nmax + r] : kInactive;
+    for (uint32_t r = tid; r < E.n; r += kEB) rfe[r] = s < nsides ? E.L.fe[s * E.nmax + r] : kInactive;
   }
   if (tid == 0) {
     Gm<uint32_t>* h = (Gm<uint32_t>*)rec;
@@ -1373,7 +1373,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t slot = uni(ctl.ch_slot[c]);
       const uint32_t olen = uni(E.L.meta[slot].len[sd]);
       SideView v = E.sv(slot, sd);
-      for (uint32_t base = 0; base < n; base += kBlock) {
+      for (uint32_t base = 0; base < n; base += kEB) {
         const uint32_t r = base + tid;
         uint32_t kind = 0;  // 1: group list, 2: wave list
         if (r < n) {
@@ -1415,8 +1415,8 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     WaveCounters cnt = {0, 0, 0, 0, 0};
     GroupCnt gc = {0, 0, 0, 0};
     // (up to one item per wave the 64-lane path is quicker: it goes to the wave loop)
-    const uint32_t ng = nh > (uint32_t)kWaves ? nh : 0u;
-    for (uint32_t b0 = wave_id() * 4u; b0 < ng; b0 += kWaves * 4u) {
+    const uint32_t ng = nh > (uint32_t)kEW ? nh : 0u;
+    for (uint32_t b0 = wave_id() * 4u; b0 < ng; b0 += kEW * 4u) {
       const uint32_t k = b0 + ((uint32_t)lane >> 4);
       const bool act = k < ng;
       const uint32_t it = act ? E.L.list[k] : 0u;
@@ -1459,7 +1459,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     cnt.compares += wave_sum_u32(gc.cmp);
     // ... and wide frontiers / long rows (and a few group items) one read per wave
     const uint32_t nsolo = nw + (nh - ng);
-    for (uint32_t k = wave_id(); k < nsolo; k += kWaves) {
+    for (uint32_t k = wave_id(); k < nsolo; k += kEW) {
       const uint32_t it = uni(k < nw ? E.L.list[lend - k] : E.L.list[k - nw]);
       const uint32_t q = it / n, r = it - q * n;
       const uint32_t c = c0 + q / 2, sd = q & 1u;
@@ -1499,7 +1499,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     SUB_T0(tp1);
     uint64_t ccost[kNCB] = {0, 0, 0, 0};
     uint32_t cn0[kNCB] = {0, 0, 0, 0}, cn1[kNCB] = {0, 0, 0, 0};
-    for (uint32_t r = tid; r < n; r += kBlock) {
+    for (uint32_t r = tid; r < n; r += kEB) {
       uint32_t e1[kNCB], e2[kNCB];
 #pragma unroll
       for (uint32_t k = 0; k < kNCB; ++k) {
@@ -1581,7 +1581,7 @@ WC_SINGLE_FN void single_activate(Eng& E, Lo<Ctl>& ctl, uint32_t slot, bool hot,
 // =====================================================================
 // ConsensusDWFA engine (consensus.rs:139-351)
 // =====================================================================
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) single_engine_kernel(EngineArgs A) {
+__global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) single_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
   Lo<Ctl>& ctl = *(Lo<Ctl>*)&ctl_lds;
@@ -1832,7 +1832,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
 // =====================================================================
 // DualConsensusDWFA engine (dual_consensus.rs:240-787)
 // =====================================================================
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
+__global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
   Lo<Ctl>& ctl = *(Lo<Ctl>*)&ctl_lds;
@@ -1919,7 +1919,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       // reached_all_end (dual_consensus.rs:1174-1195): per read, either side at its end
       {
         uint32_t ne = 0;
-        for (uint32_t r = tid; r < E.n; r += kBlock)
+        for (uint32_t r = tid; r < E.n; r += kEB)
           ne += (R0[r].e != kInactive && R0[r].end) || (tdual && R1[r].e != kInactive && R1[r].end);
         agg_add(&ctl.n_either, ne);
       }
@@ -1996,7 +1996,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
       if (tlen <= E.P.max_act && uni(ctl.am_len) == tlen + 1) {
         if (tid == 0) ctl.act_cnt = 0;
         __syncthreads();
-        for (uint32_t r = tid; r < E.n; r += kBlock)
+        for (uint32_t r = tid; r < E.n; r += kEB)
           if (E.ract[E.P.read_begin + r] == (int64_t)tlen) atomicAdd(&ctl.act_cnt, 1u);
         __syncthreads();
         nadd = uni(ctl.act_cnt);
@@ -2137,7 +2137,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WC_
   }
 }
 
-#ifndef WC_GLOBAL_STATE
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW)
 // =====================================================================
 // standalone DWFALite jobs (dynamic_wfa.rs:48-265): one wave per job
 // =====================================================================
@@ -2195,18 +2195,18 @@ __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
 #endif
 
 void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(single_engine_kernel, dim3(grid), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL(single_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(dual_engine_kernel, dim3(grid), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL(dual_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
 int engine_blocks_per_cu(uint32_t sides, size_t lds) {
   int nb = 0;
-  hipError_t e = sides == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kBlock, lds)
-                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kBlock, lds);
+  hipError_t e = sides == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kEB, lds)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kEB, lds);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
-#ifndef WC_GLOBAL_STATE
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW)
 void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s) {
   hipLaunchKernelGGL(dwfa_jobs_kernel, dim3(n), dim3(64), 0, s, jobs);
 }

@@ -22,6 +22,15 @@
 namespace WC_ENGINE_NS {
 using namespace ::wc;
 
+// threads per engine workgroup of this build (engine_narrow.hip: 128); the
+// LDS/HBM layouts (engine_shared.hpp) are sized for kBlock = 256, the widest
+#ifndef WC_BLOCK
+#define WC_BLOCK 256
+#endif
+constexpr int kEB = WC_BLOCK;
+constexpr int kEW = kEB / 64;
+static_assert(kEB % 64 == 0 && kEB <= kBlock, "engine workgroup size");
+
 // Explicit address spaces: HBM (global) and LDS pointers compile to global_* /
 // ds_* instructions instead of flat_* (which wait on both counters and take
 // the slower path). The engines keep every pointer in one of these types:

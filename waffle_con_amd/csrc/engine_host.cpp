@@ -21,6 +21,7 @@
 #include <deque>
 #include <memory>
 #include <numeric>
+#include <queue>
 #include <thread>
 
 #include "host_internal.hpp"
@@ -47,6 +48,7 @@ struct Caps {
   int per_cu = 1;
   uint64_t wsb = 0, ob = 0;
   bool gstate = false;  // search state in HBM (engine_gstate.hip): it does not fit LDS
+  bool narrow = false;  // 128-thread build (engine_narrow.hip)
   uint64_t gsb = 0;     // its bytes per workgroup
   uint32_t conc = 0;    // workgroups the HBM share was planned for
   bool pool_short = false;  // a retried item's node pool did not get its full growth
@@ -108,14 +110,22 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
     pcap = np;
   }
   if (lds_bytes(sides, pcap, nmax, chain) > kLdsMax) gstate = true;
+  // 128-thread workgroups for problems of <= 128 reads (engine_narrow.hip):
+  // (WC_NARROW=0: never, =1: the single engine only, default 2: both engines)
+  const char* nenv = getenv("WC_NARROW");
+  const int nmode = nenv ? atoi(nenv) : 2;
+  c.narrow = !gstate && nmax <= 128 && (sides == 1 ? nmode >= 1 : nmode >= 2);
+  auto occupancy = [&](size_t l) {
+    return c.narrow ? wcn::engine_blocks_per_cu(sides, l) : engine_blocks_per_cu(sides, l);
+  };
   // longer chains amortise the per-chain work (prediction, acceptance, the
   // literal pop between chains); take the longest one whose LDS still gives
   // the workgroups per CU of the default length (results do not depend on it)
   if (!chain_env && chain > 0 && !gstate) {
-    const int occ = engine_blocks_per_cu(sides, (size_t)lds_bytes(sides, pcap, nmax, chain));
+    const int occ = occupancy((size_t)lds_bytes(sides, pcap, nmax, chain));
     for (uint32_t k = chain + 1; k <= kChainMax; ++k) {
       const uint64_t l = lds_bytes(sides, pcap, nmax, k);
-      if (l > 60 * 1024 || engine_blocks_per_cu(sides, (size_t)l) < occ) break;
+      if (l > 60 * 1024 || occupancy((size_t)l) < occ) break;
       chain = k;
     }
   }
@@ -148,7 +158,7 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
   c.gstate = gstate;
   c.gsb = align16(lds_bytes(sides, pcap, nmax, chain));
   c.lds = gstate ? 0 : (size_t)c.gsb;
-  c.per_cu = gstate ? wcg::engine_blocks_per_cu(sides, 0) : engine_blocks_per_cu(sides, c.lds);
+  c.per_cu = gstate ? wcg::engine_blocks_per_cu(sides, 0) : occupancy(c.lds);
   c.wsb = ws_bytes(sides, pcap, nmax, c.wcap, c.lcap);
   c.ob = out_bytes(sides, c.rmax, nmax, c.lcap);
   return WC_OK;
@@ -204,6 +214,9 @@ static int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps
   if (caps.gstate) {
     if (caps.sides == 1) wcg::launch_single_engine(a, L.grid, 0, L.stream);
     else wcg::launch_dual_engine(a, L.grid, 0, L.stream);
+  } else if (caps.narrow) {
+    if (caps.sides == 1) wcn::launch_single_engine(a, L.grid, caps.lds, L.stream);
+    else wcn::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else {
     if (caps.sides == 1) launch_single_engine(a, L.grid, caps.lds, L.stream);
     else launch_dual_engine(a, L.grid, caps.lds, L.stream);
@@ -316,8 +329,8 @@ static int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
-            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
+    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
+            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
   return WC_OK;
 }
 
@@ -397,7 +410,8 @@ static int launch_finish(wc_ctx* ctx, Launch& L) {
 constexpr uint32_t kMaxAttempts = 8;
 
 int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, std::vector<SubProb>& items,
-               std::vector<EngineOut>& out, double& kernel_ms, uint64_t& launches) {
+               std::vector<EngineOut>& out, double& kernel_ms, uint64_t& launches,
+               const std::function<void(uint32_t)>* on_final) {
   out.resize(items.size());
   std::vector<uint32_t> pending;
   for (uint32_t i = 0; i < items.size(); ++i)
@@ -429,27 +443,49 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
     rc = launch_start(ctx, *L, b, cfg, items, run, caps);
     if (rc != WC_OK) return rc;
     const auto t1 = std::chrono::steady_clock::now();
+    // consume problems as their completion flags appear, while the launch
+    // runs: the result copies and on_final (the caller's result building)
+    // overlap the kernel instead of following it
+    std::vector<uint32_t> retry;
+    std::vector<uint8_t> got(L->P, 0);
+    uint32_t ngot = 0;
+    auto take = [&](uint32_t k) {
+      const uint32_t id = L->ids[k];
+      const uint32_t st = harvest(*L, k, items[id], out[id]);
+      if (st & ST_RETRY) {
+        bump(items[id], st);
+        if (items[id].attempts < kMaxAttempts) {
+          retry.push_back(id);
+          return;
+        }
+        out[id].status = WC_E_LIMIT;
+        out[id].error = retry_msg(st, items[id].attempts);
+      }
+      if (on_final) (*on_final)(id);
+    };
+    volatile uint32_t* done = L->done();
+    while (ngot < L->P) {
+      bool any = false;
+      for (uint32_t k = 0; k < L->P; ++k) {
+        if (got[k] || !__atomic_load_n(&done[k], __ATOMIC_ACQUIRE)) continue;
+        got[k] = 1;
+        ngot++;
+        any = true;
+        take(k);
+      }
+      if (any) continue;
+      if (hipStreamQuery(L->stream) != hipErrorNotReady) break;  // ended (or failed: launch_finish reports it)
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
     rc = launch_finish(ctx, *L);
     if (rc != WC_OK) return rc;
     const auto t2 = std::chrono::steady_clock::now();
     kernel_ms += L->kernel_ms;
     launches++;
-    std::vector<uint32_t> retry;
-    for (uint32_t k = 0; k < L->P; ++k) {
-      const uint32_t id = L->ids[k];
-      const uint32_t st = harvest(*L, k, items[id], out[id]);
-      if (st & ST_RETRY) {
-        bump(items[id], st);
-        if (items[id].attempts >= kMaxAttempts) {
-          out[id].status = WC_E_LIMIT;
-          out[id].error = retry_msg(st, items[id].attempts);
-        } else {
-          retry.push_back(id);
-        }
-      }
-    }
+    for (uint32_t k = 0; k < L->P; ++k)
+      if (!got[k]) take(k);
     if (getenv("WC_HOST_TIMING"))
-      fprintf(stderr, "[wc] launch: start %.3f ms, to completion %.3f ms (kernel %.3f), harvest %.3f ms\n",
+      fprintf(stderr, "[wc] launch: start %.3f ms, to completion %.3f ms (kernel %.3f), harvest after %.3f ms\n",
               std::chrono::duration<double, std::milli>(t1 - t0).count(),
               std::chrono::duration<double, std::milli>(t2 - t1).count(), L->kernel_ms,
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
@@ -558,51 +594,68 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   uint32_t beat = 0, finished = 0;
   const bool log = getenv("WC_LAUNCH_LOG") != nullptr;
   auto t_log = std::chrono::steady_clock::now();
+  // what is ready but not yet published, in publication order: continuations
+  // first, then the largest (reads x bases)
+  auto later = [&](uint32_t x, uint32_t y) {
+    if (items[x].cont != items[y].cont) return items[y].cont;
+    const double kx = (double)items[x].work * (double)items[x].gid.size();
+    const double ky = (double)items[y].work * (double)items[y].gid.size();
+    return kx != ky ? kx < ky : x > y;
+  };
+  std::priority_queue<uint32_t, std::vector<uint32_t>, decltype(later)> waiting(later);
   for (;;) {
     bool progress = false;
     if (log && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_log).count() > 10.0) {
       t_log = std::chrono::steady_clock::now();
       fprintf(stderr, "[wc] stream: %u published, %u finished, %u outstanding, %zu waiting\n",
-              (uint32_t)seq_item.size(), finished, outstanding, ready.size());
+              (uint32_t)seq_item.size(), finished, outstanding, ready.size() + waiting.size());
     }
     __atomic_store_n(&sc->heartbeat, ++beat, __ATOMIC_RELAXED);
-    // publish (largest first within what is ready now)
-    if (!ready.empty()) {
-      std::vector<uint32_t> batch(ready.begin(), ready.end());
-      ready.clear();
-      std::stable_sort(batch.begin(), batch.end(), [&](uint32_t x, uint32_t y) { return items[x].work > items[y].work; });
-      size_t k = 0;
-      for (; k < batch.size(); ++k) {
-        const uint32_t id = batch[k];
-        if (!live(id)) {
-          on_done(id, ~0u);  // dropped: its problem already failed
-          continue;
-        }
-        const SubProb& s = items[id];
-        const uint32_t seq = (uint32_t)seq_item.size();
-        const uint64_t ow = oldest < seq ? seq_rw[oldest] : rw;
-        if (seq - oldest >= kQcap || rw + s.gid.size() - ow > kQslots) break;  // ring full: later
-        DevProblem d;
-        memset(&d, 0, sizeof(d));
-        d.read_begin = (uint32_t)(rw % kQslots);
-        d.n_reads = (uint32_t)s.gid.size();
-        d.max_read_len = s.max_len;
-        d.n_active = s.n_active;
-        d.max_act = s.max_act;
-        qp[seq % kQcap] = d;
-        for (size_t r = 0; r < s.gid.size(); ++r) {
-          const uint64_t q = (rw + r) % kQslots;
-          qroff[q] = b->roff_h[s.gid[r]];
-          qract[q] = s.act[r];
-          qrlen[q] = b->rlen_h[s.gid[r]];
-        }
-        seq_item.push_back(id);
-        seq_rw.push_back(rw);
-        seq_done.push_back(0);
-        rw += s.gid.size();
-        outstanding++;
+    // publish. Workgroups claim in publication order, so the host keeps the
+    // order: at most a grid and a quarter of problems are published and
+    // unfinished at once; the rest wait here, continuations of started
+    // problems first (they are on those problems' critical paths), then the
+    // largest (reads x bases) first
+    const uint32_t backlog = L.grid + L.grid / 4;
+    while (!ready.empty()) {  // new arrivals into the host-side order
+      waiting.push(ready.front());
+      ready.pop_front();
+    }
+    bool published = false;
+    while (!waiting.empty() && outstanding < backlog) {
+      const uint32_t id = waiting.top();
+      if (!live(id)) {
+        waiting.pop();
+        on_done(id, ~0u);  // dropped: its problem already failed
+        continue;
       }
-      for (; k < batch.size(); ++k) ready.push_back(batch[k]);
+      const SubProb& s = items[id];
+      const uint32_t seq = (uint32_t)seq_item.size();
+      const uint64_t ow = oldest < seq ? seq_rw[oldest] : rw;
+      if (seq - oldest >= kQcap || rw + s.gid.size() - ow > kQslots) break;  // ring full: later
+      waiting.pop();
+      DevProblem d;
+      memset(&d, 0, sizeof(d));
+      d.read_begin = (uint32_t)(rw % kQslots);
+      d.n_reads = (uint32_t)s.gid.size();
+      d.max_read_len = s.max_len;
+      d.n_active = s.n_active;
+      d.max_act = s.max_act;
+      qp[seq % kQcap] = d;
+      for (size_t r = 0; r < s.gid.size(); ++r) {
+        const uint64_t q = (rw + r) % kQslots;
+        qroff[q] = b->roff_h[s.gid[r]];
+        qract[q] = s.act[r];
+        qrlen[q] = b->rlen_h[s.gid[r]];
+      }
+      seq_item.push_back(id);
+      seq_rw.push_back(rw);
+      seq_done.push_back(0);
+      rw += s.gid.size();
+      outstanding++;
+      published = true;
+    }
+    if (published) {
       std::atomic_thread_fence(std::memory_order_release);
       __atomic_store_n(&sc->tail, (uint32_t)seq_item.size(), __ATOMIC_RELEASE);
       progress = true;
@@ -622,7 +675,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
       on_done(id, st);
       progress = true;
     }
-    if (outstanding == 0 && ready.empty()) break;
+    if (outstanding == 0 && ready.empty() && waiting.empty()) break;
     if (progress) {
       t_idle = std::chrono::steady_clock::now();
       continue;
@@ -639,6 +692,10 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
       break;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  while (!waiting.empty()) {  // not published (an error ended the epoch)
+    ready.push_back(waiting.top());
+    waiting.pop();
   }
   __atomic_store_n(&sc->stop, 1u, __ATOMIC_RELEASE);
   const int frc = launch_finish(ctx, L);
@@ -743,6 +800,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
   std::vector<bool> alive(n, true);
   std::deque<uint32_t> ready, retry_ready;
 
+  bool roots_made = false;  // sub-problems made after the roots are continuations
   auto make = [&](uint32_t i, std::vector<uint8_t> inc, uint32_t level, std::vector<ConsRec> chain) {
     const wc_chain_problem& q = problems[i];
     const uint32_t id = (uint32_t)pool.size();
@@ -755,6 +813,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     subs.emplace_back();
     outs.emplace_back();
     SubProb& s = subs.back();
+    s.cont = roots_made;
     std::vector<int64_t> offs;
     for (uint32_t c = 0; c < q.n_chains; ++c) {
       if (!w.inc[c]) continue;
@@ -795,6 +854,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
       make(i, std::move(inc), 0, {});
     }
   }
+  roots_made = true;
 
   // pop finished tops in LIFO order (priority_consensus.rs:195-307); the
   // counters of a sub-problem are added when it is popped

@@ -205,13 +205,17 @@ int batch_run(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, wc
   double kms = 0;
   uint64_t nl = 0;
   const auto t1 = std::chrono::steady_clock::now();
-  int rc = run_engine(ctx, b, cfg, sides, items, outs, kms, nl);
-  if (rc != WC_OK) return rc;
-  const auto t2 = std::chrono::steady_clock::now();
-  for (uint32_t i = 0; i < n; ++i) {
+  std::vector<uint8_t> built(n, 0);
+  const std::function<void(uint32_t)> build = [&](uint32_t i) {
     if (sides == 1) build_single(outs[i], cfg.consensus_cost, R->probs[i]);
     else build_dual(outs[i], b->probs[i].n_reads, cfg.consensus_cost, R->probs[i]);
-  }
+    built[i] = 1;
+  };
+  int rc = run_engine(ctx, b, cfg, sides, items, outs, kms, nl, &build);
+  if (rc != WC_OK) return rc;
+  const auto t2 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0; i < n; ++i)
+    if (!built[i]) build(i);
   double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (getenv("WC_HOST_TIMING")) {
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
@@ -385,6 +389,42 @@ int wc_results_single(const wc_results* r, uint32_t p, uint32_t k, const uint8_t
   *seq_len = c.seq.size();
   *scores = c.scores.data();
   *n_scores = c.scores.size();
+  return WC_OK;
+}
+
+int wc_results_single_sizes(const wc_results* r, uint64_t* n_results, uint64_t* seq_bytes, uint64_t* n_scores) {
+  if (r->kind != 0) return WC_E_BAD_INPUT;
+  uint64_t nr = 0, sb = 0, ns = 0;
+  for (const ProbRes& p : r->probs)
+    for (const ConsRec& c : p.single) {
+      nr++;
+      sb += c.seq.size();
+      ns += c.scores.size();
+    }
+  *n_results = nr;
+  *seq_bytes = sb;
+  *n_scores = ns;
+  return WC_OK;
+}
+
+int wc_results_single_pack(const wc_results* r, int32_t* status, uint32_t* count, uint8_t* seq, uint64_t* seq_off,
+                           uint64_t* scores, uint64_t* score_off) {
+  if (r->kind != 0) return WC_E_BAD_INPUT;
+  uint64_t k = 0, so = 0, co = 0;
+  seq_off[0] = score_off[0] = 0;
+  for (size_t p = 0; p < r->probs.size(); ++p) {
+    const ProbRes& pr = r->probs[p];
+    status[p] = pr.status;
+    count[p] = (uint32_t)pr.single.size();
+    for (const ConsRec& c : pr.single) {
+      if (!c.seq.empty()) memcpy(seq + so, c.seq.data(), c.seq.size());
+      if (!c.scores.empty()) memcpy(scores + co, c.scores.data(), c.scores.size() * 8);
+      so += c.seq.size();
+      co += c.scores.size();
+      seq_off[++k] = so;
+      score_off[k] = co;
+    }
+  }
   return WC_OK;
 }
 

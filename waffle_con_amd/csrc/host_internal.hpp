@@ -6,6 +6,7 @@
 #include <array>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -25,6 +26,11 @@ void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hi
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 int engine_blocks_per_cu(uint32_t sides, size_t lds);
 }  // namespace wcg
+namespace wcn {  // engine_narrow.hip: 128-thread workgroups (problems of <= 128 reads)
+void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+int engine_blocks_per_cu(uint32_t sides, size_t lds);
+}  // namespace wcn
 
 // device buffer, grown on demand (never shrinks)
 struct DevBuf {
@@ -158,6 +164,7 @@ struct SubProb {
   std::vector<int64_t> act;
   uint32_t n_active = 0, max_act = 0, max_len = 0;
   uint64_t work = 0;
+  bool cont = false;  // PriorityConsensusDWFA: a later sub-problem of an already started problem
   // capacity growth earned by ST_RETRY outcomes (log2 multipliers)
   uint8_t wcap_x = 0, pcap_x = 0, lcap_x = 0, rmax_x = 0;
   uint32_t attempts = 0;
@@ -175,9 +182,12 @@ struct EngineOut {
 };
 
 // Runs `items` (all reads in batch `b`) to completion on the device, with
-// capacity retries; out[i] is item i's outcome.
+// capacity retries; out[i] is item i's outcome. on_final(i), if given, is
+// called once per item as soon as out[i] is final (possibly while the launch
+// still runs); items that fail before any launch are not reported to it.
 int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, std::vector<SubProb>& items,
-               std::vector<EngineOut>& out, double& kernel_ms, uint64_t& launches);
+               std::vector<EngineOut>& out, double& kernel_ms, uint64_t& launches,
+               const std::function<void(uint32_t)>* on_final = nullptr);
 
 // PriorityConsensusDWFA over many problems, streamed (engine_host.cpp).
 int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chain_problem* problems,
