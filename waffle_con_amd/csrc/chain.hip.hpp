@@ -199,10 +199,12 @@ struct Win {
 // The loads are unconditional (clamped into the window) so the eight LDS reads
 // issue back to back under one wait. Returns whether a tip inside the read lies
 // outside the window (the chain then stops before this step's node).
-__device__ __forceinline__ bool win_tip_bytes(const Win& W, const Front& f, uint32_t blen, uint32_t (&x)[kF]) {
+__device__ __forceinline__ bool win_tip_bytes(const Win& W, const Front& f, uint32_t blen, uint32_t kb,
+                                              uint32_t (&x)[kF]) {
   bool oob = false;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
+    if ((uint32_t)k >= kb) break;
     const uint32_t bo = f.fd[k] + f.e - f.fi[k];
     const uint32_t q = bo - W.wb;
     const bool in = q < 64u;
@@ -214,10 +216,12 @@ __device__ __forceinline__ bool win_tip_bytes(const Win& W, const Front& f, uint
 // DWFALite::update's extend for one appended symbol on the frontier
 // (thread_push<kLazy> semantics), comparing against the preloaded tip bytes.
 __device__ __forceinline__ bool chain_push(Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t old_len,
-                                           uint32_t sym, int wc, bool early, Gm<uint32_t>* row, uint32_t& cmp) {
+                                           uint32_t sym, int wc, bool early, Gm<uint32_t>* row, uint32_t kb,
+                                           uint32_t& cmp) {
   uint32_t c = f.nscmp, mb = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
+    if ((uint32_t)k >= kb) break;
     if (!(f.mask & (1u << k))) continue;
     const uint32_t d = f.fd[k];
     const uint32_t bo = d + f.e - f.fi[k];
@@ -244,12 +248,14 @@ __device__ __forceinline__ bool chain_push(Front& f, const uint32_t (&x)[kF], ui
 }
 // get_extension_candidates + reached_baseline_end of one read from its
 // frontier and the bytes at its tips (thread_nominate semantics).
-__device__ __forceinline__ Nom chain_nominate(const Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t len) {
+__device__ __forceinline__ Nom chain_nominate(const Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t len,
+                                          uint32_t kb) {
   uint32_t mb = f.maxb;
   uint64_t keys = 0;
   uint32_t cnts = 0, nk = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
+    if ((uint32_t)k >= kb) break;
     if (!(f.mask & (1u << k))) continue;
     const uint32_t bo = f.fd[k] + f.e - f.fi[k];
     mb = max(mb, bo);
@@ -359,8 +365,15 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   // this wave's share of the node cost; changes only when an edit distance grows
   uint64_t wcost = kFirst ? wave_sum_u64(active ? cost_of(f.e, cfg.cost_mode) : 0ull) : 0ull;
   uint32_t x[kF];  // bytes at the current tips
+  // frontier entries sit at mask bits below 32 - clz(mask) (entries only
+  // leave between rebuilds): kb, the wave's largest such bound, is a scalar
+  // loop bound for the per-entry work (typically 1-3 of the kF = 8 slots)
+  auto front_bound = [&]() {
+    return wave_max_u32(active && f.mask ? 32u - (uint32_t)__builtin_clz(f.mask) : 0u);
+  };
+  uint32_t kb = front_bound();
   {
-    const bool oob = win_tip_bytes(W, f, blen, x) && active;
+    const bool oob = win_tip_bytes(W, f, blen, kb, x) && active;
     if (kFirst && ballot(oob) && lane == 0) atomicMin(&ctl.chain_stop, 0u);
   }
   uint32_t nsym = uni((uint32_t)E.L.cpred[1]);
@@ -372,7 +385,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     uint32_t cmp = 0;
     bool heavy = false;
     SUB_T0(ta);
-    if (active) heavy = chain_push(f, x, blen, olen - 1, sym, wc, early, wf_row, cmp);
+    if (active) heavy = chain_push(f, x, blen, olen - 1, sym, wc, early, wf_row, kb, cmp);
     t_cmp += cmp;
     if (active && !heavy) {
       t_upd++;
@@ -420,12 +433,13 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     }
     SUB_T1(17, tb);
     SUB_T0(tc);
+    if (ballot(heavy)) kb = front_bound();  // rebuilt frontiers
     // bytes at the new tips: this node's nominations and the next push
-    const bool oob = win_tip_bytes(W, f, blen, x) && active;
+    const bool oob = win_tip_bytes(W, f, blen, kb, x) && active;
     Nom o;
     o.sym = o.occ = 0;
     o.n = o.split = o.end = 0;
-    if (active) o = chain_nominate(f, x, blen, olen);
+    if (active) o = chain_nominate(f, x, blen, olen, kb);
     SUB_T1(26, tc);
     SUB_T0(td);
     if (kFirst) {

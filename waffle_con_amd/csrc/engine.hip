@@ -1861,6 +1861,12 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
         if (ctl.heap_n == 0) {
           ctl.action = 2;
         } else {
+          // the node to pop is heap[0] already: its HBM-resident counts
+          // (processed per length of both trackers, active_min) are loaded
+          // first, under one wait, while the threshold walk and the sift run
+          const uint32_t plen = E.L.heap[0].len;
+          const uint32_t pc_pre[2] = {E.tracker(ctl, 0).processed(plen), E.tracker(ctl, 1).processed(plen)};
+          const uint64_t am_pre = plen < ctl.am_len ? E.active_min[plen] : 0;
           ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)ctl.heap_n);
           ctl.cnt[S_POPS]++;
           for (int k = 0; k < 2; ++k) {
@@ -1880,10 +1886,10 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
           ctl.top_len = top.len;
           ctl.top_cost = top.cost;
           ctl.top_dual = dual;
-          const uint64_t am = top.len < ctl.am_len ? E.active_min[top.len] : 0;
+          const uint64_t am = am_pre;
           const bool imbalanced = dual && (m.nsome[0] < am || m.nsome[1] < am);
           if (top.len >= ctl.am_len) ctl.status = WC_E_INVARIANT_CODE;
-          const bool at_cap = t.processed(top.len) >= t.cap;
+          const bool at_cap = pc_pre[dual] >= t.cap;
           if (top.cost > ctl.max_err || top.len < ctl.trk_thr[dual] || at_cap || imbalanced) {
             ctl.cnt[S_IGNORED]++;
             E.L.freestack[ctl.nfree++] = top.slot;

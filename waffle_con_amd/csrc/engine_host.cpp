@@ -59,7 +59,8 @@ struct Caps {
 // node-pool slots from the HBM share, linear-chain length from the LDS left at
 // the same occupancy. Retry outcomes raise them per item (log2 multipliers).
 static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vector<SubProb>& items,
-                     const std::vector<uint32_t>& ids, uint64_t hbm_budget, Caps& c, std::string& err) {
+                     const std::vector<uint32_t>& ids, uint64_t hbm_budget, Caps& c, std::string& err,
+                     uint32_t max_per_cu = 4) {
   uint32_t nmax = 1, maxlen = 1, wx = 0, px = 0, lx = 0, rx = 0;
   bool any_act = false;
   for (uint32_t id : ids) {
@@ -87,11 +88,13 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
   // at ~480 queued nodes), so the dual pool gets the launch's HBM share over
   // the workgroups that can run at once (16..256 MiB each).
   const uint64_t sb = slot_bytes(sides, nmax, c.wcap, c.lcap);
-  const uint64_t conc = std::max<uint64_t>(1, std::min<uint64_t>(ids.size(), 4ull * (uint64_t)ctx->n_cu));
+  const uint64_t conc = std::max<uint64_t>(1, std::min<uint64_t>(ids.size(), (uint64_t)max_per_cu * ctx->n_cu));
   const uint64_t per_wg = std::max<uint64_t>(16ull << 20, hbm_budget / conc);
   const uint64_t budget = sides == 1 ? (16ull << 20) : std::min<uint64_t>(256ull << 20, per_wg);
   const uint32_t pmax = sides == 1 ? 256u : 1024u;
-  const uint64_t lmax = sides == 1 ? 40 * 1024 : 48 * 1024;
+  uint64_t lmax = sides == 1 ? 40 * 1024 : 48 * 1024;
+  if (const char* e = getenv("WC_DUAL_LDS_KB"))  // experiment hook: LDS budget of the dual node pool
+    if (sides == 2) lmax = (uint64_t)atoi(e) * 1024;
   // WC_GSTATE=1 (test hook) forces the global-state build for every launch
   bool gstate = getenv("WC_GSTATE") != nullptr;
   uint32_t pcap = 16;
@@ -942,9 +945,17 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     Caps caps;
     std::string err;
     int prc = WC_OK;
+    bool widened = false;
     for (;;) {
       std::vector<uint32_t> ids(conc, 0);
-      prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(L->ws.cap, 0.8), caps, err);
+      prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(L->ws.cap, 0.8), caps, err, 8);
+      // a first epoch whose workgroups fit more than 4 per CU plans for all of them
+      if (prc == WC_OK && !widened && nretry == 0 && !caps.pool_short &&
+          (size_t)caps.per_cu * ctx->n_cu > conc) {
+        widened = true;
+        conc = (size_t)caps.per_cu * ctx->n_cu;
+        continue;
+      }
       if (prc != WC_OK || !caps.pool_short || conc <= std::max<size_t>(1, nretry)) break;
       conc = std::max<size_t>(std::max<size_t>(1, nretry), conc / 2);
     }

@@ -11,7 +11,8 @@
 #define WC_NARROW 1
 #define WC_BLOCK 128
 #define WC_ENGINE_NS wcn
-#ifndef WC_WAVES_PER_EU
-#define WC_WAVES_PER_EU 2
+#ifndef WC_NARROW_WAVES_PER_EU
+#define WC_NARROW_WAVES_PER_EU 2
 #endif
+#define WC_WAVES_PER_EU WC_NARROW_WAVES_PER_EU
 #include "engine.hip"
