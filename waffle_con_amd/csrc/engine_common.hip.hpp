@@ -29,6 +29,10 @@ using namespace ::wc;
 #endif
 constexpr int kEB = WC_BLOCK;
 constexpr int kEW = kEB / 64;
+// thread paths skip frontier slots past the lane's last live one; the
+// 256-thread build (128 VGPRs) spills more with the extra control flow than it
+// saves (cfg3 -6%), the 128-thread build has the registers (cfg5 +4%)
+constexpr bool kSlotBound = kEB <= 128;
 static_assert(kEB % 64 == 0 && kEB <= kBlock, "engine workgroup size");
 
 // Explicit address spaces: HBM (global) and LDS pointers compile to global_* /
@@ -637,9 +641,13 @@ template <class RB>
 __device__ inline Nom thread_nominate(const Front& f, RB rd, uint32_t blen, uint32_t len) {
   uint32_t mb = f.maxb;
   uint32_t tipsym[kF];
+  // live slots sit below 32 - clz(mask): the slots past it are skipped (for
+  // the whole wave when every lane's frontier is that short)
+  const uint32_t hi = f.mask ? 32u - (uint32_t)__builtin_clz(f.mask) : 0u;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
     tipsym[k] = 0x100;
+    if (kSlotBound && (uint32_t)k >= hi) continue;
     if (f.mask & (1u << k)) {
       const uint32_t bo = f.fd[k] + f.e - f.fi[k];
       mb = max(mb, bo);
@@ -650,6 +658,7 @@ __device__ inline Nom thread_nominate(const Front& f, RB rd, uint32_t blen, uint
   uint32_t cnts = 0, nk = 0;  // counts: 4-bit nibbles (<= kF tips)
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
+    if (kSlotBound && (uint32_t)k >= hi) break;
     const uint32_t s = tipsym[k];
     if (s == 0x100) continue;
     uint32_t j = 0;
@@ -716,9 +725,11 @@ template <bool kLazy = false, class RB>
 __device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_len, uint8_t sym, int wc,
                                    bool early, Gm<uint32_t>* wf_row, uint32_t& cmp) {
   uint32_t x[kF];
+  const uint32_t hi = f.mask ? 32u - (uint32_t)__builtin_clz(f.mask) : 0u;  // live slots: below hi
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
     x[k] = 0x100;
+    if (kSlotBound && (uint32_t)k >= hi) continue;
     if (f.mask & (1u << k)) {
       const uint32_t bo = f.fd[k] + f.e - f.fi[k];
       if (f.fd[k] + f.off == old_len && bo < blen) x[k] = rd(bo);
@@ -728,6 +739,7 @@ __device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_
   uint32_t mb = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
+    if (kSlotBound && (uint32_t)k >= hi) break;
     if (!(f.mask & (1u << k))) continue;
     const uint32_t d = f.fd[k];
     const uint32_t bo = d + f.e - f.fi[k];
