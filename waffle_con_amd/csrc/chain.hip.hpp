@@ -312,10 +312,10 @@ static_assert(kF == 8, "vote_unit covers split <= 8");
 // straight to the chain totals.
 __device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
                                              const Gm<uint8_t>* con, uint32_t olen, uint32_t sym, int wc, bool early,
-                                             uint32_t wcap, Lo<uint64_t>* tot) {
+                                             uint32_t wcap, Lo<uint64_t>* tot, Gm<uint32_t>* bak) {
   WaveCounters cnt = {0, 0, 0, 0, 0};
   uint32_t e_out = 0;
-  const bool ok = wave_heavy(tmp, wf, rd, blen, con, olen, (uint8_t)sym, wc, early, wcap, cnt, e_out);
+  const bool ok = wave_heavy(tmp, wf, rd, blen, con, olen, (uint8_t)sym, wc, early, wcap, cnt, e_out, bak);
   if (lane_id() == 0) {
     atomicAdd((unsigned long long*)&tot[0], (unsigned long long)cnt.updates);
     atomicAdd((unsigned long long*)&tot[1], (unsigned long long)cnt.w_out);
@@ -401,25 +401,22 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
       if (lane == l) front_store(tmp, f);
       wave_lds_sync();
       const uint32_t rl = (uint32_t)l * kEW + (uint32_t)wave;
+      const uint32_t e_in = uni(tmp->e);
+      Gm<uint32_t>* bdst = nullptr;
       if (kFirst && !((bak >> l) & 1ull)) {
-        // first rewrite of this row in the chain: keep a copy in slot S (the
-        // rows are otherwise only touched at frontier diagonals, which a
-        // rollback restores from the node's LDS RStates)
-        const uint32_t W0 = 2 * tmp->e + 1;
-        const Gm<uint32_t>* src = v.wf + (uint64_t)rl * E.wcap;
-        Gm<uint32_t>* dst = E.sv(S, 0).wf + (uint64_t)rl * E.wcap;
-        for (uint32_t i = lane; i < W0; i += 64) dst[i] = src[i];
+        // first rewrite of this row in the chain: chain_heavy keeps a copy in
+        // slot S (the rows are otherwise only touched at frontier diagonals,
+        // which a rollback restores from the node's LDS RStates)
+        bdst = E.sv(S, 0).wf + (uint64_t)rl * E.wcap;
         if (lane == 0) {
           const uint32_t k = atomicAdd(&ctl.chain_nbak, 1u);
           E.L.list[2 * k] = rl;
-          E.L.list[2 * k + 1] = W0;
+          E.L.list[2 * k + 1] = 2 * e_in + 1;
         }
         bak |= 1ull << l;
-        __threadfence_block();
       }
-      const uint32_t e_in = uni(tmp->e);
       const uint32_t e_out = chain_heavy(tmp, v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, olen,
-                                         sym, wc, early, E.wcap, ctl.chain_tot);
+                                         sym, wc, early, E.wcap, ctl.chain_tot, bdst);
       const bool ok = e_out != kInactive;
       wave_lds_sync();
       if (!ok && lane == 0) atomicMin(&ctl.chain_stop, j - 1);

@@ -855,10 +855,17 @@ __device__ inline void regs_rebuild(const uint32_t (&v)[kRegQ], uint32_t e, uint
 template <class P>
 __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
                                   const Gm<uint8_t>* con, uint32_t olen, uint8_t sym, int wc, bool early, uint32_t wcap, WaveCounters& cnt,
-                                  uint32_t& e_out) {
+                                  uint32_t& e_out, Gm<uint32_t>* bak = nullptr) {
+  // bak: a copy of the row as it is on entry goes there (the linear chain's
+  // rollback copy), from the registers the row is loaded into anyway
   const uint32_t flags = rsp->flags;
   uint32_t e = rsp->e;
   const uint32_t off = rsp->off;
+  if (bak && ((flags & kWide) || 2 * e + 3 > 64u * kRegQ)) {
+    for (uint32_t i = (uint32_t)lane_id(); i < 2 * e + 1; i += 64) bak[i] = wf[i];
+    bak = nullptr;
+    __builtin_amdgcn_wave_barrier();
+  }
   if (flags & kWide) {
     if (!wave_push_read(wf, e, off, rd, blen, con, olen, sym, wc, early, wcap, cnt)) return false;
     __builtin_amdgcn_wave_barrier();
@@ -870,6 +877,7 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
   uint32_t v[kRegQ];
   bool regs = W + 2 <= 64u * kRegQ;
   if (regs) regs_load(v, wf, W);
+  if (bak) regs_store(v, bak, W);
   do {
     if (W + 2 > wcap) return false;
     if (regs && W + 2 > 64u * kRegQ) {
