@@ -138,7 +138,7 @@ class Cfg2:
     """ConsensusDWFA throughput (BASELINE configs[1], north-star 1,000-locus form)."""
     name = "cfg2"
     scaling = "weak"
-    kernel = "wc::single_engine_kernel"
+    kernel = "wcn::single_engine_kernel"  # 128-thread build (<= 128 reads, engine_narrow.hip)
 
     def __init__(self, a, rank, world, ctx):
         import waffle_con_amd as w
@@ -327,7 +327,7 @@ class Cfg5:
     """PriorityConsensusDWFA over a fixed batch of cfg5 loci, strong-scaled."""
     name = "cfg5"
     scaling = "strong"
-    kernel = "wc::dual_engine_kernel"
+    kernel = "wcn::dual_engine_kernel"
 
     def __init__(self, a, rank, world, ctx):
         from waffle_con_amd import shard, synth
