@@ -377,6 +377,8 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     if (kFirst && ballot(oob) && lane == 0) atomicMin(&ctl.chain_stop, 0u);
   }
   uint32_t nsym = uni((uint32_t)E.L.cpred[1]);
+  uint64_t a_cost = 0, a_po = 0, a_ef = 0;  // kFirst: step (lane) aggregates of this wave
+  uint32_t jlast = 0;                       // last step this wave walked
   for (uint32_t j = 1; j <= K; ++j) {
     if (kFirst && j > uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
     const uint32_t sym = nsym;
@@ -496,16 +498,24 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
       else
         po = (uint64_t)wave_sum_u32(vp) | ((uint64_t)wave_sum_u32(vo) << 32);
       if (ballot(stop) && lane == 0) atomicMin(&ctl.chain_stop, j - 1);
-      if (lane == 0) {
-        auto& st = E.L.cstep[j];
-        atomicAdd((unsigned long long*)&st.cost, (unsigned long long)wcost);
-        atomicAdd((unsigned long long*)&st.po, (unsigned long long)po);
-        atomicAdd((unsigned long long*)&st.ef, (unsigned long long)(nend | nmul << 16 | nfrac << 32));
+      // lane j keeps step j's aggregates (j <= K < 64); they go to LDS once,
+      // after the walk, one atomic per aggregate for all steps at once
+      if ((uint32_t)lane == j) {
+        a_cost = wcost;
+        a_po = po;
+        a_ef = nend | nmul << 16 | nfrac << 32;
       }
+      jlast = j;
     } else if (j == K && has) {
       rinfo_store(&E.L.rinfo[r], o, f.e);
     }
     SUB_T1(18, tc);
+  }
+  if (kFirst && lane >= 1 && (uint32_t)lane <= jlast) {
+    auto& st = E.L.cstep[lane];
+    atomicAdd((unsigned long long*)&st.cost, (unsigned long long)a_cost);
+    atomicAdd((unsigned long long*)&st.po, (unsigned long long)a_po);
+    atomicAdd((unsigned long long*)&st.ef, (unsigned long long)a_ef);
   }
   if (active) front_flush(f, wf_row);  // lazy rows: write the final frontier
   if (has) {
