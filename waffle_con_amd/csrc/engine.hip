@@ -42,8 +42,15 @@ namespace WC_ENGINE_NS {
 #ifndef WC_WAVES_PER_EU
 #define WC_WAVES_PER_EU 4
 #endif
+// The 256-thread dual engine (problems of more than 128 reads) at 3 waves per
+// SIMD: 168 VGPRs (40 spilled instead of 62 at 128), 3 workgroups per CU;
+// cfg3 (768 loci of 200 reads) +9%, cfg4 +1% (tools/gpu_r02_dw.sh)
 #ifndef WC_DUAL_WAVES_PER_EU
+#ifdef WC_NARROW
 #define WC_DUAL_WAVES_PER_EU WC_WAVES_PER_EU
+#else
+#define WC_DUAL_WAVES_PER_EU 3
+#endif
 #endif
 
 constexpr int kMaxChild = 64;
