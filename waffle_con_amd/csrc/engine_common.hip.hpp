@@ -721,10 +721,11 @@ __device__ inline void thread_analyze(const Front& f, const Gm<uint8_t>* rd, uin
 // when a diagonal leaves the frontier; front_flush writes the final frontier.
 // Between the two, RState (not the row) is authoritative for frontier
 // diagonals, so the hot loop issues no global stores.
-template <bool kLazy = false, class RB>
-__device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_len, uint8_t sym, int wc,
-                                   bool early, Gm<uint32_t>* wf_row, uint32_t& cmp) {
-  uint32_t x[kF];
+// thread_push in two halves, so that several reads' (or sides') byte loads
+// can be in flight together: the tip bytes, then the update on them
+template <class RB>
+__device__ __forceinline__ void thread_tips(const Front& f, RB rd, uint32_t blen, uint32_t old_len,
+                                            uint32_t (&x)[kF]) {
   const uint32_t hi = f.mask ? 32u - (uint32_t)__builtin_clz(f.mask) : 0u;  // live slots: below hi
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
@@ -735,6 +736,11 @@ __device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_
       if (f.fd[k] + f.off == old_len && bo < blen) x[k] = rd(bo);
     }
   }
+}
+template <bool kLazy = false>
+__device__ __forceinline__ bool thread_apply(Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t old_len,
+                                             uint8_t sym, int wc, bool early, Gm<uint32_t>* wf_row, uint32_t& cmp) {
+  const uint32_t hi = f.mask ? 32u - (uint32_t)__builtin_clz(f.mask) : 0u;
   uint32_t c = f.nscmp;
   uint32_t mb = 0;
 #pragma unroll
@@ -764,6 +770,13 @@ __device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_
   mb = max(mb, f.maxb);
   cmp = c;
   return f.mask == 0 && !(early && mb == blen);
+}
+template <bool kLazy = false, class RB>
+__device__ inline bool thread_push(Front& f, RB rd, uint32_t blen, uint32_t old_len, uint8_t sym, int wc,
+                                   bool early, Gm<uint32_t>* wf_row, uint32_t& cmp) {
+  uint32_t x[kF];
+  thread_tips(f, rd, blen, old_len, x);
+  return thread_apply<kLazy>(f, x, blen, old_len, sym, wc, early, wf_row, cmp);
 }
 
 // write the frontier diagonals back into the wavefront row (end of a lazy walk)
