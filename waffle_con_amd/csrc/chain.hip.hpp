@@ -376,13 +376,98 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     const bool oob = win_tip_bytes(W, f, blen, kb, x) && active;
     if (kFirst && ballot(oob) && lane == 0) atomicMin(&ctl.chain_stop, 0u);
   }
-  uint32_t nsym = uni((uint32_t)E.L.cpred[1]);
+  // predicted symbols in a register: lane t holds N_t's symbol (t <= K + 1 < 64)
+  const uint32_t predv = (uint32_t)E.L.cpred[min((uint32_t)lane, K + 1)];
+  auto pred_at = [&](uint32_t t) { return (uint32_t)__builtin_amdgcn_readlane((int)predv, (int)t); };
+  // lane t: the predictions N_t .. N_t+7 packed (bytes past N_K+1 are never compared)
+  uint32_t plo = 0, phi = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u) {
+    plo |= (uint32_t)E.L.cpred[min((uint32_t)lane + u, 127u)] << (8 * u);
+    phi |= (uint32_t)E.L.cpred[min((uint32_t)lane + 4 + u, 127u)] << (8 * u);
+  }
   uint64_t a_cost = 0, a_po = 0, a_ef = 0;  // kFirst: step (lane) aggregates of this wave
   uint32_t jlast = 0;                       // last step this wave walked
+#ifdef WC_NO_FF
+  const bool ffon = false;
+#else
+  const bool ffon = wc < 0;  // a wildcard read byte matches but nominates itself: no quiet runs
+#endif
   for (uint32_t j = 1; j <= K; ++j) {
-    if (kFirst && j > uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
-    const uint32_t sym = nsym;
-    nsym = j < K ? uni((uint32_t)E.L.cpred[j + 1]) : 0x100u;  // issued early: used next step (and as `pred`)
+    const uint32_t stopv =
+        kFirst ? uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) : K;
+    if (kFirst && j > stopv) break;
+    // ---- quiet steps in bulk ----
+    // From step j, read r's pushes match for m steps when every live tip
+    // slot's read bytes equal the predictions N_j, N_j+1, ... (8-byte XOR +
+    // ctz against the LDS window); the first m - 1 of those steps then
+    // nominate exactly the next prediction with weight 1. Steps every read of
+    // the wave is quiet in are applied at once: tips advance, the counters
+    // grow by the per-step amounts, each step votes 840/840 per active read
+    // for its prediction and nothing else. Step K and every other step take
+    // the step path below.
+    if (ffon && j < K) {
+      uint32_t qn = 8;  // inactive lanes never limit the run
+      uint32_t nlive = 0;
+      if (active) {
+        qn = 0;
+        if (f.mask != 0 && f.maxb != blen) {
+          const uint64_t p8 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)plo, (int)j) |
+                              (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)phi, (int)j) << 32;
+          uint32_t m = min(8u, K - j + 1);
+          bool ok = true;
+#pragma unroll
+          for (int k = 0; k < kF; ++k) {
+            if ((uint32_t)k >= kb) break;
+            if (!(f.mask & (1u << k))) continue;
+            const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+            ok &= f.fd[k] + f.off == L0 + j - 1 && bo < blen;
+            const uint32_t q = bo - W.wb;
+            // 8 window bytes from q: three aligned dwords, funnel-shifted
+            // (the window slot is dword aligned; bytes past 64 are not used)
+            const Sh<uint32_t>* w32 = (const Sh<uint32_t>*)W.w + (min(q, 63u) >> 2);
+            const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2], sh = q & 3u;
+            const uint64_t r8 = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
+                                (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
+            const uint64_t mm = nz_bytes(r8 ^ p8);
+            const uint32_t t0 = mm ? (uint32_t)__builtin_ctzll(mm) >> 3 : 8u;
+            m = min(m, min(t0, min(blen - bo, q < 64u ? 64u - q : 0u)));
+            nlive++;
+          }
+          qn = ok && m >= 1 ? m - 1 : 0u;
+        }
+      }
+      uint32_t Q = 8u - wave_max_u32(8u - qn);
+      Q = min(Q, min(K - j, stopv - j));  // the step after the run is walked normally, and none past the stop
+      if (Q > 0) {
+        if (active) {
+#pragma unroll
+          for (int k = 0; k < kF; ++k) {
+            if ((uint32_t)k >= kb) break;
+            if (f.mask & (1u << k)) f.fd[k] += Q;
+          }
+          t_upd += Q;
+          t_wout += Q * (2 * f.e + 1);
+          t_cmp += Q * (f.nscmp + nlive);
+        }
+        if (kFirst) {
+          const uint64_t nact = (uint64_t)__popcll((unsigned long long)ballot(active));
+          if ((uint32_t)lane >= j && (uint32_t)lane < j + Q) {
+            a_cost = wcost;
+            a_po = (uint64_t)kVoteDen * nact;
+            a_ef = 0;
+          }
+          if (has)
+            for (uint32_t t = j; t < j + Q; ++t)
+              E.L.cnom[t * E.nmax + r] = (uint16_t)(active ? (kNomActive | kNomOne | pred_at(t + 1)) : 0u);
+          jlast = j + Q - 1;
+        }
+        j += Q;
+        win_tip_bytes(W, f, blen, kb, x);  // the tips moved (all inside the window)
+      }
+    }
+    const uint32_t sym = pred_at(j);
+    const uint32_t nsym = j < K ? pred_at(j + 1) : 0x100u;  // the next prediction (`pred` below)
     const uint32_t olen = L0 + j;
     uint32_t cmp = 0;
     bool heavy = false;

@@ -46,7 +46,7 @@ namespace WC_ENGINE_NS {
 // SIMD: 168 VGPRs (40 spilled instead of 62 at 128), 3 workgroups per CU;
 // cfg3 (768 loci of 200 reads) +9%, cfg4 +1% (tools/gpu_r02_dw.sh)
 #ifndef WC_DUAL_WAVES_PER_EU
-#ifdef WC_NARROW
+#if defined(WC_NARROW) || defined(WC_GLOBAL_STATE)
 #define WC_DUAL_WAVES_PER_EU WC_WAVES_PER_EU
 #else
 #define WC_DUAL_WAVES_PER_EU 3
