@@ -138,7 +138,7 @@ class Cfg2:
     """ConsensusDWFA throughput (BASELINE configs[1], north-star 1,000-locus form)."""
     name = "cfg2"
     scaling = "weak"
-    kernel = "wcn::single_engine_kernel"  # 128-thread build (<= 128 reads, engine_narrow.hip)
+    kernel = "wc::single_engine_kernel"
 
     def __init__(self, a, rank, world, ctx):
         import waffle_con_amd as w

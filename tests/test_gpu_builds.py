@@ -1,6 +1,6 @@
 """GPU parity of every engine build on the same problems: the 256-thread
-build (WC_NARROW=0), the 128-thread build (engine_narrow.hip, the default for
-problems of <= 128 reads) and the global-state build (WC_GSTATE). The build is
+build (WC_NARROW=0), the 128-thread build (engine_narrow.hip; WC_NARROW bit 0 =
+single engine, bit 1 = dual engine, default 2) and the global-state build (WC_GSTATE). The build is
 picked per launch from the environment (engine_host.cpp plan_caps), so one
 process exercises all of them. Sequences, scores and every work counter must
 equal the oracle's."""
@@ -16,8 +16,8 @@ hip = pytest.importorskip("hip_runner")
 
 KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored", "nodes_ignored",
         "peak_queue_size")
-BUILDS = {"wide": {"WC_NARROW": "0"}, "narrow-single": {"WC_NARROW": "1"}, "narrow": {"WC_NARROW": "2"},
-          "gstate": {"WC_GSTATE": "1"}}
+BUILDS = {"wide": {"WC_NARROW": "0"}, "narrow-single": {"WC_NARROW": "1"}, "narrow-dual": {"WC_NARROW": "2"},
+          "narrow": {"WC_NARROW": "3"}, "gstate": {"WC_GSTATE": "1"}}
 
 
 @pytest.fixture(params=sorted(BUILDS))

@@ -114,10 +114,12 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
   }
   if (lds_bytes(sides, pcap, nmax, chain) > kLdsMax) gstate = true;
   // 128-thread workgroups for problems of <= 128 reads (engine_narrow.hip):
-  // (WC_NARROW=0: never, =1: the single engine only, default 2: both engines)
+  // for the dual engine (WC_NARROW: bit 0 single engine, bit 1 dual engine;
+  // default 2). The single engine's chain walk is faster with 4 waves of
+  // fewer reads each: its quiet-step runs are longer (cfg2 34.4 vs 37.1 ms)
   const char* nenv = getenv("WC_NARROW");
   const int nmode = nenv ? atoi(nenv) : 2;
-  c.narrow = !gstate && nmax <= 128 && (sides == 1 ? nmode >= 1 : nmode >= 2);
+  c.narrow = !gstate && nmax <= 128 && (nmode & (sides == 1 ? 1 : 2)) != 0;
   auto occupancy = [&](size_t l) {
     return c.narrow ? wcn::engine_blocks_per_cu(sides, l) : engine_blocks_per_cu(sides, l);
   };
