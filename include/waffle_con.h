@@ -138,6 +138,12 @@ int wc_results_single(const wc_results* r, uint32_t p, uint32_t k, const uint8_t
  * back), seq_off[n_results + 1], scores[n_scores], score_off[n_results + 1],
  * results in problem order. */
 int wc_results_single_sizes(const wc_results* r, uint64_t* n_results, uint64_t* seq_bytes, uint64_t* n_scores);
+/* The same results without copies: pointers into arrays the result set owns
+ * (valid until wc_results_free): status[problems], count[problems], the
+ * sequence and score arenas, and per result (problem order) four u64: sequence
+ * start and length in `seq`, scores start and length in `scores`. */
+int wc_results_single_view(wc_results* r, const int32_t** status, const uint32_t** count, const uint8_t** seq,
+                           const uint64_t** scores, const uint64_t** index);
 int wc_results_single_pack(const wc_results* r, int32_t* status, uint32_t* count, uint8_t* seq, uint64_t* seq_off,
                            uint64_t* scores, uint64_t* score_off);
 

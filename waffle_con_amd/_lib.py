@@ -112,7 +112,7 @@ EXPORTED = (
     "wc_consensus_batch", "wc_dual_consensus_batch", "wc_priority_consensus_batch",
     "wc_batch_create", "wc_batch_refill", "wc_batch_free", "wc_batch_bytes", "wc_batch_consensus", "wc_batch_dual_consensus",
     "wc_results_free", "wc_results_problems", "wc_results_status", "wc_results_error",
-    "wc_results_count", "wc_results_single", "wc_results_single_sizes", "wc_results_single_pack", "wc_results_dual", "wc_results_chain_len",
+    "wc_results_count", "wc_results_single", "wc_results_single_sizes", "wc_results_single_pack", "wc_results_single_view", "wc_results_dual", "wc_results_chain_len",
     "wc_results_chain", "wc_results_sequence_indices", "wc_results_stats",
     "wc_results_problem_stats", "wc_dwfa_batch", "wc_generate_test", "wc_gen_consensus",
     "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_wfa_ed_batch", "wc_rng_words", "wc_rng_stdrng_chain",
@@ -164,6 +164,9 @@ def lib():
         u64p = ctypes.POINTER(ctypes.c_uint64)
         L.wc_results_single_sizes.argtypes = [vp, u64p, u64p, u64p]
         L.wc_results_single_pack.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.wc_results_single_view.argtypes = [vp, ctypes.POINTER(ctypes.POINTER(ctypes.c_int32)),
+                                             ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)), ctypes.POINTER(_u8p),
+                                             ctypes.POINTER(u64p), ctypes.POINTER(u64p)]
         L.wc_results_dual.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(WcDualView)]
         L.wc_results_chain_len.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32]
         L.wc_results_chain_len.restype = ctypes.c_uint32

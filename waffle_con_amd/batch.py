@@ -48,11 +48,8 @@ class ResidentBatch:
         rc = L.wc_batch_consensus(ctx.handle, self.handle, ctypes.byref(cfg), ctypes.byref(res))
         if rc != _lib.WC_OK:
             raise _lib.WaffleConError("wc_batch_consensus failed: " + ctx.last_error(), rc)
-        try:
-            out = _single_results(res, len(self._batch), config.consensus_cost, L, return_errors)
-            return out, _stats(res, L, per_problem)
-        finally:
-            L.wc_results_free(res)
+        stats = _stats(res, L, per_problem)
+        return _single_results(res, len(self._batch), config.consensus_cost, L, return_errors), stats
 
     def dual_consensus(self, config=None, return_errors=True, context=None, per_problem=False):
         config = config or CdwfaConfig()

@@ -13,9 +13,9 @@ from .cdwfa_config import CdwfaConfig, ConsensusCost
 
 
 class Consensus:
-    """consensus.rs:42-74. Results of a batch call share one packed host
-    buffer (wc_results_single_pack); each Consensus unpacks its own sequence
-    and scores from it into Python objects on first access."""
+    """consensus.rs:42-74. Results of a batch call stay in the library's
+    result arenas (wc_results_single_view); each Consensus unpacks its own
+    sequence and scores from them into Python objects on first access."""
     __slots__ = ("_sequence", "_consensus_cost", "_scores", "_src")
 
     def __init__(self, sequence, consensus_cost, scores):
@@ -26,8 +26,8 @@ class Consensus:
 
     @classmethod
     def _packed(cls, pack, j, consensus_cost):
-        """Result j of a packed result set pack = (seq u8 array, seq offsets,
-        scores u64 array, score offsets)."""
+        """Result j of a result set viewed in place: pack = (sequence arena,
+        per-result [seq start, len, scores start, len] list, score arena, owner)."""
         c = cls.__new__(cls)
         c._sequence = c._scores = None
         c._consensus_cost = consensus_cost
@@ -35,9 +35,10 @@ class Consensus:
         return c
 
     def _unpack(self):
-        (seq, so, sc, co), j = self._src
-        self._sequence = seq[so[j]:so[j + 1]].tobytes()
-        self._scores = sc[co[j]:co[j + 1]].tolist()
+        (seq, idx, sc, _owner), j = self._src
+        a, la, c, lc = idx[4 * j:4 * j + 4]
+        self._sequence = seq[a:a + la].tobytes()
+        self._scores = sc[c:c + lc].tolist()
         self._src = None
 
     def sequence(self):
@@ -68,23 +69,40 @@ def _raise_for(results, p, L):
         raise _lib.WaffleConError(L.wc_results_error(results, p).decode(), st)
 
 
+class _Owned:
+    """Keeps a result set alive while Consensus objects still view its arenas."""
+    __slots__ = ("handle",)
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def __del__(self):
+        try:
+            _lib.lib().wc_results_free(self.handle)
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
+            pass
+
+
 def _single_results(res, n, cost, L, return_errors):
-    """Per problem: a list of Consensus, or its WaffleConError. Everything
-    comes out of the library in one wc_results_single_pack call."""
+    """Per problem: a list of Consensus, or its WaffleConError. The results
+    stay in the library's arenas (wc_results_single_view, no copy); takes
+    ownership of `res` (freed when no Consensus refers to it any more)."""
+    owner = _Owned(res)
     u64 = ctypes.c_uint64
     nr, sb, ns = u64(), u64(), u64()
     if L.wc_results_single_sizes(res, ctypes.byref(nr), ctypes.byref(sb), ctypes.byref(ns)) != _lib.WC_OK:
         raise _lib.WaffleConError("wc_results_single_sizes: not a single-consensus result set", _lib.WC_E_BAD_INPUT)
-    status = np.zeros(max(n, 1), np.int32)
-    count = np.zeros(max(n, 1), np.uint32)
-    seq = np.empty(max(sb.value, 1), np.uint8)
-    soff = np.empty(nr.value + 1, np.uint64)
-    sc = np.empty(max(ns.value, 1), np.uint64)
-    coff = np.empty(nr.value + 1, np.uint64)
-    L.wc_results_single_pack(res, status.ctypes.data, count.ctypes.data, seq.ctypes.data, soff.ctypes.data,
-                             sc.ctypes.data, coff.ctypes.data)
-    so, co, cnt, st = soff.tolist(), coff.tolist(), count.tolist(), status.tolist()
-    pack = (seq, so, sc, co)
+    st_p, cnt_p = ctypes.POINTER(ctypes.c_int32)(), ctypes.POINTER(ctypes.c_uint32)()
+    seq_p, sc_p, idx_p = _lib._u8p(), ctypes.POINTER(u64)(), ctypes.POINTER(u64)()
+    L.wc_results_single_view(res, ctypes.byref(st_p), ctypes.byref(cnt_p), ctypes.byref(seq_p), ctypes.byref(sc_p),
+                             ctypes.byref(idx_p))
+    as_np = np.ctypeslib.as_array
+    seq = as_np(seq_p, shape=(max(sb.value, 1),))
+    sc = as_np(sc_p, shape=(max(ns.value, 1),))
+    idx = as_np(idx_p, shape=(max(4 * nr.value, 1),)).tolist()
+    st = as_np(st_p, shape=(max(n, 1),)).tolist()
+    cnt = as_np(cnt_p, shape=(max(n, 1),)).tolist()
+    pack = (seq, idx, sc, owner)
     out, k = [], 0
     mk = Consensus._packed
     for p in range(n):
@@ -145,11 +163,8 @@ def consensus_batch(problems, config=None, context=None, return_errors=False):
     rc = L.wc_consensus_batch(ctx.handle, ctypes.byref(cfg), len(batch), arr, ctypes.byref(res))
     if rc != _lib.WC_OK:
         raise _lib.WaffleConError("wc_consensus_batch failed: " + ctx.last_error(), rc)
-    try:
-        out = _single_results(res, len(batch), config.consensus_cost, L, return_errors)
-        return out, _stats(res, L)
-    finally:
-        L.wc_results_free(res)
+    stats = _stats(res, L)
+    return _single_results(res, len(batch), config.consensus_cost, L, return_errors), stats
 
 
 class ConsensusDWFA:

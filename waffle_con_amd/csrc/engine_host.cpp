@@ -1096,6 +1096,16 @@ void fill_stats(wc_results* R, double kernel_ms, uint64_t launches, double wall_
 }
 
 // consensus.rs:345 — single results sorted by sequence
+void pack_single(wc_results* R, uint32_t p) {
+  const ProbRes& pr = R->probs[p];
+  R->p_seq0[p] = R->a_seq.size();
+  R->p_sc0[p] = R->a_sc.size();
+  for (const ConsRec& c : pr.single) {
+    R->a_seq.insert(R->a_seq.end(), c.seq.begin(), c.seq.end());
+    R->a_sc.insert(R->a_sc.end(), c.scores.begin(), c.scores.end());
+  }
+}
+
 void build_single(const EngineOut& E, int mode, ProbRes& pr) {
   for (int s = 0; s < S_NSTAT; ++s) pr.stats[s] = E.stats[s];
   pr.status = E.status;

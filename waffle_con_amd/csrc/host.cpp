@@ -206,9 +206,20 @@ int batch_run(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, wc
   uint64_t nl = 0;
   const auto t1 = std::chrono::steady_clock::now();
   std::vector<uint8_t> built(n, 0);
+  if (sides == 1) {
+    uint64_t guess = 0;
+    for (uint32_t i = 0; i < n; ++i) guess += b->probs[i].max_len + b->probs[i].max_len / 16;
+    R->a_seq.reserve(guess);
+    R->p_seq0.assign(n, ~0ull);
+    R->p_sc0.assign(n, ~0ull);
+  }
   const std::function<void(uint32_t)> build = [&](uint32_t i) {
-    if (sides == 1) build_single(outs[i], cfg.consensus_cost, R->probs[i]);
-    else build_dual(outs[i], b->probs[i].n_reads, cfg.consensus_cost, R->probs[i]);
+    if (sides == 1) {
+      build_single(outs[i], cfg.consensus_cost, R->probs[i]);
+      pack_single(R, i);
+    } else {
+      build_dual(outs[i], b->probs[i].n_reads, cfg.consensus_cost, R->probs[i]);
+    }
     built[i] = 1;
   };
   int rc = run_engine(ctx, b, cfg, sides, items, outs, kms, nl, &build);
@@ -425,6 +436,44 @@ int wc_results_single_pack(const wc_results* r, int32_t* status, uint32_t* count
       score_off[k] = co;
     }
   }
+  return WC_OK;
+}
+
+int wc_results_single_view(wc_results* r, const int32_t** status, const uint32_t** count, const uint8_t** seq,
+                           const uint64_t** scores, const uint64_t** index) {
+  if (r->kind != 0) return WC_E_BAD_INPUT;
+  if (!r->view_ready) {
+    const uint32_t n = (uint32_t)r->probs.size();
+    if (r->p_seq0.size() != n) {
+      r->p_seq0.assign(n, ~0ull);
+      r->p_sc0.assign(n, ~0ull);
+    }
+    for (uint32_t p = 0; p < n; ++p)
+      if (r->p_seq0[p] == ~0ull) pack_single(r, p);
+    r->v_status.resize(std::max<size_t>(n, 1));
+    r->v_count.resize(std::max<size_t>(n, 1));
+    r->v_idx.clear();
+    for (uint32_t p = 0; p < n; ++p) {
+      const ProbRes& pr = r->probs[p];
+      r->v_status[p] = pr.status;
+      r->v_count[p] = (uint32_t)pr.single.size();
+      uint64_t so = r->p_seq0[p], co = r->p_sc0[p];
+      for (const ConsRec& c : pr.single) {
+        r->v_idx.insert(r->v_idx.end(), {so, (uint64_t)c.seq.size(), co, (uint64_t)c.scores.size()});
+        so += c.seq.size();
+        co += c.scores.size();
+      }
+    }
+    if (r->a_seq.empty()) r->a_seq.push_back(0);
+    if (r->a_sc.empty()) r->a_sc.push_back(0);
+    if (r->v_idx.empty()) r->v_idx.push_back(0);
+    r->view_ready = true;
+  }
+  *status = r->v_status.data();
+  *count = r->v_count.data();
+  *seq = r->a_seq.data();
+  *scores = r->a_sc.data();
+  *index = r->v_idx.data();
   return WC_OK;
 }
 

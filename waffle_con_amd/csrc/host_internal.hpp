@@ -139,7 +139,18 @@ struct wc_results {
   int kind = 0;  // 0 single, 1 dual, 2 priority
   std::vector<ProbRes> probs;
   wc_stats stats;
+  // single-consensus results in two arenas (wc_results_single_view): the
+  // batch path fills them as problems finish (while the kernel runs), in
+  // finishing order; the per-result index below is in problem order
+  std::vector<uint8_t> a_seq;
+  std::vector<uint64_t> a_sc;
+  std::vector<uint64_t> p_seq0, p_sc0;  // per problem: arena start of its first result (~0 = not packed)
+  std::vector<int32_t> v_status;
+  std::vector<uint32_t> v_count;
+  std::vector<uint64_t> v_idx;  // per result: seq start, seq len, scores start, scores len
+  bool view_ready = false;
 };
+
 
 struct RawRecord {
   uint32_t len[2] = {0, 0};
@@ -196,6 +207,8 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
 void destroy_launches(wc_ctx* ctx);
 bool dual_from_record(const RawRecord& rr, uint32_t n, int mode, DualRec& d);
 void build_single(const EngineOut& E, int mode, ProbRes& pr);
+// appends problem p's single results to the arenas (wc_results::a_seq/a_sc)
+void pack_single(wc_results* R, uint32_t p);
 void build_dual(const EngineOut& E, uint32_t n, int mode, ProbRes& pr);
 void fill_stats(wc_results* R, double kernel_ms, uint64_t launches, double wall_ms);
 }  // namespace wch
