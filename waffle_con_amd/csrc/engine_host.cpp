@@ -943,7 +943,14 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     // item's node pool outgrows that share, the epoch runs fewer workgroups
     // (halving, down to one per retried item) so that each gets more HBM
     const size_t nretry = std::count_if(ready.begin(), ready.end(), [&](uint32_t id) { return subs[id].attempts > 0; });
-    size_t conc = 4 * ctx->n_cu;
+    // a problem rarely has more than a few sub-problems runnable at once (the
+    // groups of one split level): a few loci get a few workgroups with large
+    // node pools, not a full chip of small ones (cfg4: one locus; allocating
+    // pools for 768 workgroups cost seconds per epoch)
+    size_t live = 0;
+    for (uint32_t i = 0; i < n; ++i) live += alive[i] && !stacks[i].empty();
+    const size_t conc_cap = std::max<size_t>(std::max<size_t>(1, nretry), 8 * live);
+    size_t conc = std::min<size_t>(4 * ctx->n_cu, conc_cap);
     Caps caps;
     std::string err;
     int prc = WC_OK;
@@ -953,9 +960,9 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
       prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(L->ws.cap, 0.8), caps, err, 8);
       // a first epoch whose workgroups fit more than 4 per CU plans for all of them
       if (prc == WC_OK && !widened && nretry == 0 && !caps.pool_short &&
-          (size_t)caps.per_cu * ctx->n_cu > conc) {
+          std::min<size_t>((size_t)caps.per_cu * ctx->n_cu, conc_cap) > conc) {
         widened = true;
-        conc = (size_t)caps.per_cu * ctx->n_cu;
+        conc = std::min<size_t>((size_t)caps.per_cu * ctx->n_cu, conc_cap);
         continue;
       }
       if (prc != WC_OK || !caps.pool_short || conc <= std::max<size_t>(1, nretry)) break;
