@@ -1,6 +1,8 @@
 """GPU parity of every engine build on the same problems: the 256-thread
-build (WC_NARROW=0), the 128-thread build (engine_narrow.hip; WC_NARROW bit 0 =
-single engine, bit 1 = dual engine, default 2) and the global-state build (WC_GSTATE). The build is
+build at 4 waves/SIMD (WC_NARROW=0 WC_LOWLAT=0), the same at 2 waves/SIMD
+(engine_lowlat.hip, the default for launches of at most 2 problems per CU),
+the 128-thread build (engine_narrow.hip; WC_NARROW bit 0 = single engine,
+bit 1 = dual engine, default 2) and the global-state build (WC_GSTATE). The build is
 picked per launch from the environment (engine_host.cpp plan_caps), so one
 process exercises all of them. Sequences, scores and every work counter must
 equal the oracle's."""
@@ -16,13 +18,14 @@ hip = pytest.importorskip("hip_runner")
 
 KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored", "nodes_ignored",
         "peak_queue_size")
-BUILDS = {"wide": {"WC_NARROW": "0"}, "narrow-single": {"WC_NARROW": "1"}, "narrow-dual": {"WC_NARROW": "2"},
-          "narrow": {"WC_NARROW": "3"}, "gstate": {"WC_GSTATE": "1"}}
+BUILDS = {"wide": {"WC_NARROW": "0", "WC_LOWLAT": "0"}, "lowlat": {"WC_NARROW": "0"},
+          "narrow-single": {"WC_NARROW": "1"}, "narrow-dual": {"WC_NARROW": "2"}, "narrow": {"WC_NARROW": "3"},
+          "gstate": {"WC_GSTATE": "1"}}
 
 
 @pytest.fixture(params=sorted(BUILDS))
 def build(request):
-    old = {k: os.environ.get(k) for k in ("WC_NARROW", "WC_GSTATE")}
+    old = {k: os.environ.get(k) for k in ("WC_NARROW", "WC_GSTATE", "WC_LOWLAT")}
     for k in old:
         os.environ.pop(k, None)
     os.environ.update(BUILDS[request.param])

@@ -2150,7 +2150,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
   }
 }
 
-#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW)
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT)
 // =====================================================================
 // standalone DWFALite jobs (dynamic_wfa.rs:48-265): one wave per job
 // =====================================================================
@@ -2219,7 +2219,7 @@ int engine_blocks_per_cu(uint32_t sides, size_t lds) {
                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kEB, lds);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
-#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW)
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT)
 void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s) {
   hipLaunchKernelGGL(dwfa_jobs_kernel, dim3(n), dim3(64), 0, s, jobs);
 }

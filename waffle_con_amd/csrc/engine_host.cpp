@@ -49,6 +49,7 @@ struct Caps {
   uint64_t wsb = 0, ob = 0;
   bool gstate = false;  // search state in HBM (engine_gstate.hip): it does not fit LDS
   bool narrow = false;  // 128-thread build (engine_narrow.hip)
+  bool lowlat = false;  // 256-thread build at 2 waves/SIMD (engine_lowlat.hip)
   uint64_t gsb = 0;     // its bytes per workgroup
   uint32_t conc = 0;    // workgroups the HBM share was planned for
   bool pool_short = false;  // a retried item's node pool did not get its full growth
@@ -120,8 +121,13 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
   const char* nenv = getenv("WC_NARROW");
   const int nmode = nenv ? atoi(nenv) : 2;
   c.narrow = !gstate && nmax <= 128 && (nmode & (sides == 1 ? 1 : 2)) != 0;
+  // a launch of at most 2 problems per CU gets the 2-wave register budget
+  // (no spills: each workgroup's latency is what counts); WC_LOWLAT=0 disables
+  const char* lenv = getenv("WC_LOWLAT");
+  c.lowlat = !gstate && !c.narrow && ids.size() <= 2ull * (uint64_t)ctx->n_cu && !(lenv && atoi(lenv) == 0);
   auto occupancy = [&](size_t l) {
-    return c.narrow ? wcn::engine_blocks_per_cu(sides, l) : engine_blocks_per_cu(sides, l);
+    return c.narrow ? wcn::engine_blocks_per_cu(sides, l)
+                    : (c.lowlat ? wcl::engine_blocks_per_cu(sides, l) : engine_blocks_per_cu(sides, l));
   };
   // longer chains amortise the per-chain work (prediction, acceptance, the
   // literal pop between chains); take the longest one whose LDS still gives
@@ -222,6 +228,9 @@ static int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps
   } else if (caps.narrow) {
     if (caps.sides == 1) wcn::launch_single_engine(a, L.grid, caps.lds, L.stream);
     else wcn::launch_dual_engine(a, L.grid, caps.lds, L.stream);
+  } else if (caps.lowlat) {
+    if (caps.sides == 1) wcl::launch_single_engine(a, L.grid, caps.lds, L.stream);
+    else wcl::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else {
     if (caps.sides == 1) launch_single_engine(a, L.grid, caps.lds, L.stream);
     else launch_dual_engine(a, L.grid, caps.lds, L.stream);
@@ -334,8 +343,8 @@ static int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
-            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
+    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
+            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
   return WC_OK;
 }
 
@@ -584,8 +593,9 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u\n", L.grid,
-            caps.per_cu, caps.lds, caps.pcap, caps.wcap, caps.lcap, caps.nmax, caps.rmax);
+    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u narrow=%d lowlat=%d\n",
+            L.grid, caps.per_cu, caps.lds, caps.pcap, caps.wcap, caps.lcap, caps.nmax, caps.rmax, (int)caps.narrow,
+            (int)caps.lowlat);
 
   // publication state: seq -> item, read-ring position; incomplete seqs in order
   std::vector<uint32_t> seq_item;

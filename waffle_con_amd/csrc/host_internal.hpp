@@ -31,6 +31,11 @@ void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hi
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 int engine_blocks_per_cu(uint32_t sides, size_t lds);
 }  // namespace wcn
+namespace wcl {  // engine_lowlat.hip: 256-thread workgroups at 2 waves/SIMD (launches with few problems)
+void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+int engine_blocks_per_cu(uint32_t sides, size_t lds);
+}  // namespace wcl
 
 // device buffer, grown on demand (never shrinks)
 struct DevBuf {
