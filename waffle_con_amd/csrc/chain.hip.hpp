@@ -191,6 +191,14 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
 
 // ---- thread-level step primitives over the LDS read window ----
 // A thread's read window: 64 bytes of its read staged in LDS from wb.
+// the bytes at a read's (up to kF) tips, packed four to a register (the walk
+// keeps them live across its loop; eight registers of them spilled)
+struct TipBytes {
+  uint32_t lo, hi;
+  __device__ __forceinline__ uint32_t at(int k) const {
+    return k < 4 ? (lo >> (8 * k)) & 0xFFu : (hi >> (8 * (k - 4))) & 0xFFu;
+  }
+};
 struct Win {
   const Sh<uint8_t>* w;
   uint32_t wb;
@@ -200,7 +208,8 @@ struct Win {
 // issue back to back under one wait. Returns whether a tip inside the read lies
 // outside the window (the chain then stops before this step's node).
 __device__ __forceinline__ bool win_tip_bytes(const Win& W, const Front& f, uint32_t blen, uint32_t kb,
-                                              uint32_t (&x)[kF]) {
+                                              TipBytes& x) {
+  uint32_t b[kF];
   bool oob = false;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
@@ -208,14 +217,21 @@ __device__ __forceinline__ bool win_tip_bytes(const Win& W, const Front& f, uint
     const uint32_t bo = f.fd[k] + f.e - f.fi[k];
     const uint32_t q = bo - W.wb;
     const bool in = q < 64u;
-    x[k] = W.w[in ? q : 0u];
+    b[k] = W.w[in ? q : 0u];
     oob |= ((f.mask >> k) & 1u) && !in && bo < blen;
+  }
+  x.lo = x.hi = 0;
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    if ((uint32_t)k >= kb) break;
+    if (k < 4) x.lo |= b[k] << (8 * k);
+    else x.hi |= b[k] << (8 * (k - 4));
   }
   return oob;
 }
 // DWFALite::update's extend for one appended symbol on the frontier
 // (thread_push<kLazy> semantics), comparing against the preloaded tip bytes.
-__device__ __forceinline__ bool chain_push(Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t old_len,
+__device__ __forceinline__ bool chain_push(Front& f, const TipBytes& x, uint32_t blen, uint32_t old_len,
                                            uint32_t sym, int wc, bool early, Gm<uint32_t>* row, uint32_t kb,
                                            uint32_t& cmp) {
   uint32_t c = f.nscmp, mb = 0;
@@ -228,7 +244,7 @@ __device__ __forceinline__ bool chain_push(Front& f, const uint32_t (&x)[kF], ui
     if (d + f.off == old_len) {
       if (bo < blen) {
         c++;
-        if (x[k] == sym || (wc >= 0 && x[k] == (uint32_t)(uint8_t)wc)) {
+        if (x.at(k) == sym || (wc >= 0 && x.at(k) == (uint32_t)(uint8_t)wc)) {
           f.fd[k] = d + 1;
           mb = max(mb, bo + 1);
           continue;
@@ -248,7 +264,7 @@ __device__ __forceinline__ bool chain_push(Front& f, const uint32_t (&x)[kF], ui
 }
 // get_extension_candidates + reached_baseline_end of one read from its
 // frontier and the bytes at its tips (thread_nominate semantics).
-__device__ __forceinline__ Nom chain_nominate(const Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t len,
+__device__ __forceinline__ Nom chain_nominate(const Front& f, const TipBytes& x, uint32_t blen, uint32_t len,
                                           uint32_t kb) {
   uint32_t mb = f.maxb;
   uint64_t keys = 0;
@@ -260,7 +276,7 @@ __device__ __forceinline__ Nom chain_nominate(const Front& f, const uint32_t (&x
     const uint32_t bo = f.fd[k] + f.e - f.fi[k];
     mb = max(mb, bo);
     if (!(f.fd[k] + f.off == len && bo < blen)) continue;
-    const uint32_t s = x[k];
+    const uint32_t s = x.at(k);
     uint32_t j = 0;
     while (j < nk && byte_at(keys, j) != s) ++j;
     if (j == nk) {
@@ -364,7 +380,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   uint64_t bak = 0;  // lanes whose row was backed up (wave-uniform)
   // this wave's share of the node cost; changes only when an edit distance grows
   uint64_t wcost = kFirst ? wave_sum_u64(active ? cost_of(f.e, cfg.cost_mode) : 0ull) : 0ull;
-  uint32_t x[kF];  // bytes at the current tips
+  TipBytes x;  // bytes at the current tips
   // frontier entries sit at mask bits below 32 - clz(mask) (entries only
   // leave between rebuilds): kb, the wave's largest such bound, is a scalar
   // loop bound for the per-entry work (typically 1-3 of the kF = 8 slots)
