@@ -152,28 +152,43 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
       if (pad) memset(h + roff[r] + len, 0, pad);
     }
   };
-  // split the reads into contiguous ranges of about equal bytes
-  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(hw, total >> 23));  // >= 8 MiB per thread
-  if (nt <= 1 || nr < 2) {
-    fill(0, nr);
-  } else {
-    std::vector<std::thread> th;
-    uint64_t r0 = 0;
-    for (unsigned t = 0; t < nt; ++t) {
-      const uint64_t want = pos * (t + 1) / nt;
-      uint64_t r1 = r0;
-      while (r1 < nr && (t + 1 == nt || roff[r1] < want)) ++r1;
-      th.emplace_back(fill, r0, r1);
-      r0 = r1;
-    }
-    for (auto& x : th) x.join();
-  }
-  memset(h + pos, 0, 64);
   if (!b->reads.ensure(total) || !b->roff.ensure(std::max<size_t>(roff.size(), 1) * 8) ||
       !b->rlen.ensure(std::max<size_t>(b->rlen_h.size(), 1) * 4))
     return set_err(ctx, WC_E_HIP, "device allocation failed (reads)");
-  HIPCHK(hipMemcpyAsync(b->reads.p, h, total, hipMemcpyHostToDevice, ctx->stream));
+  // chunks of >= 64 MiB (at most 8): the H2D copy of chunk k runs while the
+  // host threads stage chunk k + 1; inside a chunk the reads are split into
+  // contiguous ranges of about equal bytes, one per thread
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint64_t nch = std::max<uint64_t>(1, std::min<uint64_t>(8, total >> 26));
+  uint64_t c_r0 = 0;
+  for (uint64_t c = 0; c < nch; ++c) {
+    const uint64_t want_end = pos * (c + 1) / nch;
+    uint64_t c_r1 = c_r0;
+    while (c_r1 < nr && (c + 1 == nch || roff[c_r1] < want_end)) ++c_r1;
+    const uint64_t b0 = c_r0 < nr ? roff[c_r0] : pos;
+    const uint64_t b1 = c_r1 < nr ? roff[c_r1] : pos;
+    const uint64_t nt = std::max<uint64_t>(1, std::min<uint64_t>(hw, (b1 - b0) >> 23));  // >= 8 MiB per thread
+    if (nt <= 1 || c_r1 - c_r0 < 2) {
+      fill(c_r0, c_r1);
+    } else {
+      std::vector<std::thread> th;
+      uint64_t r0 = c_r0;
+      for (uint64_t t = 0; t < nt; ++t) {
+        const uint64_t want = b0 + (b1 - b0) * (t + 1) / nt;
+        uint64_t r1 = r0;
+        while (r1 < c_r1 && (t + 1 == nt || roff[r1] < want)) ++r1;
+        th.emplace_back(fill, r0, r1);
+        r0 = r1;
+      }
+      for (auto& x : th) x.join();
+    }
+    const bool last = c + 1 == nch;
+    if (last) memset(h + pos, 0, 64);
+    const uint64_t e1 = last ? total : b1;
+    if (e1 > b0)
+      HIPCHK(hipMemcpyAsync((uint8_t*)b->reads.p + b0, h + b0, e1 - b0, hipMemcpyHostToDevice, ctx->stream));
+    c_r0 = c_r1;
+  }
   if (!roff.empty()) HIPCHK(hipMemcpyAsync(b->roff.p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
   if (!b->rlen_h.empty())
     HIPCHK(hipMemcpyAsync(b->rlen.p, b->rlen_h.data(), b->rlen_h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
