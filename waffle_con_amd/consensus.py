@@ -132,17 +132,45 @@ def _stats(results, L, per_problem=False):
     return out
 
 
+def _bytes_data_offset():
+    probe = b"waffle_con"
+    off = ctypes.cast(ctypes.c_char_p(probe), ctypes.c_void_p).value - id(probe)
+    if not 0 < off < 256:
+        raise RuntimeError("unexpected bytes object layout")
+    return off
+
+
+_BYTES_DATA = _bytes_data_offset()
+
+
 def _problems(batch):
-    keep = []
+    """WcProblem array for a list of (reads, offsets). Zero-copy and flat: one
+    pointer array and one length array for every read of the batch (the
+    bytes objects' own buffers, kept alive in `keep`); each problem points at
+    its slice. The library copies the bytes once, into its pinned staging."""
+    reads = [s if type(s) is bytes else bytes(s) for seqs, _ in batch for s in seqs]
+    n = len(reads)
+    # the data address of a bytes object is its id plus a fixed header offset
+    # (_BYTES_DATA, measured at import): one vectorised pass instead of a
+    # ctypes conversion per read
+    ptrs = np.fromiter(map(id, reads), dtype=np.uint64, count=n) + np.uint64(_BYTES_DATA)
+    lens = np.fromiter(map(len, reads), dtype=np.uint64, count=n)
+    if n == 0:
+        ptrs = lens = np.zeros(1, np.uint64)
+    base_p, base_l = ptrs.ctypes.data, lens.ctypes.data
+    rp, lp = ctypes.POINTER(_lib._u8p), ctypes.POINTER(ctypes.c_uint64)
     arr = (_lib.WcProblem * max(1, len(batch)))()
+    keep = [reads, ptrs, lens]
+    k = 0
     for i, (seqs, offsets) in enumerate(batch):
-        pr = _lib.PackedReads(seqs)
         offs = _lib.offsets_array(offsets)
-        keep.append((pr, offs))
+        if offs is not None:
+            keep.append(offs)
         arr[i].n_reads = len(seqs)
-        arr[i].reads = ctypes.cast(pr.ptrs, ctypes.POINTER(_lib._u8p))
-        arr[i].lens = ctypes.cast(pr.lens, ctypes.POINTER(ctypes.c_uint64))
+        arr[i].reads = ctypes.cast(base_p + 8 * k, rp)
+        arr[i].lens = ctypes.cast(base_l + 8 * k, lp)
         arr[i].offsets = ctypes.cast(offs, ctypes.POINTER(ctypes.c_int64)) if offs is not None else None
+        k += len(seqs)
     return arr, keep
 
 
