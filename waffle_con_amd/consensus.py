@@ -141,6 +141,9 @@ def _bytes_data_offset():
 
 
 _BYTES_DATA = _bytes_data_offset()
+# _lib.WcProblem's layout (u32 n_reads, 4 bytes padding, three pointers)
+_PROBLEM_DT = np.dtype([("n_reads", "<u4"), ("_pad", "<u4"), ("reads", "<u8"), ("lens", "<u8"), ("offsets", "<u8")])
+assert _PROBLEM_DT.itemsize == ctypes.sizeof(_lib.WcProblem) and _lib.WcProblem.reads.offset == 8
 
 
 def _problems(batch):
@@ -158,19 +161,24 @@ def _problems(batch):
     if n == 0:
         ptrs = lens = np.zeros(1, np.uint64)
     base_p, base_l = ptrs.ctypes.data, lens.ctypes.data
-    rp, lp = ctypes.POINTER(_lib._u8p), ctypes.POINTER(ctypes.c_uint64)
-    arr = (_lib.WcProblem * max(1, len(batch)))()
-    keep = [reads, ptrs, lens]
-    k = 0
-    for i, (seqs, offsets) in enumerate(batch):
-        offs = _lib.offsets_array(offsets)
-        if offs is not None:
-            keep.append(offs)
-        arr[i].n_reads = len(seqs)
-        arr[i].reads = ctypes.cast(base_p + 8 * k, rp)
-        arr[i].lens = ctypes.cast(base_l + 8 * k, lp)
-        arr[i].offsets = ctypes.cast(offs, ctypes.POINTER(ctypes.c_int64)) if offs is not None else None
-        k += len(seqs)
+    # the WcProblem array as a numpy record array of the same layout
+    nb = len(batch)
+    counts = np.fromiter((len(seqs) for seqs, _ in batch), dtype=np.uint64, count=nb)
+    starts = np.zeros(max(1, nb), np.uint64)
+    if nb > 1:
+        np.cumsum(counts[:-1], out=starts[1:nb])
+    rec = np.zeros(max(1, nb), dtype=_PROBLEM_DT)
+    rec["n_reads"][:nb] = counts
+    rec["reads"][:nb] = np.uint64(base_p) + np.uint64(8) * starts[:nb]
+    rec["lens"][:nb] = np.uint64(base_l) + np.uint64(8) * starts[:nb]
+    keep = [reads, ptrs, lens, rec]
+    for i, (_, offsets) in enumerate(batch):
+        if offsets is not None:
+            offs = _lib.offsets_array(offsets)
+            if offs is not None:
+                keep.append(offs)
+                rec["offsets"][i] = ctypes.addressof(offs)
+    arr = ctypes.cast(rec.ctypes.data, ctypes.POINTER(_lib.WcProblem))
     return arr, keep
 
 
