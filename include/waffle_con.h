@@ -227,13 +227,6 @@ const uint8_t* wc_gen_consensus(const wc_gen* g, uint64_t* len);
 const uint8_t* wc_gen_sample(const wc_gen* g, uint64_t i, uint64_t* len);
 void wc_gen_free(wc_gen* g);
 
-/* Known-answer hooks for the RNG restatement: raw ChaCha(rounds) words from a
- * 32-byte seed; StdRng::from_seed -> next_u64, then StdRng::from_rng -> next_u64;
- * StdRng::seed_from_u64 words. */
-void wc_rng_words(const uint8_t* seed32, int rounds, uint32_t n, uint32_t* out);
-void wc_rng_stdrng_chain(const uint8_t* seed32, uint64_t* out2);
-void wc_rng_seed_from_u64(uint64_t seed, uint32_t n, uint32_t* out);
-
 /* sequence_alignment.rs:18,36 — pairwise WFA edit distance (host reference API). */
 uint64_t wc_wfa_ed_config(const uint8_t* v1, uint64_t l1, const uint8_t* v2, uint64_t l2, uint8_t require_both_end,
                           int32_t wildcard);

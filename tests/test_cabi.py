@@ -25,10 +25,22 @@ def test_header_symbols_exported():
     assert set(_lib.EXPORTED) <= names
 
 
+def _rng_hooks():
+    """oracle/librnghooks.so: the product's ChaCha/StdRng source (example_gen.cpp)
+    behind test-only known-answer hooks (the product library exports none)."""
+    return ctypes.CDLL(os.path.join(ROOT, "oracle", "librnghooks.so"))
+
+
+def test_rng_hooks_not_in_product_abi():
+    L = _lib.lib()
+    for name in ("wc_rng_words", "wc_rng_stdrng_chain", "wc_rng_seed_from_u64"):
+        assert not hasattr(L, name), name
+
+
 def test_chacha20_zero_key_vector():
     """Original ChaCha20 (64-bit nonce) keystream, all-zero key/nonce, block 0."""
     out = (ctypes.c_uint32 * 16)()
-    _lib.lib().wc_rng_words(bytes(32), 20, 16, out)
+    _rng_hooks().wc_rng_words(bytes(32), 20, 16, out)
     exp = bytes.fromhex("76b8e0ada0f13d90405d6ae55386bd28bdd219b8a08ded1aa836efcc8b770dc7"
                         "da41597c5157488d7724e03fb8d84a376a43b8f41518a11cc387b669b2ee6586")
     assert bytes(out) == exp
@@ -38,7 +50,7 @@ def test_stdrng_construction_vector():
     """rand 0.8 src/rngs/std.rs test_stdrng_construction target values."""
     o = (ctypes.c_uint64 * 2)()
     seed = bytes([1, 0, 0, 0, 23, 0, 0, 0, 200, 1, 0, 0, 210, 30, 0, 0] + [0] * 16)
-    _lib.lib().wc_rng_stdrng_chain(seed, o)
+    _rng_hooks().wc_rng_stdrng_chain(seed, o)
     assert list(o) == [10719222850664546238, 14064965282130556830]
 
 
@@ -137,3 +149,32 @@ def test_hpc_codec_and_synthetic_shapes():
     assert len(c4) == 12
     c5 = synth.cfg5_locus(3, len_range=(200, 300), reads_range=(3, 5))
     assert all(len(ch) == 2 and ch[0] == synth.hpc_compress(ch[1]) for ch in c5)
+
+
+def test_consensus_pickle_and_deepcopy_of_a_lazy_result():
+    """A batch result that still views the library's arenas (Consensus._packed)
+    pickles and deep-copies as its plain values (consensus.rs derives Clone),
+    never as the arenas or the owner's ctypes handle."""
+    import copy
+    import pickle
+    import numpy as np
+    from waffle_con_amd.consensus import Consensus
+
+    class _Handle:  # stands in for the result-set owner: not picklable
+        def __init__(self):
+            self.h = ctypes.c_void_p(1)
+
+        def __reduce__(self):
+            raise TypeError("the result-set owner must not be serialised")
+
+    seq = np.frombuffer(b"ACGTTTGCA", dtype=np.uint8)
+    sc = np.array([3, 1, 4, 1, 5], dtype=np.uint64)
+    idx = [0, 4, 0, 2, 4, 5, 2, 3]
+    pack = (seq, idx, sc, _Handle())
+    c0 = Consensus._packed(pack, 0, w.ConsensusCost.L1Distance)
+    c1 = Consensus._packed(pack, 1, w.ConsensusCost.L2Distance)
+    r0 = pickle.loads(pickle.dumps(c0))
+    assert r0 == Consensus(b"ACGT", w.ConsensusCost.L1Distance, [3, 1])
+    r1 = copy.deepcopy(c1)
+    assert r1.sequence() == b"TTGCA" and r1.scores() == [4, 1, 5] and r1._src is None
+    assert copy.copy(c1) == c1

@@ -56,3 +56,43 @@ def test_chain_length_invariance(chain, L, N, err, seed, monkeypatch):
     assert got == exp
     for k in COUNTER_KEYS:
         assert gc[k] == ec[k], (k, gc[k], ec[k])
+
+
+def test_failed_refill_leaves_the_batch_usable():
+    """host.cpp upload_batch is transactional: a refill rejected by validation
+    changes nothing, so the batch still runs its previous problems."""
+    import ctypes
+    import waffle_con_amd as w
+    from waffle_con_amd import _lib
+    probs = [_gen(300, 8, 0.03, s) for s in range(4)]
+    b = w.ResidentBatch(probs)
+    exp, _ = b.consensus(w.CdwfaConfig(min_count=2))
+    exp = [[(c.sequence(), c.scores()) for c in r] for r in exp]
+    bad = (_lib.WcProblem * 1)()
+    bad[0].n_reads = 1
+    ptrs = (_lib._u8p * 1)()  # a null read pointer with a non-zero length
+    lens = (ctypes.c_uint64 * 1)(5)
+    bad[0].reads = ptrs
+    bad[0].lens = lens
+    rc = _lib.lib().wc_batch_refill(b.ctx.handle, b.handle, 1, bad)
+    assert rc == _lib.WC_E_BAD_INPUT
+    got, _ = b.consensus(w.CdwfaConfig(min_count=2))
+    assert [[(c.sequence(), c.scores()) for c in r] for r in got] == exp
+    b.close()
+
+
+def test_batch_results_pickle_after_the_batch_is_gone():
+    import copy
+    import gc
+    import pickle
+    import waffle_con_amd as w
+    probs = [_gen(300, 8, 0.03, s) for s in range(3)]
+    res, _ = w.consensus_batch(probs, w.CdwfaConfig(min_count=2))
+    blobs = [pickle.dumps(r) for r in res]
+    dup = copy.deepcopy(res)
+    del res
+    gc.collect()
+    for p, blob, d in zip(probs, blobs, dup):
+        exp = orc.consensus(p, min_count=2)
+        assert [{"sequence": c.sequence(), "scores": list(c.scores())} for c in pickle.loads(blob)] == exp
+        assert [{"sequence": c.sequence(), "scores": list(c.scores())} for c in d] == exp

@@ -1,0 +1,54 @@
+#!/bin/bash
+# One runner for every GPU-box job (run through gpurun from the repo root):
+#   bash tools/gpu.sh tests  <tag> [pytest args]      pytest -m gpu (default: whole suite)
+#   bash tools/gpu.sh check  <tag> <lib> [pytest args] a bounds-checked library variant (make check)
+#   bash tools/gpu.sh bench  <tag> [bench.py args]    one bench line -> gpurun_out/<tag>/bench.json
+#   bash tools/gpu.sh profile <tag> [bench.py args]   tools/profile_round.sh (kernel trace + PMC passes)
+#   bash tools/gpu.sh smoke  <tag>                    __graft_entry__.smoke()
+# Jobs can be chained: bash tools/gpu.sh tests t1 -- bench t1 --workload cfg5
+# Every GPU step has its own timeout; the first failing step ends the call.
+set -o pipefail
+export TMPDIR=/tmp
+run_job() {
+  local job=$1 tag=$2
+  shift 2
+  local O=gpurun_out/$tag
+  mkdir -p $O
+  case $job in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" \
+        > $O/pytest_gpu.log 2>&1 || { echo "tests failed"; tail -40 $O/pytest_gpu.log; return 1; }
+      tail -2 $O/pytest_gpu.log ;;
+    check)
+      local lib=$1
+      shift
+      WAFFLE_CON_LIB=$PWD/$lib timeout -k 10 900 python -u -m pytest -s -x -v --timeout 300 --timeout-method thread "$@" \
+        > $O/check.log 2>&1 || { echo "check run failed"; grep -a "wc-check\|FAIL\|Error\|error" $O/check.log | head -40; tail -20 $O/check.log; return 1; }
+      grep -a "wc-check" $O/check.log | head -20 || true
+      tail -3 $O/check.log ;;
+    bench)
+      timeout -k 10 900 python -u bench.py "$@" > $O/bench.json 2> $O/bench.err \
+        || { echo "bench failed"; tail -30 $O/bench.err; return 1; }
+      tail -c 3000 $O/bench.json ;;
+    profile)
+      bash tools/profile_round.sh $tag "$@" > $O/profile.log 2>&1 || { echo "profile failed"; tail -30 $O/profile.log; return 1; }
+      tail -3 $O/profile.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
+        || { echo "smoke failed"; tail -30 $O/smoke.log; return 1; }
+      tail -2 $O/smoke.log ;;
+    *) echo "unknown job $job"; return 2 ;;
+  esac
+}
+# split the arguments on "--" into jobs
+args=()
+for a in "$@"; do
+  if [ "$a" = "--" ]; then
+    run_job "${args[@]}" || exit 1
+    args=()
+  else
+    args+=("$a")
+  fi
+done
+[ ${#args[@]} -gt 0 ] && { run_job "${args[@]}" || exit 1; }
+exit 0

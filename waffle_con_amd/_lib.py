@@ -22,6 +22,8 @@ WC_E_FINALIZE_UNINIT = 1
 WC_E_NO_START = 2
 WC_E_COVERAGE_GAP = 3
 WC_E_CAPACITY = 4
+WC_E_BAD_INPUT = 9
+WC_E_INVARIANT = 10
 WC_E_LIMIT = 11
 WC_E_HIP = 12
 
@@ -115,8 +117,7 @@ EXPORTED = (
     "wc_results_count", "wc_results_single", "wc_results_single_sizes", "wc_results_single_pack", "wc_results_single_view", "wc_results_dual", "wc_results_chain_len",
     "wc_results_chain", "wc_results_sequence_indices", "wc_results_stats",
     "wc_results_problem_stats", "wc_dwfa_batch", "wc_generate_test", "wc_gen_consensus",
-    "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_wfa_ed_batch", "wc_rng_words", "wc_rng_stdrng_chain",
-    "wc_rng_seed_from_u64",
+    "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_wfa_ed_batch",
 )
 
 

@@ -26,11 +26,14 @@ class ResidentBatch:
         """Upload a new set of problems into this batch's device buffers
         (wc_batch_refill: reused when large enough, so no allocation)."""
         L = _lib.lib()
-        self._batch = [(p, None) if not isinstance(p, tuple) else p for p in problems]
-        arr, keep = _problems(self._batch)
-        rc = L.wc_batch_refill(self.ctx.handle, self.handle, len(self._batch), arr)
+        batch = [(p, None) if not isinstance(p, tuple) else p for p in problems]
+        arr, keep = _problems(batch)
+        rc = L.wc_batch_refill(self.ctx.handle, self.handle, len(batch), arr)
         if rc != _lib.WC_OK:
+            # the library left the batch as it was (host.cpp upload_batch commits
+            # only a complete upload), so this object keeps describing it
             raise _lib.WaffleConError("wc_batch_refill failed: " + self.ctx.last_error(), rc)
+        self._batch = batch
         self.bytes = L.wc_batch_bytes(self.handle)
 
     def __len__(self):

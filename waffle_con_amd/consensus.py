@@ -41,6 +41,11 @@ class Consensus:
         self._scores = sc[c:c + lc].tolist()
         self._src = None
 
+    def __reduce__(self):
+        """pickle / copy / deepcopy: the plain values only (never the result
+        arenas this object may still view), as the reference's derived Clone."""
+        return (Consensus, (self.sequence(), self._consensus_cost, self.scores()))
+
     def sequence(self):
         if self._src is not None:
             self._unpack()

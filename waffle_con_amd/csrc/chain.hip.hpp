@@ -513,8 +513,8 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
         bdst = E.sv(S, 0).wf + (uint64_t)rl * E.wcap;
         if (lane == 0) {
           const uint32_t k = atomicAdd(&ctl.chain_nbak, 1u);
-          E.L.list[2 * k] = rl;
-          E.L.list[2 * k + 1] = 2 * e_in + 1;
+          E.L.list[WC_IX(2 * k, list_entries(E.sides, E.nmax))] = rl;
+          E.L.list[WC_IX(2 * k + 1, list_entries(E.sides, E.nmax))] = 2 * e_in + 1;
         }
         bak |= 1ull << l;
       }
@@ -748,7 +748,7 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
     ctl.chain_k = 0;
     if (K >= 2 && ctl.nfree > 0) {
       ctl.chain_k = K;
-      ctl.chain_slot = E.L.freestack[--ctl.nfree];
+      ctl.chain_slot = E.L.freestack[WC_IX(--ctl.nfree, E.pcap)];
       ctl.chain_stop = K;
       ctl.chain_novf = 0;
       ctl.chain_nochain = 0;
@@ -767,7 +767,7 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
   __syncthreads();
   PH_MARK(8);
   if (uni(ctl.chain_nochain)) {
-    if (tid == 0) E.L.freestack[ctl.nfree++] = S;
+    if (tid == 0) E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = S;
     __syncthreads();
     return 0;
   }
@@ -820,7 +820,7 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
     const int lane = lane_id();
     const uint32_t nb = uni(ctl.chain_nbak);
     for (uint32_t k = wave_id(); k < nb; k += kEW) {
-      const uint32_t r = E.L.list[2 * k], W = E.L.list[2 * k + 1];
+      const uint32_t r = E.L.list[WC_IX(2 * k, list_entries(E.sides, E.nmax))], W = E.L.list[WC_IX(2 * k + 1, list_entries(E.sides, E.nmax))];
       const Gm<uint32_t>* src = b.wf + (uint64_t)r * E.wcap;
       Gm<uint32_t>* dst = v.wf + (uint64_t)r * E.wcap;
       for (uint32_t i = lane; i < W; i += 64) dst[i] = src[i];
@@ -849,13 +849,13 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
 #ifdef WC_PHASE_PROF
     ctl.ph[15] += 1ull + ((jstar == K && Keff == K) ? (1ull << 20) : 0ull) + ((uint64_t)jstar << 40);
 #endif
-    E.L.freestack[ctl.nfree++] = S;
+    E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = S;
     if (jstar > 0) {
       const auto& st = E.L.cstep[jstar];
       const uint32_t clen = L0 + jstar;
       E.L.meta[top].len[0] = clen;
       E.tracker(ctl, 0).insert(clen);
-      heap_push(E.L.heap, ctl.heap_n, HeapEntry{st.cost, clen, top});
+      heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{st.cost, clen, top});
       ctl.cache_slot = top;
       ctl.cache_nend = step_nend(st.ef);
       ctl.cache_multi = step_nmulti(st.ef) ? 1u : 0u;

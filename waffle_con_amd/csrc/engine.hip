@@ -239,8 +239,9 @@ __device__ __forceinline__ bool prio_less(const A& a, const B& b) {
   if (a.cost != b.cost) return a.cost > b.cost;  // Reverse(cost)
   return a.len < b.len;
 }
-__device__ __forceinline__ void heap_push(Sh<HeapEntry>* h, Lo<uint32_t>& n, HeapEntry e) {
-  uint32_t pos = n++;
+__device__ __forceinline__ void heap_push(Sh<HeapEntry>* h, Lo<uint32_t>& n, uint32_t cap, HeapEntry e) {
+  uint32_t pos = WC_IX(n++, cap);
+  (void)cap;
   while (pos > 0) {
     uint32_t parent = (pos - 1) / 2;
     if (!prio_less(h[parent], e)) break;
@@ -249,8 +250,10 @@ __device__ __forceinline__ void heap_push(Sh<HeapEntry>* h, Lo<uint32_t>& n, Hea
   }
   h[pos] = e;
 }
-__device__ __forceinline__ HeapEntry heap_pop(Sh<HeapEntry>* h, Lo<uint32_t>& n) {
-  const HeapEntry top = h[0];
+__device__ __forceinline__ HeapEntry heap_pop(Sh<HeapEntry>* h, Lo<uint32_t>& n, uint32_t cap) {
+  HeapEntry top = h[0];
+  top.slot = WC_IX(top.slot, cap);
+  (void)cap;
   n--;
   // sift the last entry down from the root: the swap-per-level loop of the
   // reference, with the moving entry kept in registers (same final layout)
@@ -297,22 +300,23 @@ struct TrackerRef {
   Lo<uint64_t>* total;
   Lo<uint64_t>* thr;
   uint64_t cap;
+  uint32_t lim;  // entries of lc / pc (lcap + 2)
   __device__ __forceinline__ void insert(uint32_t v) {
-    atomicAdd((uint32_t*)&lc[v], 1u);
+    atomicAdd((uint32_t*)&lc[WC_IX(v, lim)], 1u);
     if (v >= *thr) (*total)++;
   }
   __device__ __forceinline__ void remove(uint32_t v) {
-    atomicSub((uint32_t*)&lc[v], 1u);
+    atomicSub((uint32_t*)&lc[WC_IX(v, lim)], 1u);
     if (v >= *thr) (*total)--;
   }
   __device__ __forceinline__ void increment_threshold() {
-    *total -= trk_load(&lc[*thr]);
+    *total -= trk_load(&lc[WC_IX(*thr, lim)]);
     (*thr)++;
   }
-  __device__ __forceinline__ uint32_t processed(uint32_t v) const { return trk_load(&pc[v]); }
+  __device__ __forceinline__ uint32_t processed(uint32_t v) const { return trk_load(&pc[WC_IX(v, lim)]); }
   // process() of a length whose processed() count is below capacity (the pop
   // just checked it; only this workgroup's thread 0 touches the tracker)
-  __device__ __forceinline__ void process_unchecked(uint32_t v) { atomicAdd((uint32_t*)&pc[v], 1u); }
+  __device__ __forceinline__ void process_unchecked(uint32_t v) { atomicAdd((uint32_t*)&pc[WC_IX(v, lim)], 1u); }
 };
 
 __device__ inline uint64_t ceil_u64(double x) {
@@ -408,14 +412,14 @@ struct Eng {
   DevProblem P;
   Lds L;
   __device__ SideView sv(uint32_t slot, uint32_t side) const {
-    return side_view(ws + (uint64_t)slot * sbytes, side, nmax, wcap, lcap);
+    return side_view(ws + (uint64_t)WC_IX(slot, pcap) * sbytes, WC_IX(side, sides), nmax, wcap, lcap);
   }
-  __device__ const Gm<uint8_t>* read(uint32_t r) const { return rbytes + roff[P.read_begin + r]; }
-  __device__ uint32_t rlen(uint32_t r) const { return rlenp[P.read_begin + r]; }
+  __device__ const Gm<uint8_t>* read(uint32_t r) const { return rbytes + roff[P.read_begin + WC_IX(r, nmax)]; }
+  __device__ uint32_t rlen(uint32_t r) const { return rlenp[P.read_begin + WC_IX(r, nmax)]; }
   __device__ __forceinline__ TrackerRef tracker(Lo<Ctl>& ctl, int k) const {
     const uint64_t L2 = lcap + 2;
     return TrackerRef{trk + 2 * k * L2, trk + (2 * k + 1) * L2, &ctl.trk_total[k], &ctl.trk_thr[k],
-                      cfg.max_capacity_per_size};
+                      cfg.max_capacity_per_size, (uint32_t)L2};
   }
 };
 
@@ -619,7 +623,7 @@ __device__ inline void init_problem(Eng& E, Lo<Ctl>& ctl) {
     E.total_active[0] = E.P.n_active;
     E.active_min[0] = (uint32_t)max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.P.n_active));
     E.tracker(ctl, 0).insert(0);
-    heap_push(E.L.heap, ctl.heap_n, HeapEntry{0, 0, 0});
+    heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{0, 0, 0});
   }
   __syncthreads();
 }
@@ -673,7 +677,7 @@ WC_PHASE_FN void analyze_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t nsi
       }
     }
     const uint32_t k = agg_append(&ctl.nheavy, wide);
-    if (wide) E.L.list[k] = it;
+    if (wide) E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))] = it;
   }
   agg_add(&ctl.n_end[0], ends0);
   agg_add(&ctl.n_end[1], ends1);
@@ -682,7 +686,7 @@ WC_PHASE_FN void analyze_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t nsi
   __syncthreads();
   const uint32_t nh = uni(ctl.nheavy);
   for (uint32_t k = wave_id(); k < nh; k += kEW) {
-    const uint32_t it = uni(E.L.list[k]);
+    const uint32_t it = uni(E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))]);
     const uint32_t side = it >= n ? 1u : 0u, r = it - side * n;
     Sh<RInfo>* out = (side ? out1 : out0) + r;
     const auto rs = node_rs<kHot>(E, slot, side);
@@ -801,7 +805,7 @@ WC_SINGLE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1
     }
     } while (0);
     const uint32_t k = agg_append(&ctl.nheavy, heavy_item);
-    if (heavy_item) E.L.list[k] = side * E.n + r;
+    if (heavy_item) E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))] = side * E.n + r;
   }
 
   flush_thread_counters(ctl, tc);
@@ -814,7 +818,7 @@ WC_SINGLE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1
   const uint32_t nh = uni(ctl.nheavy);
   WaveCounters cnt = {0, 0, 0, 0, 0};
   for (uint32_t k = wave_id(); k < nh; k += kEW) {
-    const uint32_t it = E.L.list[k];
+    const uint32_t it = E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))];
     const uint32_t side = it >= E.n ? 1u : 0u, r = it - side * E.n;
     SideView v = E.sv(slot, side);
     const uint32_t olen = side == 0 ? len0 : len1;
@@ -910,14 +914,14 @@ WC_PHASE_FN void activate_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t sid
   if (tid == 0) ctl.nheavy = 0;
   __syncthreads();
   for (uint32_t r = tid; r < E.n; r += kEB)
-    if (E.ract[E.P.read_begin + r] == (int64_t)alen) E.L.list[atomicAdd(&ctl.nheavy, 1u)] = r;
+    if (E.ract[E.P.read_begin + r] == (int64_t)alen) E.L.list[WC_IX(atomicAdd(&ctl.nheavy, 1u), list_entries(E.sides, E.nmax))] = r;
   __syncthreads();
   const uint32_t nh = uni(ctl.nheavy);
   SideView v = E.sv(slot, side);
   const auto dst = node_rs<kHot>(E, slot, side);
   WaveCounters cnt = {0, 0, 0, 0, 0};
   for (uint32_t k = wave_id(); k < nh; k += kEW) {
-    const uint32_t r = E.L.list[k];
+    const uint32_t r = E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))];
     if (uni(dst[r].e) != kInactive) {
       if (lane == 0) atomicOr(&ctl.ovf, 16u);
       continue;
@@ -1325,7 +1329,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
             ctl.status = ST_RETRY | ST_RETRY_PCAP;
             break;
           }
-          slot = E.L.freestack[--ctl.nfree];
+          slot = E.L.freestack[WC_IX(--ctl.nfree, E.pcap)];
         }
         ctl.ch_slot[c] = slot;
         ctl.ch_cost[c] = 0;
@@ -1341,7 +1345,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         for (int sd = 0; sd < 2; ++sd) {
           const int sym = ctl.ch_s[c][sd];
           if (sym >= 0) {
-            E.sv(slot, sd).con[m.len[sd]] = (uint8_t)sym;
+            E.sv(slot, sd).con[WC_IX(m.len[sd], E.lcap)] = (uint8_t)sym;
             m.len[sd]++;
           } else if (kind == 0) {
             m.flags |= (sd == 0 ? 2u : 4u);  // lock_sequence
@@ -1358,7 +1362,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     // into side 2, straight from the parent (a split child's parent is single,
     // so the in-place child's side 2 is not read by any clone)
     for (uint32_t c = c0; c < c0 + cn; ++c) {
-      const uint32_t slot = uni(ctl.ch_slot[c]);
+      const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       if (slot != top) {
         copy_side<false>(E, top, 0, slot, 0, tm.len[0]);
         if (tdual) copy_side<false>(E, top, 1, slot, 1, tm.len[1]);
@@ -1377,7 +1381,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t c = c0 + q / 2, sd = q & 1u;
       const int sym = uni((int32_t)ctl.ch_s[c][sd]);
       if (sym < 0) continue;
-      const uint32_t slot = uni(ctl.ch_slot[c]);
+      const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       const uint32_t olen = uni(E.L.meta[slot].len[sd]);
       SideView v = E.sv(slot, sd);
       for (uint32_t base = 0; base < n; base += kEB) {
@@ -1407,8 +1411,8 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         }
         const uint32_t kg = agg_append(&ctl.nheavy, kind == 1);
         const uint32_t kw = agg_append(&ctl.nwide, kind == 2);
-        if (kind == 1) E.L.list[kg] = q * n + r;
-        if (kind == 2) E.L.list[lend - kw] = q * n + r;
+        if (kind == 1) E.L.list[WC_IX(kg, list_entries(E.sides, E.nmax))] = q * n + r;
+        if (kind == 2) E.L.list[WC_IX(lend - kw, list_entries(E.sides, E.nmax))] = q * n + r;
       }
     }
     flush_thread_counters(ctl, tc);
@@ -1426,7 +1430,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     for (uint32_t b0 = wave_id() * 4u; b0 < ng; b0 += kEW * 4u) {
       const uint32_t k = b0 + ((uint32_t)lane >> 4);
       const bool act = k < ng;
-      const uint32_t it = act ? E.L.list[k] : 0u;
+      const uint32_t it = act ? E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))] : 0u;
       const uint32_t q = it / n, r = it - q * n;
       const uint32_t c = c0 + q / 2, sd = q & 1u;
       const uint32_t slot = ctl.ch_slot[c];
@@ -1467,10 +1471,10 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     // ... and wide frontiers / long rows (and a few group items) one read per wave
     const uint32_t nsolo = nw + (nh - ng);
     for (uint32_t k = wave_id(); k < nsolo; k += kEW) {
-      const uint32_t it = uni(k < nw ? E.L.list[lend - k] : E.L.list[k - nw]);
+      const uint32_t it = uni(k < nw ? E.L.list[WC_IX(lend - k, list_entries(E.sides, E.nmax))] : E.L.list[WC_IX(k - nw, list_entries(E.sides, E.nmax))]);
       const uint32_t q = it / n, r = it - q * n;
       const uint32_t c = c0 + q / 2, sd = q & 1u;
-      const uint32_t slot = uni(ctl.ch_slot[c]);
+      const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       SideView v = E.sv(slot, sd);
       uint32_t e = 0;
       if (!wave_heavy(&v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
@@ -1486,7 +1490,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     // reads whose offset activates at a child's new max length
     // (dual_consensus.rs:633-639): consensus 1 always, consensus 2 too when dual
     for (uint32_t c = c0; c < c0 + cn; ++c) {
-      const uint32_t slot = uni(ctl.ch_slot[c]);
+      const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       const uint32_t nl0 = uni(E.L.meta[slot].len[0]), nl1 = uni(E.L.meta[slot].len[1]);
       if (max(nl0, nl1) > E.P.max_act) continue;
       activate_side<false>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
@@ -1622,7 +1626,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_WAV
             t.increment_threshold();
             ctl.last_constraint[0] = 0;
           }
-          HeapEntry top = heap_pop(E.L.heap, ctl.heap_n);
+          HeapEntry top = heap_pop(E.L.heap, ctl.heap_n, E.pcap);
           t.remove(top.len);
           ctl.top_slot = top.slot;
           ctl.top_len = top.len;
@@ -1630,7 +1634,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_WAV
           const bool at_cap = t.processed(top.len) >= t.cap;
           if (top.cost > ctl.max_err || top.len < ctl.trk_thr[0] || at_cap) {
             ctl.cnt[S_IGNORED]++;
-            E.L.freestack[ctl.nfree++] = top.slot;
+            E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top.slot;
             if (top.slot == ctl.hot_slot) ctl.hot_slot = kNoSlot;
             ctl.action = 1;
           } else {
@@ -1758,7 +1762,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_WAV
             ctl.status = WC_E_COVERAGE_GAP_CODE;
             ((Gm<uint32_t>*)outp)[1] = len;
           }
-          E.L.freestack[ctl.nfree++] = top;
+          E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top;
           ctl.hot_slot = kNoSlot;
         }
         __syncthreads();
@@ -1783,7 +1787,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_WAV
           uint32_t slot = top;
           if (c + 1 < nc) {
             if (ctl.nfree == 0) ctl.status = ST_RETRY | ST_RETRY_PCAP;
-            else slot = E.L.freestack[--ctl.nfree];
+            else slot = E.L.freestack[WC_IX(--ctl.nfree, E.pcap)];
           }
           ctl.cur_slot = slot;
           ctl.cost_acc = 0;
@@ -1822,7 +1826,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_WAV
         TrackerRef t = E.tracker(ctl, 0);
         for (uint32_t c = 0; c < nc; ++c) {
           t.insert(len + 1);
-          heap_push(E.L.heap, ctl.heap_n, HeapEntry{ctl.ch_cost[c], len + 1, ctl.ch_slot[c]});
+          heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{ctl.ch_cost[c], len + 1, ctl.ch_slot[c]});
         }
         // the last child's nominations are in LDS: reuse them if it is popped next
         ctl.cache_slot = ctl.ch_slot[nc - 1];
@@ -1873,7 +1877,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
           // first, under one wait, while the threshold walk and the sift run
           const uint32_t plen = E.L.heap[0].len;
           const uint32_t pc_pre[2] = {E.tracker(ctl, 0).processed(plen), E.tracker(ctl, 1).processed(plen)};
-          const uint64_t am_pre = plen < ctl.am_len ? E.active_min[plen] : 0;
+          const uint64_t am_pre = plen < ctl.am_len ? E.active_min[WC_IX(plen, E.lcap + 2)] : 0;
           ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)ctl.heap_n);
           ctl.cnt[S_POPS]++;
           for (int k = 0; k < 2; ++k) {
@@ -1884,7 +1888,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
               ctl.last_constraint[k] = 0;
             }
           }
-          HeapEntry top = heap_pop(E.L.heap, ctl.heap_n);
+          HeapEntry top = heap_pop(E.L.heap, ctl.heap_n, E.pcap);
           const auto& m = E.L.meta[top.slot];
           const uint32_t dual = m.flags & 1u;
           TrackerRef t = E.tracker(ctl, dual);
@@ -1899,7 +1903,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
           const bool at_cap = pc_pre[dual] >= t.cap;
           if (top.cost > ctl.max_err || top.len < ctl.trk_thr[dual] || at_cap || imbalanced) {
             ctl.cnt[S_IGNORED]++;
-            E.L.freestack[ctl.nfree++] = top.slot;
+            E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top.slot;
             ctl.action = 1;
           } else {
             ctl.farthest[dual] = max(ctl.farthest[dual], (uint64_t)top.len);
@@ -2122,7 +2126,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
       if (uni(ctl.status) != ST_OK) break;
       const uint32_t nc = uni(ctl.nchild);
       if (nc == 0) {
-        if (tid == 0) E.L.freestack[ctl.nfree++] = top;
+        if (tid == 0) E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top;
         __syncthreads();
         continue;
       }
@@ -2140,7 +2144,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
         for (uint32_t c = 0; c < nc; ++c) {
           const uint32_t k = (E.L.meta[ctl.ch_slot[c]].flags & 1u) ? 1 : 0;
           E.tracker(ctl, k).insert(ctl.ch_len[c]);
-          heap_push(E.L.heap, ctl.heap_n, HeapEntry{ctl.ch_cost[c], ctl.ch_len[c], ctl.ch_slot[c]});
+          heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{ctl.ch_cost[c], ctl.ch_len[c], ctl.ch_slot[c]});
         }
       }
       // (no barrier: the next pop is thread 0's too, and the block meets after it)

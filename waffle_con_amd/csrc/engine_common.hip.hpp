@@ -58,6 +58,28 @@ template <class T> using Sh = T;
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
+// Bounds-checked debug builds (-DWC_CHECK, `make check`): every index into the
+// node pool, the search state (heap, free stack, work list, slot metadata),
+// the read table and the tracker arrays goes through WC_IX(i, n). An index out
+// of range is reported (file line, index, bound, workgroup, thread) and
+// replaced by 0, so the access stays inside its buffer instead of faulting;
+// the host reads the hit count back after the launch (wc_check_hits).
+#ifdef WC_CHECK
+__device__ unsigned int wc_chk_hits;
+__device__ __noinline__ uint32_t wc_chk_fail(uint32_t line, uint64_t i, uint64_t n) {
+  if (atomicAdd(&wc_chk_hits, 1u) < 64u)
+    printf("[wc-check] line %u: index %llu >= bound %llu (workgroup %u thread %u)\n", line, (unsigned long long)i,
+           (unsigned long long)n, blockIdx.x, threadIdx.x);
+  return 0;
+}
+__device__ __forceinline__ uint32_t wc_ix(uint64_t i, uint64_t n, uint32_t line) {
+  return i < n ? (uint32_t)i : wc_chk_fail(line, i, n);
+}
+#define WC_IX(i, n) wc_ix((i), (n), __LINE__)
+#else
+#define WC_IX(i, n) (i)
+#endif
+
 // Wave64 reductions through DPP lane moves (VALU, no LDS round trips): quad
 // swaps, half-row and row mirrors leave every lane with its 16-lane row
 // result; the four row results are read into scalar registers. Lanes outside

@@ -6,4 +6,8 @@
 // (consensus.rs:110-134). Same source as engine.hip, namespace wcg.
 #define WC_GLOBAL_STATE 1
 #define WC_ENGINE_NS wcg
+// register budget of the dual engine in this build (default: WC_WAVES_PER_EU)
+#ifdef WC_GSTATE_DUAL_WPE
+#define WC_DUAL_WAVES_PER_EU WC_GSTATE_DUAL_WPE
+#endif
 #include "engine.hip"

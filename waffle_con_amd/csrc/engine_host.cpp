@@ -32,6 +32,15 @@ namespace wch {
 
 namespace {
 constexpr uint32_t kLdsMax = 160 * 1024;  // one workgroup may take the whole CU's LDS
+// Bounds-checked builds (WC_CHECK): every workgroup's HBM regions (workspace,
+// global search state) are followed by a guard zone filled with kGuardByte
+// before the launch and verified after it (check_guards)
+#ifdef WC_CHECK
+constexpr uint64_t kGuard = 4096;
+constexpr uint8_t kGuardByte = 0xA5;
+#else
+constexpr uint64_t kGuard = 0;
+#endif
 
 // HBM the node pools of one launch may take: `share` of what is free plus the
 // launch's own cached workspace (reused by the launch)
@@ -190,6 +199,7 @@ struct Launch {
   uint32_t n_taken = 0;
   bool busy = false;
   double kernel_ms = 0;
+  uint64_t ws_stride = 0;  // WC_CHECK: workspace bytes per workgroup (guard zone at the end)
   std::vector<DevProblem> dp;
   std::vector<uint64_t> h_sroff;
   std::vector<uint32_t> h_srlen;
@@ -217,10 +227,15 @@ void destroy_launches(wc_ctx* ctx) {
 // launches the engine of `caps` (LDS or global-state build) on L's stream
 static int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
   if (caps.gstate) {
-    if (!L.gst.ensure(caps.gsb * L.grid)) return set_err(ctx, WC_E_HIP, "device allocation failed (search state)");
+    if (!L.gst.ensure((caps.gsb + kGuard) * L.grid)) return set_err(ctx, WC_E_HIP, "device allocation failed (search state)");
     a.gstate = (uint8_t*)L.gst.p;
-    a.gstate_stride = caps.gsb;
+    a.gstate_stride = caps.gsb + kGuard;
   }
+#ifdef WC_CHECK
+  L.ws_stride = a.ws_stride;
+  HIPCHK(hipMemsetAsync(L.ws.p, kGuardByte, a.ws_stride * L.grid, L.stream));
+  if (caps.gstate) HIPCHK(hipMemsetAsync(L.gst.p, kGuardByte, a.gstate_stride * L.grid, L.stream));
+#endif
   HIPCHK(hipEventRecord(L.ev0, L.stream));
   if (caps.gstate) {
     if (caps.sides == 1) wcg::launch_single_engine(a, L.grid, 0, L.stream);
@@ -296,7 +311,7 @@ static int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
     return set_err(ctx, WC_E_HIP, "device allocation failed (activation scratch)");
   if (!L.probs.ensure(P * sizeof(DevProblem)) || !L.sroff.ensure(L.h_sroff.size() * 8) ||
       !L.srlen.ensure(L.h_srlen.size() * 4) || !L.ract.ensure(L.h_ract.size() * 8) ||
-      !L.ws.ensure(caps.wsb * L.grid) || !L.counter.ensure(4))
+      !L.ws.ensure((caps.wsb + kGuard) * L.grid) || !L.counter.ensure(4))
     return set_err(ctx, WC_E_HIP, "device allocation failed (workspace)");
   HIPCHK(hipMemcpyAsync(L.probs.p, L.dp.data(), P * sizeof(DevProblem), hipMemcpyHostToDevice, L.stream));
   HIPCHK(hipMemcpyAsync(L.sroff.p, L.h_sroff.data(), L.h_sroff.size() * 8, hipMemcpyHostToDevice, L.stream));
@@ -318,7 +333,7 @@ static int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.rlen = (const uint32_t*)L.srlen.p;
   a.ractivate = (const int64_t*)L.ract.p;
   a.ws = (uint8_t*)L.ws.p;
-  a.ws_stride = caps.wsb;
+  a.ws_stride = caps.wsb + kGuard;
   a.pcap = caps.pcap;
   a.wcap = caps.wcap;
   a.lcap = caps.lcap;
@@ -401,8 +416,34 @@ static void bump(SubProb& s, uint32_t st) {
   s.attempts++;
 }
 
+#ifdef WC_CHECK
+// every workgroup's guard zones must still hold kGuardByte
+static int check_guards(wc_ctx* ctx, const Launch& L) {
+  std::vector<uint8_t> g(kGuard);
+  auto scan = [&](const DevBuf& b, uint64_t stride, const char* what) -> int {
+    for (uint32_t w = 0; w < L.grid; ++w) {
+      HIPCHK(hipMemcpy(g.data(), (const uint8_t*)b.p + (uint64_t)w * stride + stride - kGuard, kGuard,
+                       hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < kGuard; ++i)
+        if (g[i] != kGuardByte) {
+          fprintf(stderr, "[wc-check] %s guard of workgroup %u overwritten at +%llu (byte 0x%02x)\n", what, w,
+                  (unsigned long long)i, g[i]);
+          return set_err(ctx, WC_E_INVARIANT, std::string("bounds check: ") + what + " guard overwritten");
+        }
+    }
+    return WC_OK;
+  };
+  int rc = scan(L.ws, L.ws_stride, "workspace");
+  if (rc == WC_OK && L.caps.gstate) rc = scan(L.gst, L.caps.gsb + kGuard, "search-state");
+  return rc;
+}
+#endif
+
 static int launch_finish(wc_ctx* ctx, Launch& L) {
   HIPCHK(hipStreamSynchronize(L.stream));
+#ifdef WC_CHECK
+  if (const int grc = check_guards(ctx, L)) return grc;
+#endif
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, L.ev0, L.ev1));
   L.kernel_ms = ms;
@@ -545,7 +586,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   uint64_t* qroff = (uint64_t*)(rh + off_roff);
   int64_t* qract = (int64_t*)(rh + off_ract);
   uint32_t* qrlen = (uint32_t*)(rh + off_rlen);
-  const uint64_t wsb = caps.wsb + rtab_bytes(caps.nmax);
+  const uint64_t wsb = caps.wsb + rtab_bytes(caps.nmax) + kGuard;
   if (caps.act_m && !L.act.ensure(act_scr_u64(caps.act_m) * 8 * L.grid))
     return set_err(ctx, WC_E_HIP, "device allocation failed (activation scratch)");
   if (!L.ws.ensure(wsb * L.grid + 64) || !L.counter.ensure(4))

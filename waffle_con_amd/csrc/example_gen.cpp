@@ -145,27 +145,3 @@ void generate_test(uint8_t alphabet, size_t seq_len, size_t num_samples, double 
 }
 
 }  // namespace wc
-
-// Known-answer hooks for the RNG restatement (tests/test_cabi.py):
-// raw ChaCha(rounds) output words from a 32-byte seed, and StdRng-style u64s.
-extern "C" void wc_rng_words(const uint8_t* seed32, int rounds, uint32_t n, uint32_t* out) {
-  wc::ChaChaRng r(seed32, rounds);
-  for (uint32_t i = 0; i < n; ++i) out[i] = r.next_u32();
-}
-// StdRng::from_seed(seed) -> next_u64 ; then StdRng::from_rng(that) -> next_u64
-// (rand 0.8 src/rngs/std.rs test_stdrng_construction shape)
-extern "C" void wc_rng_stdrng_chain(const uint8_t* seed32, uint64_t* out2) {
-  wc::ChaChaRng r0(seed32, 12);
-  out2[0] = r0.next_u64();
-  uint8_t s2[32];
-  for (int k = 0; k < 8; ++k) {
-    uint32_t w = r0.next_u32();
-    memcpy(s2 + 4 * k, &w, 4);
-  }
-  wc::ChaChaRng r1(s2, 12);
-  out2[1] = r1.next_u64();
-}
-extern "C" void wc_rng_seed_from_u64(uint64_t seed, uint32_t n, uint32_t* out) {
-  wc::ChaChaRng r = wc::ChaChaRng::seed_from_u64(seed, 12);
-  for (uint32_t i = 0; i < n; ++i) out[i] = r.next_u32();
-}

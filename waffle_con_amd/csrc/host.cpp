@@ -101,33 +101,38 @@ DevConfig to_dev(const wc_config& c) {
 // The host side is one pass of memcpy into pinned staging (split over threads
 // by bytes), then a single DMA; the device buffer of `b` is reused when it is
 // large enough (wc_batch_refill), so a refill needs no allocation.
+// Transactional: the input is validated and the new read tables are built in
+// locals first; a buffer that must grow is allocated next to the old one. `b`
+// changes only when the whole upload succeeded. The one partial outcome is a
+// failed copy into a reused buffer: the batch is then marked invalid and every
+// later run on it returns WC_E_BAD_INPUT.
 int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* b) {
-  b->ctx = ctx;
-  b->probs.assign(n, BatchProblem());
-  b->rlen_h.clear();
+  std::vector<BatchProblem> probs(n);
   uint64_t nr = 0;
   for (uint32_t i = 0; i < n; ++i) {
     if (problems[i].n_reads && (!problems[i].reads || !problems[i].lens))
       return set_err(ctx, WC_E_BAD_INPUT, "problem with reads but no read/length arrays");
+    for (uint32_t r = 0; r < problems[i].n_reads; ++r) {
+      if (problems[i].lens[r] >= (1ull << 31)) return set_err(ctx, WC_E_BAD_INPUT, "read longer than 2^31 bytes");
+      if (problems[i].lens[r] && !problems[i].reads[r]) return set_err(ctx, WC_E_BAD_INPUT, "null read pointer");
+    }
     nr += problems[i].n_reads;
   }
-  std::vector<uint64_t>& roff = b->roff_h;
-  roff.assign(nr, 0);
-  b->rlen_h.resize(nr);
+  std::vector<uint64_t> roff(nr, 0);
+  std::vector<uint32_t> rlen(nr);
   std::vector<const uint8_t*> src(nr);
   uint64_t pos = 0, k = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const wc_problem& p = problems[i];
-    BatchProblem& q = b->probs[i];
+    BatchProblem& q = probs[i];
     q.read_begin = (uint32_t)k;
     q.n_reads = p.n_reads;
     q.offsets.assign(p.n_reads, -1);
     for (uint32_t r = 0; r < p.n_reads; ++r, ++k) {
       if (p.offsets) q.offsets[r] = p.offsets[r] < 0 ? -1 : p.offsets[r];
-      if (p.lens[r] >= (1ull << 31)) return set_err(ctx, WC_E_BAD_INPUT, "read longer than 2^31 bytes");
       roff[k] = pos;
       src[k] = p.reads[r];
-      b->rlen_h[k] = (uint32_t)p.lens[r];
+      rlen[k] = (uint32_t)p.lens[r];
       pos += (p.lens[r] + 15) & ~15ull;
       q.max_len = std::max<uint32_t>(q.max_len, (uint32_t)p.lens[r]);
       q.work += p.lens[r];
@@ -136,7 +141,6 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
   // reads start 16-byte aligned; 64 bytes of tail padding let the engine load
   // 64-byte windows with 16-byte accesses anywhere inside a read
   const uint64_t total = pos + 64;
-  b->bytes = total;
   std::vector<uint8_t> fallback;
   uint8_t* h = nullptr;
   if (ctx->upstage.ensure(total)) {
@@ -147,14 +151,29 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
   }
   auto fill = [&](uint64_t r0, uint64_t r1) {
     for (uint64_t r = r0; r < r1; ++r) {
-      const uint64_t len = b->rlen_h[r], pad = ((len + 15) & ~15ull) - len;
+      const uint64_t len = rlen[r], pad = ((len + 15) & ~15ull) - len;
       if (len) memcpy(h + roff[r], src[r], len);
       if (pad) memset(h + roff[r] + len, 0, pad);
     }
   };
-  if (!b->reads.ensure(total) || !b->roff.ensure(std::max<size_t>(roff.size(), 1) * 8) ||
-      !b->rlen.ensure(std::max<size_t>(b->rlen_h.size(), 1) * 4))
-    return set_err(ctx, WC_E_HIP, "device allocation failed (reads)");
+  // device buffers: reused when large enough, else new ones beside the old
+  DevBuf grown[3];
+  DevBuf* dst[3] = {&b->reads, &b->roff, &b->rlen};
+  const size_t want[3] = {total, std::max<size_t>(roff.size(), 1) * 8, std::max<size_t>(rlen.size(), 1) * 4};
+  for (int i = 0; i < 3; ++i) {
+    if (want[i] <= dst[i]->cap) continue;
+    if (!grown[i].ensure(want[i])) {
+      for (DevBuf& g : grown) g.release();
+      return set_err(ctx, WC_E_HIP, "device allocation failed (reads)");
+    }
+    dst[i] = &grown[i];
+  }
+  const bool in_place = dst[0] == &b->reads || dst[1] == &b->roff || dst[2] == &b->rlen;
+  if (in_place) b->valid = false;  // until every copy below has landed
+  auto fail = [&](const std::string& what) {
+    for (DevBuf& g : grown) g.release();
+    return set_err(ctx, WC_E_HIP, what);
+  };
   // chunks of >= 64 MiB (at most 8): the H2D copy of chunk k runs while the
   // host threads stage chunk k + 1; inside a chunk the reads are split into
   // contiguous ranges of about equal bytes, one per thread
@@ -174,9 +193,9 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
       std::vector<std::thread> th;
       uint64_t r0 = c_r0;
       for (uint64_t t = 0; t < nt; ++t) {
-        const uint64_t want = b0 + (b1 - b0) * (t + 1) / nt;
+        const uint64_t want_b = b0 + (b1 - b0) * (t + 1) / nt;
         uint64_t r1 = r0;
-        while (r1 < c_r1 && (t + 1 == nt || roff[r1] < want)) ++r1;
+        while (r1 < c_r1 && (t + 1 == nt || roff[r1] < want_b)) ++r1;
         th.emplace_back(fill, r0, r1);
         r0 = r1;
       }
@@ -185,14 +204,33 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
     const bool last = c + 1 == nch;
     if (last) memset(h + pos, 0, 64);
     const uint64_t e1 = last ? total : b1;
-    if (e1 > b0)
-      HIPCHK(hipMemcpyAsync((uint8_t*)b->reads.p + b0, h + b0, e1 - b0, hipMemcpyHostToDevice, ctx->stream));
+    if (e1 > b0 && hipMemcpyAsync((uint8_t*)dst[0]->p + b0, h + b0, e1 - b0, hipMemcpyHostToDevice, ctx->stream) !=
+                       hipSuccess)
+      return fail("read upload failed");
     c_r0 = c_r1;
   }
-  if (!roff.empty()) HIPCHK(hipMemcpyAsync(b->roff.p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-  if (!b->rlen_h.empty())
-    HIPCHK(hipMemcpyAsync(b->rlen.p, b->rlen_h.data(), b->rlen_h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (!roff.empty() &&
+      hipMemcpyAsync(dst[1]->p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+    return fail("read table upload failed");
+  if (!rlen.empty() &&
+      hipMemcpyAsync(dst[2]->p, rlen.data(), rlen.size() * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+    return fail("read table upload failed");
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail("read upload failed");
+  // commit
+  for (int i = 0; i < 3; ++i)
+    if (dst[i] == &grown[i]) {
+      DevBuf* old = i == 0 ? &b->reads : (i == 1 ? &b->roff : &b->rlen);
+      old->release();
+      *old = grown[i];
+      grown[i].p = nullptr;
+      grown[i].cap = 0;
+    }
+  b->ctx = ctx;
+  b->probs.swap(probs);
+  b->roff_h.swap(roff);
+  b->rlen_h.swap(rlen);
+  b->bytes = total;
+  b->valid = true;
   return WC_OK;
 }
 
@@ -341,6 +379,7 @@ uint64_t wc_batch_bytes(const wc_batch* b) { return b ? b->bytes : 0; }
 
 int wc_batch_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out) {
   *out = nullptr;
+  if (!b || !b->valid) return set_err(ctx, WC_E_BAD_INPUT, "batch is not usable (a failed refill left it incomplete)");
   if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
   std::unique_ptr<wc_results> R(new wc_results());
   int rc = batch_run(ctx, b, *cfg, 1, R.get());
@@ -351,6 +390,7 @@ int wc_batch_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_result
 
 int wc_batch_dual_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out) {
   *out = nullptr;
+  if (!b || !b->valid) return set_err(ctx, WC_E_BAD_INPUT, "batch is not usable (a failed refill left it incomplete)");
   if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, WC_E_HIP, "hipSetDevice failed");
   std::unique_ptr<wc_results> R(new wc_results());
   int rc = batch_run(ctx, b, *cfg, 2, R.get());

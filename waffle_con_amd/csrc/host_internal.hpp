@@ -114,6 +114,7 @@ struct wc_batch {
   std::vector<uint64_t> roff_h;
   DevBuf reads, roff, rlen;
   uint64_t bytes = 0;
+  bool valid = false;  // every read is on the device (upload_batch completed)
   ~wc_batch() {
     reads.release();
     roff.release();
