@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable CPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--api-threads", type=int, default=64, help="cfg2-api: native caller threads")
     return ap.parse_args()
 
 
@@ -236,6 +237,113 @@ class Cfg2:
                 "sample": "%d loci of the same workload (seeds %d..%d), C++ oracle, one locus per thread, %.1f s wall"
                           % (n, self.seeds[0], self.seeds[0] + n - 1, dt),
                 "gpu_matches_cpu_on_sample": ok, "checked": "sequences + per-read scores of every result"}
+
+
+class Cfg2Api(Cfg2):
+    """The reference's per-locus API (SURVEY §8(b) "Threading": consensus(&self)
+    is re-entrant, one instance per thread) from T native host threads, each
+    calling ConsensusDWFA::consensus on its own cfg2 loci one at a time, as a
+    Rust caller binding the C ABI would (tools/api_bench.cpp). The calls go
+    through the device's submission service (wc_service_consensus: persistent
+    launches shared by all callers). One step = every locus once. Reported
+    beside the value: a thread sweep, the per-call-launch path (one
+    wc_consensus_batch per call) at the same thread counts, and the batch path
+    (wc_batch_consensus over all loci at once) on the same loci."""
+    name = "cfg2-api"
+    scaling = "weak"
+
+    def __init__(self, a, rank, world, ctx):
+        import ctypes
+        from waffle_con_amd import _lib
+        from waffle_con_amd.consensus import _problems
+        a.loci = a.loci or 1024
+        super().__init__(a, rank, world, ctx)
+        self.threads = a.api_threads
+        path = os.path.join(ROOT, "tools", "libapibench.so")
+        if not os.path.exists(path):
+            raise RuntimeError("tools/libapibench.so is missing: build it with `make -C tools`")
+        self.H = ctypes.CDLL(path)
+        self.H.api_bench_run.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.POINTER(_lib.WcProblem),
+                                         ctypes.POINTER(_lib.WcConfig), ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_lib.WcServiceStats)]
+        self.arr, self.keep = _problems([(p, None) for p in self.loci])
+        self.ccfg = _lib.make_config(self.cfg)
+        self.lat = []
+
+    def run(self, mode, threads, n=None):
+        """n loci on `threads` native threads; returns (wall s, latencies ms, results, stats, service stats)."""
+        import ctypes
+        from waffle_con_amd import _lib
+        from waffle_con_amd.consensus import _single_results, _stats
+        n = n or self.n
+        res = (ctypes.c_void_p * n)()
+        lat = (ctypes.c_double * n)()
+        wall = ctypes.c_double()
+        sst = _lib.WcServiceStats()
+        L = _lib.lib()
+        rc = self.H.api_bench_run(_lib.LIB_PATH.encode(), self.ctx.device, mode, threads, 1, n, self.arr,
+                                  ctypes.byref(self.ccfg), res, lat, ctypes.byref(wall), ctypes.byref(sst))
+        if rc != 0:
+            raise RuntimeError("api_bench_run failed (rc %d)" % rc)
+        tot = {"kernel_ms": 0.0, "updates": 0, "w_out": 0, "compares": 0, "launches": 0}
+        out = []
+        for i in range(n):
+            st = _stats(res[i], L)
+            for k in ("updates", "w_out", "compares", "launches"):
+                tot[k] += st[k]
+            tot["kernel_ms"] += st["kernel_ms"]
+            out.append(_single_results(res[i], 1, self.cfg.consensus_cost, L, True)[0])
+        return wall.value, list(lat), out, tot, sst.as_dict()
+
+    def step(self):
+        wall, lat, res, tot, sst = self.run(0, self.threads)
+        bad = [r for r in res if isinstance(r, Exception)]
+        if bad:
+            raise RuntimeError("engine error: %s" % bad[0])
+        self.last = res
+        self.lat = lat
+        self.svc = sst
+        return tot, len(res)
+
+    def extra(self):
+        """Thread sweep (service and per-call launches) and the batch path on the
+        same loci; every service result is checked against the batch path's."""
+        def key(rs):
+            return [[(c.sequence(), list(c.scores())) for c in r] for r in rs]
+        batch_t0 = time.perf_counter()
+        bres, _ = self.batch.consensus(self.cfg)
+        batch_s = time.perf_counter() - batch_t0
+        same = key(self.last) == key(bres)
+        out = {"api_threads": self.threads, "api_matches_batch_path": same,
+               "api_latency_ms_median": statistics.median(self.lat),
+               "api_latency_ms_p90": sorted(self.lat)[int(0.9 * (len(self.lat) - 1))],
+               "api_service_stats": self.svc,
+               "batch_path_loci_per_s": self.n / batch_s}
+        sweep = {}
+        for t in sorted({16, 64, 256, self.threads}):
+            w, _, r, _, _ = self.run(0, t)
+            sweep[str(t)] = self.n / w
+            out["api_matches_batch_path"] &= key(r) == key(bres)
+        out["api_service_loci_per_s_by_threads"] = sweep
+        per_call = {}
+        for t in (16, 64):
+            n = min(self.n, 256)
+            w, _, r, _, _ = self.run(1, t, n)
+            per_call[str(t)] = n / w
+        out["api_per_call_launch_loci_per_s_by_threads"] = per_call
+        return out
+
+    def config(self):
+        c = super().config()
+        c["workload"] = ("ConsensusDWFA cfg2 through the reference's per-locus API: %d loci/GPU x %d reads x %d bp "
+                         "@ %g error, min_count %d, %d native caller threads, one locus per call"
+                         % (self.n, self.N, self.L, self.err, self.N // 4, self.threads))
+        c["api_threads"] = self.threads
+        return c
+
+    def e2e(self, steps):
+        return None
 
 
 class Cfg2Latency(Cfg2):
@@ -420,7 +528,8 @@ class Cfg4(Cfg5):
         return None  # the oracle needs ~2 min for this locus; measured separately
 
 
-WORKLOADS = {"cfg2": Cfg2, "cfg2-latency": Cfg2Latency, "cfg3": Cfg3, "cfg4": Cfg4, "cfg5": Cfg5}
+WORKLOADS = {"cfg2": Cfg2, "cfg2-api": Cfg2Api, "cfg2-latency": Cfg2Latency, "cfg3": Cfg3, "cfg4": Cfg4,
+             "cfg5": Cfg5}
 
 
 # ---------------------------------------------------------------------------
@@ -538,8 +647,8 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": elapsed / a.steps * 1e3,
-        "ms_per_step_median": statistics.median(step_ms),
+        "ms_per_step": statistics.median(step_ms),
+        "ms_per_step_mean": elapsed / a.steps * 1e3,
         "kernel_ms_per_step": kernel_ms / a.steps,
         "higher_is_better": True,
         "scaling": W.scaling,
@@ -551,6 +660,9 @@ def main():
         "gen_s": W.gen_s,
         "upload_s": W.upload_s,
     }
+    if hasattr(W, "extra"):
+        note("extra legs")
+        line.update(W.extra())
     if e2e:
         line["e2e_loci_per_s"], line["e2e_upload_ms"], line["e2e_compute_ms"] = e2e
         line["e2e_note"] = ("fresh batch every step: Python marshalling + pinned staging + H2D of the reads, "

@@ -5,7 +5,8 @@
  * FFI; its public API is ConsensusDWFA / DualConsensusDWFA /
  * PriorityConsensusDWFA + CdwfaConfig. A Rust shim keeps that
  * API and calls these entry points; consensus() of each engine maps to one
- * wc_*_batch call with a batch of one problem (or many, for throughput).
+ * wc_service_* call (many host threads share the device) or to wc_*_batch
+ * calls over many problems at once (throughput).
  *
  * Conventions: return 0 = OK, otherwise a WC_E_* code; wc_last_error() holds
  * the message. Caller owns inputs (copied during the call); result sets are
@@ -118,6 +119,30 @@ void wc_batch_free(wc_batch* b);
 uint64_t wc_batch_bytes(const wc_batch* b);
 int wc_batch_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out);
 int wc_batch_dual_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_results** out);
+
+/* Submission service: the reference's per-locus API from any number of host
+ * threads. ConsensusDWFA::consensus (consensus.rs:139) and
+ * DualConsensusDWFA::consensus (dual_consensus.rs:240) are `&self`, re-entrant
+ * and one instance per thread; a caller binds them here instead of one
+ * wc_*_batch call per locus. Concurrent calls share persistent engine launches
+ * on the device (one workgroup per in-flight locus; service.cpp), each call
+ * blocks until its own result is ready and returns a one-problem result set
+ * (free with wc_results_free), exactly what wc_consensus_batch /
+ * wc_dual_consensus_batch with that one problem return. Thread-safe; one
+ * service per device. arena_bytes: HBM for in-flight reads (0 = 4 GiB). */
+typedef struct wc_service wc_service;
+typedef struct wc_service_stats {
+  uint64_t calls;       /* consensus calls */
+  uint64_t served;      /* answered by the persistent launches */
+  uint64_t fallback;    /* answered by the batch path (offsets, > 256 reads, capacity retries) */
+  uint64_t lane_starts; /* persistent launches started */
+} wc_service_stats;
+int wc_service_create(int device, uint64_t arena_bytes, wc_service** out);
+void wc_service_destroy(wc_service* s);
+int wc_service_consensus(wc_service* s, const wc_config* cfg, const wc_problem* problem, wc_results** out);
+int wc_service_dual_consensus(wc_service* s, const wc_config* cfg, const wc_problem* problem, wc_results** out);
+int wc_service_get_stats(wc_service* s, wc_service_stats* out);
+const char* wc_service_last_error(wc_service* s);
 
 void wc_results_free(wc_results* r);
 uint32_t wc_results_problems(const wc_results* r);

@@ -1,0 +1,117 @@
+"""GPU parity of the submission service (wc_service_*, csrc/service.cpp): the
+reference's per-locus API (ConsensusDWFA / DualConsensusDWFA.consensus(),
+consensus.rs:139, dual_consensus.rs:240) called from many threads at once.
+Every result must equal the oracle's, whichever lane or path served it."""
+import threading
+
+import pytest
+
+import oracle_ffi as orc
+
+pytestmark = pytest.mark.gpu
+
+w = pytest.importorskip("waffle_con_amd")
+hip = pytest.importorskip("hip_runner")
+
+
+def _gen(L, N, err, seed):
+    return w.generate_test(4, L, N, err, seed)[1]
+
+
+def _run_threads(jobs, nthreads):
+    """jobs: list of callables; returns their results in order (exceptions re-raised)."""
+    out = [None] * len(jobs)
+    err = []
+    nxt = [0]
+    lock = threading.Lock()
+
+    def worker():
+        while True:
+            with lock:
+                i = nxt[0]
+                nxt[0] += 1
+            if i >= len(jobs):
+                return
+            try:
+                out[i] = jobs[i]()
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+                return
+
+    th = [threading.Thread(target=worker) for _ in range(nthreads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if err:
+        raise err[0]
+    return out
+
+
+def _stats():
+    from waffle_con_amd import _lib
+    return _lib.service().stats()
+
+
+def test_threaded_single_calls_match_oracle():
+    loci = [_gen(1200, 16, 0.02, 100 + s) for s in range(48)]
+    s0 = _stats()
+    got = _run_threads([lambda p=p: hip.consensus(p, counters=True, min_count=4) for p in loci], 24)
+    s1 = _stats()
+    for p, (g, gc) in zip(loci, got):
+        e, ec = orc.consensus(p, counters=True, min_count=4)
+        assert g == e
+        for k in ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored"):
+            assert gc[k] == ec[k], k
+    assert s1["served"] - s0["served"] == len(loci)
+
+
+def test_threaded_dual_calls_match_oracle():
+    def mix(s):
+        a, b = _gen(600, 10, 0.01, 2 * s), _gen(600, 10, 0.01, 2 * s + 1)
+        return [x for pair in zip(a, b) for x in pair]
+    loci = [mix(200 + s) for s in range(12)]
+    got = _run_threads([lambda p=p: hip.dual_consensus(p, min_count=3) for p in loci], 12)
+    for p, g in zip(loci, got):
+        assert g == orc.dual_consensus(p, min_count=3)
+
+
+def test_mixed_configs_and_kinds_concurrently():
+    """Different CdwfaConfigs and both engines at once: one lane each."""
+    single = [_gen(800, 12, 0.03, 300 + s) for s in range(16)]
+    jobs, exp = [], []
+    for i, p in enumerate(single):
+        kw = dict(min_count=3) if i % 2 else dict(min_count=4, consensus_cost=1)
+        jobs.append(lambda p=p, kw=kw: hip.consensus(p, **kw))
+        exp.append(orc.consensus(p, **kw))
+    a, b = _gen(500, 8, 0.01, 41), _gen(500, 8, 0.01, 42)
+    mix = [x for pair in zip(a, b) for x in pair]
+    jobs.append(lambda: hip.dual_consensus(mix, min_count=2))
+    exp.append(orc.dual_consensus(mix, min_count=2))
+    assert _run_threads(jobs, 17) == exp
+
+
+def test_larger_problem_restarts_the_lane():
+    """A lane planned for small loci drains and restarts for a larger one."""
+    small = [_gen(400, 8, 0.02, 500 + s) for s in range(6)]
+    big = _gen(3000, 40, 0.01, 77)
+    jobs = [lambda p=p: hip.consensus(p, min_count=2) for p in small] + [lambda: hip.consensus(big, min_count=2)]
+    got = _run_threads(jobs, 7)
+    assert got == [orc.consensus(p, min_count=2) for p in small + [big]]
+
+
+def test_offsets_and_deep_problems_take_the_batch_path():
+    base = _gen(700, 10, 0.02, 61)
+    offs = [None] * 8 + [100, 150]
+    s0 = _stats()
+    assert hip.consensus(base, offsets=offs, min_count=3) == orc.consensus(base, offsets=offs, min_count=3)
+    s1 = _stats()
+    assert s1["fallback"] - s0["fallback"] == 1
+
+
+def test_service_off_uses_per_call_launches(monkeypatch):
+    monkeypatch.setenv("WAFFLE_CON_SERVICE", "0")
+    p = _gen(600, 10, 0.02, 9)
+    s0 = _stats()
+    assert hip.consensus(p, min_count=3) == orc.consensus(p, min_count=3)
+    assert _stats()["calls"] == s0["calls"]

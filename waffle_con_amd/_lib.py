@@ -97,6 +97,13 @@ class WcStats(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class WcServiceStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("calls", "served", "fallback", "lane_starts")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 class WcDwfaJob(ctypes.Structure):
     _fields_ = [("baseline", _u8p), ("baseline_len", ctypes.c_uint64),
                 ("other", _u8p), ("other_len", ctypes.c_uint64),
@@ -118,6 +125,8 @@ EXPORTED = (
     "wc_results_chain", "wc_results_sequence_indices", "wc_results_stats",
     "wc_results_problem_stats", "wc_dwfa_batch", "wc_generate_test", "wc_gen_consensus",
     "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_wfa_ed_batch",
+    "wc_service_create", "wc_service_destroy", "wc_service_consensus", "wc_service_dual_consensus",
+    "wc_service_get_stats", "wc_service_last_error",
 )
 
 
@@ -194,6 +203,13 @@ def lib():
         L.wc_wfa_ed_batch.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(_u8p), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(_u8p), ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint8,
                                       ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]
+        L.wc_service_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(vp)]
+        L.wc_service_destroy.argtypes = [vp]
+        for f in ("wc_service_consensus", "wc_service_dual_consensus"):
+            getattr(L, f).argtypes = [vp, ctypes.POINTER(WcConfig), ctypes.POINTER(WcProblem), ctypes.POINTER(vp)]
+        L.wc_service_get_stats.argtypes = [vp, ctypes.POINTER(WcServiceStats)]
+        L.wc_service_last_error.argtypes = [vp]
+        L.wc_service_last_error.restype = ctypes.c_char_p
         _lib = L
         return L
 
@@ -234,6 +250,65 @@ def default_context():
         ctx = Context(dev)
         _ctx_local.ctx = ctx
     return ctx
+
+
+class Service:
+    """The device's submission service (wc_service_*, csrc/service.cpp): the
+    per-locus ConsensusDWFA / DualConsensusDWFA.consensus() calls of every
+    thread of this process share persistent engine launches on the device."""
+
+    def __init__(self, device=0, arena_bytes=0):
+        L = lib()
+        h = ctypes.c_void_p()
+        rc = L.wc_service_create(int(device), int(arena_bytes), ctypes.byref(h))
+        if rc != WC_OK:
+            raise WaffleConError("no usable HIP device %d for the waffle_con service (rc=%d)" % (device, rc), rc)
+        self.handle = h
+        self.device = device
+
+    def stats(self):
+        s = WcServiceStats()
+        lib().wc_service_get_stats(self.handle, ctypes.byref(s))
+        return s.as_dict()
+
+    def last_error(self):
+        return lib().wc_service_last_error(self.handle).decode()
+
+    def close(self):
+        if self.handle:
+            lib().wc_service_destroy(self.handle)
+            self.handle = None
+
+
+_services = {}
+
+
+def service_enabled():
+    return os.environ.get("WAFFLE_CON_SERVICE", "1") != "0"
+
+
+def service(device=None):
+    """The process-wide service of `device` (default: the default context's
+    device), created on first use and closed at exit."""
+    if device is None:
+        device = default_context().device
+    svc = _services.get(device)
+    if svc is None:
+        with _lock:
+            svc = _services.get(device)
+            if svc is None:
+                svc = Service(device)
+                _services[device] = svc
+                if len(_services) == 1:
+                    import atexit
+                    atexit.register(close_services)
+    return svc
+
+
+def close_services():
+    for svc in list(_services.values()):
+        svc.close()
+    _services.clear()
 
 
 def make_config(config):

@@ -187,6 +187,28 @@ def _problems(batch):
     return arr, keep
 
 
+def _service_call(fn, problem, config):
+    """One locus through the submission service (wc_service_consensus /
+    wc_service_dual_consensus): blocks this thread only (the GIL is released
+    while it waits). Returns the one-problem result set and its stats."""
+    svc = _lib.service()
+    L = _lib.lib()
+    arr, keep = _problems([problem])
+    cfg = _lib.make_config(config)
+    res = ctypes.c_void_p()
+    rc = getattr(L, fn)(svc.handle, ctypes.byref(cfg), arr, ctypes.byref(res))
+    if rc != _lib.WC_OK:
+        raise _lib.WaffleConError("%s failed: %s" % (fn, svc.last_error()), rc)
+    if fn == "wc_service_consensus":
+        stats = _stats(res, L)
+        return _single_results(res, 1, config.consensus_cost, L, False), stats
+    from .dual_consensus import _dual_results
+    try:
+        return _dual_results(res, [problem], config, L, False), _stats(res, L)
+    finally:
+        L.wc_results_free(res)
+
+
 def consensus_batch(problems, config=None, context=None, return_errors=False):
     """Run ConsensusDWFA::consensus for many independent problems at once.
 
@@ -239,9 +261,14 @@ class ConsensusDWFA:
         self._offsets.append(last_offset)
 
     def consensus(self):
-        """consensus.rs:139-351 (on the GPU)."""
+        """consensus.rs:139-351 (on the GPU). Through the device's submission
+        service (any number of threads share the device; WAFFLE_CON_SERVICE=0:
+        one batch call per locus instead)."""
         offs = self._offsets if any(o is not None for o in self._offsets) else None
-        (res,), stats = consensus_batch([(self._sequences, offs)], self._config)
+        if _lib.service_enabled():
+            (res,), stats = _service_call("wc_service_consensus", (self._sequences, offs), self._config)
+        else:
+            (res,), stats = consensus_batch([(self._sequences, offs)], self._config)
         self.last_stats = stats
         return res
 

@@ -24,23 +24,13 @@
 #include <queue>
 #include <thread>
 
-#include "host_internal.hpp"
+#include "sched.hpp"
 
 using namespace wc;
 
 namespace wch {
 
-namespace {
 constexpr uint32_t kLdsMax = 160 * 1024;  // one workgroup may take the whole CU's LDS
-// Bounds-checked builds (WC_CHECK): every workgroup's HBM regions (workspace,
-// global search state) are followed by a guard zone filled with kGuardByte
-// before the launch and verified after it (check_guards)
-#ifdef WC_CHECK
-constexpr uint64_t kGuard = 4096;
-constexpr uint8_t kGuardByte = 0xA5;
-#else
-constexpr uint64_t kGuard = 0;
-#endif
 
 // HBM the node pools of one launch may take: `share` of what is free plus the
 // launch's own cached workspace (reused by the launch)
@@ -49,28 +39,14 @@ uint64_t hbm_share(uint64_t cached, double share) {
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 32ull << 30;
   return (uint64_t)(((double)fr + (double)cached) * share);
 }
-}  // namespace
-
-struct Caps {
-  uint32_t sides = 1, pcap = 16, wcap = 64, lcap = 64, nmax = 1, chain = 0, rmax = 1, act_m = 0;
-  size_t lds = 0;   // dynamic LDS per workgroup (0 in the global-state build)
-  int per_cu = 1;
-  uint64_t wsb = 0, ob = 0;
-  bool gstate = false;  // search state in HBM (engine_gstate.hip): it does not fit LDS
-  bool narrow = false;  // 128-thread build (engine_narrow.hip)
-  bool lowlat = false;  // 256-thread build at 2 waves/SIMD (engine_lowlat.hip)
-  uint64_t gsb = 0;     // its bytes per workgroup
-  uint32_t conc = 0;    // workgroups the HBM share was planned for
-  bool pool_short = false;  // a retried item's node pool did not get its full growth
-};
 
 // Capacities of one launch over items[ids] (SURVEY §8(a) sizes): wavefront row
 // capacity from the longest read, consensus capacity from the longest read,
 // node-pool slots from the HBM share, linear-chain length from the LDS left at
 // the same occupancy. Retry outcomes raise them per item (log2 multipliers).
-static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vector<SubProb>& items,
+int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vector<SubProb>& items,
                      const std::vector<uint32_t>& ids, uint64_t hbm_budget, Caps& c, std::string& err,
-                     uint32_t max_per_cu = 4) {
+                     uint32_t max_per_cu) {
   uint32_t nmax = 1, maxlen = 1, wx = 0, px = 0, lx = 0, rx = 0;
   bool any_act = false;
   for (uint32_t id : ids) {
@@ -184,48 +160,13 @@ static int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const st
   return WC_OK;
 }
 
-// One engine launch and everything it owns.
-struct Launch {
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  DevBuf probs, sroff, srlen, ract, ws, counter, act, phases, gst;
-  HostBuf host;  // mapped: done[P] | status[P] | stats[P][S_NSTAT] | out[P]
-  HostBuf ring;  // mapped (stream launches): StreamCtl | problem ring | read-table rings
-  Caps caps;
-  uint32_t P = 0, grid = 0;
-  uint64_t off_status = 0, off_stats = 0, off_out = 0;
-  std::vector<uint32_t> ids;  // launch problem k -> caller item id
-  std::vector<uint8_t> taken;
-  uint32_t n_taken = 0;
-  bool busy = false;
-  double kernel_ms = 0;
-  uint64_t ws_stride = 0;  // WC_CHECK: workspace bytes per workgroup (guard zone at the end)
-  std::vector<DevProblem> dp;
-  std::vector<uint64_t> h_sroff;
-  std::vector<uint32_t> h_srlen;
-  std::vector<int64_t> h_ract;
-
-  volatile uint32_t* done() const { return (volatile uint32_t*)host.p; }
-  const uint32_t* status() const { return (const uint32_t*)((const uint8_t*)host.p + off_status); }
-  const uint64_t* stats() const { return (const uint64_t*)((const uint8_t*)host.p + off_stats); }
-  const uint8_t* out(uint32_t k) const { return (const uint8_t*)host.p + off_out + (uint64_t)k * caps.ob; }
-  ~Launch() {
-    for (DevBuf* b : {&probs, &sroff, &srlen, &ract, &ws, &counter, &act, &phases, &gst}) b->release();
-    host.release();
-    ring.release();
-    if (ev0) (void)hipEventDestroy(ev0);
-    if (ev1) (void)hipEventDestroy(ev1);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-};
-
 void destroy_launches(wc_ctx* ctx) {
   for (Launch* L : ctx->launches) delete L;
   ctx->launches.clear();
 }
 
 // launches the engine of `caps` (LDS or global-state build) on L's stream
-static int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
+int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
   if (caps.gstate) {
     if (!L.gst.ensure((caps.gsb + kGuard) * L.grid)) return set_err(ctx, WC_E_HIP, "device allocation failed (search state)");
     a.gstate = (uint8_t*)L.gst.p;
@@ -255,7 +196,7 @@ static int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps
   return WC_OK;
 }
 
-static Launch* launch_slot(wc_ctx* ctx, size_t k) {
+Launch* launch_slot(wc_ctx* ctx, size_t k) {
   while (ctx->launches.size() <= k) {
     Launch* L = new Launch();
     if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -269,7 +210,7 @@ static Launch* launch_slot(wc_ctx* ctx, size_t k) {
 }
 
 // Starts one engine launch over items[ids] (already in scheduling order).
-static int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg, const std::vector<SubProb>& items,
+int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg, const std::vector<SubProb>& items,
                         const std::vector<uint32_t>& ids, const Caps& caps) {
   L.caps = caps;
   L.ids = ids;
@@ -365,7 +306,7 @@ static int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
 
 // The outcome of launch problem k (its completion flag is set). Returns the
 // raw device status (ST_RETRY flags included); `o` gets records and counters.
-static uint32_t harvest(const Launch& L, uint32_t k, const SubProb& s, EngineOut& o) {
+uint32_t harvest(const Launch& L, uint32_t k, const SubProb& s, EngineOut& o) {
   const uint32_t st = L.status()[k];
   for (int q = 0; q < S_NSTAT; ++q) o.stats[q] = L.stats()[(uint64_t)k * S_NSTAT + q];
   o.recs.clear();
@@ -408,7 +349,7 @@ static uint32_t harvest(const Launch& L, uint32_t k, const SubProb& s, EngineOut
 }
 
 // capacity growth for a retried item
-static void bump(SubProb& s, uint32_t st) {
+void bump(SubProb& s, uint32_t st) {
   if (st & ST_RETRY_WCAP) s.wcap_x++;
   if (st & (ST_RETRY_PCAP | ST_RETRY_HEAP)) s.pcap_x += 2;
   if (st & ST_RETRY_LCAP) s.lcap_x++;
@@ -418,7 +359,7 @@ static void bump(SubProb& s, uint32_t st) {
 
 #ifdef WC_CHECK
 // every workgroup's guard zones must still hold kGuardByte
-static int check_guards(wc_ctx* ctx, const Launch& L) {
+int check_guards(wc_ctx* ctx, const Launch& L) {
   std::vector<uint8_t> g(kGuard);
   auto scan = [&](const DevBuf& b, uint64_t stride, const char* what) -> int {
     for (uint32_t w = 0; w < L.grid; ++w) {
@@ -439,7 +380,7 @@ static int check_guards(wc_ctx* ctx, const Launch& L) {
 }
 #endif
 
-static int launch_finish(wc_ctx* ctx, Launch& L) {
+int launch_finish(wc_ctx* ctx, Launch& L) {
   HIPCHK(hipStreamSynchronize(L.stream));
 #ifdef WC_CHECK
   if (const int grc = check_guards(ctx, L)) return grc;
@@ -462,7 +403,6 @@ static int launch_finish(wc_ctx* ctx, Launch& L) {
   return WC_OK;
 }
 
-constexpr uint32_t kMaxAttempts = 8;
 
 int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, std::vector<SubProb>& items,
                std::vector<EngineOut>& out, double& kernel_ms, uint64_t& launches,

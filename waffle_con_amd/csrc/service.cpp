@@ -1,0 +1,614 @@
+// Per-device submission service (wc_service_*): the reference's one-locus-per-
+// call API — ConsensusDWFA::consensus (consensus.rs:139) and
+// DualConsensusDWFA::consensus (dual_consensus.rs:240), `consensus(&self)`,
+// re-entrant, one instance per host thread (SURVEY §8(b) "Threading") — served
+// by persistent stream-mode engine launches instead of one small launch per
+// call.
+//
+// A caller packs its reads, reserves a range of the service's HBM read arena,
+// copies them there and queues the request; the service thread publishes it
+// into the host-mapped ring of a running launch ("lane": one persistent
+// launch of the single or dual engine for one CdwfaConfig; engine.hip stream
+// mode, the same machinery PriorityConsensusDWFA uses), whose workgroups claim
+// problems as they free up. The result comes back through the launch's
+// host-mapped result slots; the service builds the reference's result types
+// and wakes that caller. So any number of threads calling consensus() share
+// the whole GPU, one workgroup per in-flight locus, and a call costs one
+// locus's search latency plus a few tens of microseconds.
+//
+// Lanes start on demand and stop after kIdleMs without work (their idle
+// workgroups would otherwise hold CUs). Requests a lane cannot take — read
+// counts or lengths beyond its planned capacities — make it drain and restart
+// with larger ones. Offsets (add_sequence_offset), problems that still ask for
+// more capacity (ST_RETRY) and any service failure take the batch path on a
+// per-thread context (wc_consensus_batch with one problem), which plans and
+// retries capacities as usual: results never depend on the path.
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "sched.hpp"
+
+using namespace wc;
+using namespace wch;
+
+namespace {
+
+constexpr uint32_t kLanes = 4;            // concurrent (kind, config) lanes
+constexpr uint32_t kQcap = 1u << 14;      // published, unfinished problems per lane
+constexpr uint32_t kQslots = 1u << 21;    // their read-table entries
+constexpr double kIdleMs = 2.0;           // a lane with nothing to do stops after this
+constexpr uint64_t kArenaDefault = 4ull << 30;
+
+using Clock = std::chrono::steady_clock;
+
+struct Req {
+  uint32_t sides = 1;
+  wc_config cfg;
+  SubProb sp;                  // gid = 0..n-1 (read k of this request); activation plan
+  std::vector<uint64_t> roff;  // arena offsets of the reads
+  std::vector<uint32_t> rlen;
+  uint64_t aoff = 0;           // arena reservation
+  bool done = false;
+  uint32_t st = 0;             // raw device status (ST_RETRY flags included; ~0u = service failure)
+  EngineOut out;
+  std::condition_variable cv;
+};
+
+bool same_cfg(const wc_config& a, const wc_config& b) { return memcmp(&a, &b, sizeof(wc_config)) == 0; }
+
+struct Lane {
+  bool running = false;
+  bool draining = false;  // a queued request needs larger capacities: finish, then restart
+  uint32_t sides = 1;
+  wc_config cfg;
+  uint32_t nmax = 0, maxlen = 0;  // capacity envelope the launch was planned for
+  Launch* L = nullptr;
+  volatile StreamCtl* sc = nullptr;
+  DevProblem* qp = nullptr;
+  uint64_t* qroff = nullptr;
+  int64_t* qract = nullptr;
+  uint32_t* qrlen = nullptr;
+  std::vector<Req*> seq_req;
+  std::vector<uint64_t> seq_rw;
+  std::vector<uint8_t> seq_done;
+  uint32_t oldest = 0, outstanding = 0, published_tail = 0, beat = 0;
+  uint32_t grid_full = 0;  // workgroups a full-chip launch of this lane would ask for
+  bool can_grow = false;   // a restart with more requests waiting would get more workgroups
+  uint64_t rw = 0;
+  Clock::time_point idle_since;
+};
+
+}  // namespace
+
+struct wc_service {
+  int device = 0;
+  wc_ctx* ctx = nullptr;
+  std::mutex mu;
+  std::condition_variable cv_svc;    // requests arrived
+  std::condition_variable cv_arena;  // arena space was released
+  std::deque<Req*> ready;            // copied to the arena, not yet published (FIFO)
+  DevBuf arena;
+  std::map<uint64_t, uint64_t> live;  // arena reservations: offset -> bytes
+  uint64_t cursor = 0;
+  Lane lanes[kLanes];
+  std::thread th;
+  bool stop = false;
+  bool failed = false;  // a HIP failure disabled the service: every call takes the batch path
+  std::string err;
+  wc_service_stats stats{};
+};
+
+namespace {
+
+// ---- arena reservations (caller threads, under mu) ----
+bool arena_fits(const wc_service* S, uint64_t p, uint64_t b) {
+  if (p + b > S->arena.cap) return false;
+  auto it = S->live.upper_bound(p);
+  if (it != S->live.end() && it->first < p + b) return false;
+  if (it != S->live.begin()) {
+    const auto pr = std::prev(it);
+    if (pr->first + pr->second > p) return false;
+  }
+  return true;
+}
+bool arena_alloc(wc_service* S, uint64_t b, uint64_t& off) {
+  uint64_t p = S->cursor;
+  bool ok = arena_fits(S, p, b);
+  if (!ok && arena_fits(S, 0, b)) {
+    p = 0;
+    ok = true;
+  }
+  if (!ok)
+    for (const auto& kv : S->live)
+      if (arena_fits(S, kv.first + kv.second, b)) {
+        p = kv.first + kv.second;
+        ok = true;
+        break;
+      }
+  if (!ok) return false;
+  S->live[p] = b;
+  S->cursor = p + b;
+  off = p;
+  return true;
+}
+
+void complete(wc_service* S, Req* q, uint32_t st) {
+  q->st = st;
+  q->done = true;
+  S->live.erase(q->aoff);
+  S->cv_arena.notify_all();
+  q->cv.notify_one();
+}
+
+// ---- lanes (service thread, under mu) ----
+bool lane_fits(const Lane& ln, const Req* q) {
+  return ln.running && !ln.draining && ln.sides == q->sides && same_cfg(ln.cfg, q->cfg) &&
+         q->sp.gid.size() <= ln.nmax && q->sp.max_len <= ln.maxlen;
+}
+
+// starts lane k for the requests waiting with q's kind and config
+int lane_start(wc_service* S, uint32_t k, const Req* q) {
+  Lane& ln = S->lanes[k];
+  ln = Lane();
+  ln.sides = q->sides;
+  ln.cfg = q->cfg;
+  // capacity envelope: every waiting request of this kind and config, rounded up
+  uint32_t nmax = 1, maxlen = 1;
+  for (const Req* r : S->ready)
+    if (r->sides == q->sides && same_cfg(r->cfg, q->cfg)) {
+      nmax = std::max<uint32_t>(nmax, (uint32_t)r->sp.gid.size());
+      maxlen = std::max(maxlen, r->sp.max_len);
+    }
+  ln.nmax = std::min<uint32_t>((nmax + 7) / 8 * 8, (uint32_t)kBlock);
+  ln.maxlen = (maxlen + 1023) / 1024 * 1024;
+  std::vector<SubProb> env(1);
+  env[0].gid.assign(ln.nmax, 0);
+  env[0].max_len = ln.maxlen;
+  wc_ctx* ctx = S->ctx;
+  Launch* L = launch_slot(ctx, k);
+  if (!L) return set_err(ctx, WC_E_HIP, "stream creation failed");
+  ln.L = L;
+  // workgroups: twice the requests waiting for this lane (callers block on
+  // their result, so that bounds what it will see), 64 at least; the lane
+  // restarts larger if its callers outgrow it. Planned like a batch launch of
+  // that many problems (a small one gets the 2-wave build), with a quarter of
+  // the free HBM for the node pools.
+  uint32_t waiting = 0;
+  for (const Req* r : S->ready) waiting += r->sides == q->sides && same_cfg(r->cfg, q->cfg);
+  ln.grid_full = 4 * (uint32_t)ctx->n_cu;
+  const uint32_t want = std::min(ln.grid_full, std::max(64u, (2 * waiting + 63) / 64 * 64));
+  std::vector<uint32_t> ids(want, 0);
+  Caps caps;
+  std::string err;
+  int rc = plan_caps(ctx, ln.cfg, ln.sides, env, ids, hbm_share(L->ws.cap, 0.25), caps, err);
+  if (rc != WC_OK) return set_err(ctx, rc, err);
+  L->caps = caps;
+  L->grid = std::min<uint32_t>((uint32_t)std::max(1, caps.per_cu) * (uint32_t)ctx->n_cu, std::max(1u, caps.conc));
+  // a larger launch would have more workgroups only if this one got all it asked for
+  ln.can_grow = L->grid >= want && want < ln.grid_full;
+  L->P = 2 * L->grid;  // two output slots per workgroup
+  L->kernel_ms = 0;
+  const uint32_t P = L->P;
+  L->off_status = align16((uint64_t)P * 4);
+  L->off_stats = L->off_status + align16((uint64_t)P * 4);
+  L->off_out = L->off_stats + align16((uint64_t)P * S_NSTAT * 8);
+  if (!L->host.ensure(L->off_out + (uint64_t)P * caps.ob, true))
+    return set_err(ctx, WC_E_HIP, "pinned host allocation failed (service results)");
+  memset(L->host.p, 0, L->off_out);
+  const uint64_t off_q = align16(sizeof(StreamCtl));
+  const uint64_t off_roff = off_q + align16((uint64_t)kQcap * sizeof(DevProblem));
+  const uint64_t off_ract = off_roff + (uint64_t)kQslots * 8;
+  const uint64_t off_rlen = off_ract + (uint64_t)kQslots * 8;
+  if (!L->ring.ensure(off_rlen + (uint64_t)kQslots * 4, true))
+    return set_err(ctx, WC_E_HIP, "pinned host allocation failed (service ring)");
+  uint8_t* rh = (uint8_t*)L->ring.p;
+  ln.sc = (volatile StreamCtl*)rh;
+  ln.sc->tail = 0;
+  ln.sc->stop = 0;
+  ln.sc->abort = 0;
+  ln.sc->heartbeat = 0;
+  ln.qp = (DevProblem*)(rh + off_q);
+  ln.qroff = (uint64_t*)(rh + off_roff);
+  ln.qract = (int64_t*)(rh + off_ract);
+  ln.qrlen = (uint32_t*)(rh + off_rlen);
+  const uint64_t wsb = caps.wsb + rtab_bytes(caps.nmax) + kGuard;
+  if (!L->ws.ensure(wsb * L->grid + 64) || !L->counter.ensure(4))
+    return set_err(ctx, WC_E_HIP, "device allocation failed (service workspace)");
+  HIPCHK(hipMemsetAsync(L->counter.p, 0, 4, L->stream));
+  void *dhost = nullptr, *dring = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dhost, L->host.p, 0));
+  HIPCHK(hipHostGetDevicePointer(&dring, L->ring.p, 0));
+  uint8_t* dh = (uint8_t*)dhost;
+  uint8_t* dr = (uint8_t*)dring;
+  int clk = 0;
+  if (hipDeviceGetAttribute(&clk, hipDeviceAttributeWallClockRate, S->device) != hipSuccess || clk <= 0) clk = 100000;
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.cfg = to_dev(ln.cfg);
+  a.problems = (const DevProblem*)(dr + off_q);
+  a.sides = ln.sides;
+  a.rbytes = (const uint8_t*)S->arena.p;
+  a.roff = (const uint64_t*)(dr + off_roff);
+  a.rlen = (const uint32_t*)(dr + off_rlen);
+  a.ractivate = (const int64_t*)(dr + off_ract);
+  a.ws = (uint8_t*)L->ws.p;
+  a.ws_stride = wsb;
+  a.pcap = caps.pcap;
+  a.wcap = caps.wcap;
+  a.lcap = caps.lcap;
+  a.nmax = caps.nmax;
+  a.rmax = caps.rmax;
+  a.chain = caps.chain;
+  a.out = dh + L->off_out;
+  a.out_stride = caps.ob;
+  a.status = (uint32_t*)(dh + L->off_status);
+  a.stats = (uint64_t*)(dh + L->off_stats);
+  a.done = (uint32_t*)dh;
+  a.stream = 1;
+  a.qcap = kQcap;
+  a.qslots = kQslots;
+  a.sctl = (StreamCtl*)dr;
+  a.qhead = (uint32_t*)L->counter.p;
+  a.idle_ticks = (uint64_t)clk * 1000ull * 30ull;  // 30 s without a heartbeat: the host is gone
+  rc = launch_kernel(ctx, *L, a, caps);
+  if (rc != WC_OK) return rc;
+  L->busy = true;
+  ln.running = true;
+  ln.idle_since = Clock::now();
+  S->stats.lane_starts++;
+  if (getenv("WC_LAUNCH_LOG"))
+    fprintf(stderr, "[wc] service lane %u: sides=%u grid=%u per_cu=%d nmax=%u maxlen=%u pcap=%u wcap=%u lcap=%u chain=%u\n",
+            k, ln.sides, L->grid, caps.per_cu, caps.nmax, ln.maxlen, caps.pcap, caps.wcap, caps.lcap, caps.chain);
+  return WC_OK;
+}
+
+// publishes q into lane ln's ring; false when the ring is full
+bool lane_publish(Lane& ln, Req* q) {
+  const uint32_t seq = (uint32_t)ln.seq_req.size();
+  const uint32_t n = (uint32_t)q->sp.gid.size();
+  const uint64_t ow = ln.oldest < seq ? ln.seq_rw[ln.oldest] : ln.rw;
+  if (seq - ln.oldest >= kQcap || ln.rw + n - ow > kQslots) return false;
+  DevProblem d;
+  memset(&d, 0, sizeof(d));
+  d.read_begin = (uint32_t)(ln.rw % kQslots);
+  d.n_reads = n;
+  d.max_read_len = q->sp.max_len;
+  d.n_active = q->sp.n_active;
+  d.max_act = q->sp.max_act;
+  ln.qp[seq % kQcap] = d;
+  for (uint32_t r = 0; r < n; ++r) {
+    const uint64_t k = (ln.rw + r) % kQslots;
+    ln.qroff[k] = q->roff[r];
+    ln.qract[k] = q->sp.act[r];
+    ln.qrlen[k] = q->rlen[r];
+  }
+  ln.seq_req.push_back(q);
+  ln.seq_rw.push_back(ln.rw);
+  ln.seq_done.push_back(0);
+  ln.rw += n;
+  ln.outstanding++;
+  return true;
+}
+
+// harvests every finished problem of the lane; returns how many
+uint32_t lane_poll(wc_service* S, Lane& ln) {
+  Launch& L = *ln.L;
+  volatile uint32_t* done = L.done();
+  uint32_t got = 0;
+  for (uint32_t slot = 0; slot < L.P; ++slot) {
+    const uint32_t v = __atomic_load_n(&done[slot], __ATOMIC_ACQUIRE);
+    if (!v) continue;
+    const uint32_t seq = v - 1;
+    Req* q = ln.seq_req[seq];
+    const uint32_t st = harvest(L, slot, q->sp, q->out);
+    __atomic_store_n(&done[slot], 0u, __ATOMIC_RELEASE);  // the slot may be reused
+    ln.seq_done[seq] = 1;
+    ln.outstanding--;
+    while (ln.oldest < ln.seq_req.size() && ln.seq_done[ln.oldest]) ln.oldest++;
+    complete(S, q, st);
+    got++;
+  }
+  return got;
+}
+
+// ends the lane's launch (nothing may be outstanding unless it failed)
+void lane_stop(wc_service* S, Lane& ln, bool failed) {
+  __atomic_store_n(&ln.sc->stop, 1u, __ATOMIC_RELEASE);
+  (void)launch_finish(S->ctx, *ln.L);
+  if (failed)
+    for (uint32_t s = ln.oldest; s < ln.seq_req.size(); ++s)
+      if (!ln.seq_done[s]) complete(S, ln.seq_req[s], ~0u);
+  ln.running = false;
+  ln.draining = false;
+  ln.seq_req.clear();
+  ln.seq_rw.clear();
+  ln.seq_done.clear();
+}
+
+void service_loop(wc_service* S) {
+  (void)hipSetDevice(S->device);
+  std::unique_lock<std::mutex> lk(S->mu);
+  for (;;) {
+    bool progress = false;
+    // 1. publish in arrival order: each request to the running lane of its kind
+    //    and config; one that no lane can take starts a lane (a free one, or an
+    //    idle one is replaced), or makes its lane drain and restart with larger
+    //    capacities. A request that has to wait holds back the ones after it
+    //    only for its own lane.
+    std::vector<uint8_t> blocked(kLanes, 0);
+    for (auto it = S->ready.begin(); it != S->ready.end();) {
+      Req* q = *it;
+      int k = -1;
+      for (uint32_t j = 0; j < kLanes; ++j)
+        if (S->lanes[j].running && S->lanes[j].sides == q->sides && same_cfg(S->lanes[j].cfg, q->cfg)) k = (int)j;
+      if (k >= 0 && !blocked[k] && lane_fits(S->lanes[k], q)) {
+        if (lane_publish(S->lanes[k], q)) {
+          it = S->ready.erase(it);
+          progress = true;
+          continue;
+        }
+        blocked[k] = 1;  // ring full
+      } else if (k >= 0) {
+        if (!lane_fits(S->lanes[k], q) && !S->lanes[k].draining) S->lanes[k].draining = true;
+        blocked[k] = 1;
+      } else if (!S->failed) {
+        int f = -1;
+        for (uint32_t j = 0; j < kLanes && f < 0; ++j)
+          if (!S->lanes[j].running) f = (int)j;
+        for (uint32_t j = 0; j < kLanes && f < 0; ++j)  // replace an idle lane of another config
+          if (S->lanes[j].outstanding == 0) {
+            lane_stop(S, S->lanes[j], false);
+            f = (int)j;
+          }
+        if (f >= 0) {
+          if (lane_start(S, (uint32_t)f, q) != WC_OK) {
+            S->failed = true;
+            S->err = S->ctx->err;
+            continue;  // the request is completed below as a service failure
+          }
+          progress = true;
+          continue;  // publish it (and its companions) on the next pass
+        }
+      }
+      ++it;
+    }
+    if (S->failed) {
+      for (Req* q : S->ready) complete(S, q, ~0u);
+      S->ready.clear();
+    }
+    // 2. harvest, 3. stop lanes that are done (idle, draining and empty, failed)
+    for (uint32_t j = 0; j < kLanes; ++j) {
+      Lane& ln = S->lanes[j];
+      if (!ln.running) continue;
+      __atomic_store_n(&ln.sc->heartbeat, ++ln.beat, __ATOMIC_RELAXED);
+      const uint32_t ntail = (uint32_t)ln.seq_req.size();
+      if (ntail != ln.published_tail) {
+        std::atomic_thread_fence(std::memory_order_release);
+        __atomic_store_n(&ln.sc->tail, ntail, __ATOMIC_RELEASE);
+        ln.published_tail = ntail;
+      }
+      if (lane_poll(S, ln)) progress = true;
+      // a lane planned for fewer workgroups than its callers keep busy drains
+      // and restarts with a larger grid
+      if (!ln.draining && ln.can_grow) {
+        uint32_t waiting = 0;
+        for (const Req* r : S->ready) waiting += r->sides == ln.sides && same_cfg(r->cfg, ln.cfg);
+        if (2 * (ln.outstanding + waiting) > 3 * ln.L->grid) ln.draining = true;
+      }
+      if (ln.outstanding > 0) {
+        ln.idle_since = Clock::now();
+        if (ln.sc->abort || hipStreamQuery(ln.L->stream) == hipSuccess) {  // ended with problems out: fail them over
+          lane_stop(S, ln, true);
+          progress = true;
+        }
+        continue;
+      }
+      const double idle = std::chrono::duration<double, std::milli>(Clock::now() - ln.idle_since).count();
+      if (ln.draining || S->stop || idle > kIdleMs) {
+        lane_stop(S, ln, false);
+        progress = true;
+      }
+    }
+    bool any = false;
+    for (const Lane& ln : S->lanes) any |= ln.running;
+    if (S->stop && S->ready.empty() && !any) break;
+    if (!progress) {
+      if (!any && S->ready.empty()) S->cv_svc.wait(lk, [&] { return S->stop || !S->ready.empty(); });
+      else S->cv_svc.wait_for(lk, std::chrono::microseconds(20));
+    }
+  }
+}
+
+// the batch path on a per-thread context (offsets, capacity retries, service failures)
+struct ThreadCtx {
+  std::map<int, wc_ctx*> ctx;
+  ~ThreadCtx() {
+    for (auto& kv : ctx) wc_ctx_destroy(kv.second);
+  }
+};
+int fallback(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p, wc_results** out) {
+  static thread_local ThreadCtx tl;
+  wc_ctx*& c = tl.ctx[S->device];
+  if (!c) {
+    const int rc = wc_ctx_create(S->device, &c);
+    if (rc != WC_OK) {
+      c = nullptr;
+      return rc;
+    }
+  }
+  {
+    std::lock_guard<std::mutex> g(S->mu);
+    S->stats.fallback++;
+  }
+  const int rc = sides == 1 ? wc_consensus_batch(c, cfg, 1, p, out) : wc_dual_consensus_batch(c, cfg, 1, p, out);
+  if (rc != WC_OK) {
+    std::lock_guard<std::mutex> g(S->mu);
+    S->err = wc_last_error(c);
+  }
+  return rc;
+}
+
+// a caller thread's pinned staging buffer and copy stream (per device)
+struct ThreadStage {
+  HostBuf buf;
+  hipStream_t stream = nullptr;
+  ~ThreadStage() {
+    buf.release();
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+ThreadStage& thread_stage(int device) {
+  static thread_local std::map<int, ThreadStage> tl;
+  ThreadStage& ts = tl[device];
+  if (!ts.stream && hipSetDevice(device) == hipSuccess)
+    if (hipStreamCreateWithFlags(&ts.stream, hipStreamNonBlocking) != hipSuccess) ts.stream = nullptr;
+  return ts;
+}
+
+int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p, wc_results** out) {
+  *out = nullptr;
+  if (!S || !cfg || !p) return WC_E_BAD_INPUT;
+  const auto t0 = Clock::now();
+  const uint32_t n = p->n_reads;
+  if (n && (!p->reads || !p->lens)) return WC_E_BAD_INPUT;
+  for (uint32_t r = 0; r < n; ++r)
+    if (p->lens[r] >= (1ull << 31) || (p->lens[r] && !p->reads[r])) return WC_E_BAD_INPUT;
+  std::unique_ptr<Req> q(new Req());
+  q->sides = sides;
+  q->cfg = *cfg;
+  std::vector<int64_t> offs(n, -1);
+  if (p->offsets)
+    for (uint32_t r = 0; r < n; ++r) offs[r] = p->offsets[r] < 0 ? -1 : p->offsets[r];
+  std::string aerr;
+  const int arc = activation_plan(*cfg, offs, q->sp, aerr);
+  bool failed;
+  {
+    std::lock_guard<std::mutex> g(S->mu);
+    failed = S->failed;
+    S->stats.calls++;
+  }
+  // offsets (activation scratch), deep problems (> 256 reads: the batch path
+  // gives them a launch of their own) and a disabled service take the batch path
+  if (arc != WC_OK || q->sp.max_act > 0 || n > (uint32_t)kBlock || failed) return fallback(S, sides, cfg, p, out);
+  // reads back to back (16-byte aligned) plus 64 bytes of tail padding,
+  // staged in this thread's pinned buffer and copied on its own stream (DMA at
+  // full link speed, overlapping other callers' copies)
+  std::vector<uint64_t> rel(n);
+  uint64_t total = 0;
+  for (uint32_t r = 0; r < n; ++r) {
+    rel[r] = total;
+    total += (p->lens[r] + 15) & ~15ull;
+  }
+  total += 64;
+  ThreadStage& ts = thread_stage(S->device);
+  if (!ts.stream || !ts.buf.ensure(total)) return fallback(S, sides, cfg, p, out);
+  uint8_t* h = (uint8_t*)ts.buf.p;
+  q->sp.gid.resize(n);
+  q->rlen.resize(n);
+  q->roff.resize(n);
+  for (uint32_t r = 0; r < n; ++r) {
+    const uint64_t len = p->lens[r], pad = ((len + 15) & ~15ull) - len;
+    if (len) memcpy(h + rel[r], p->reads[r], len);
+    if (pad) memset(h + rel[r] + len, 0, pad);
+    q->sp.gid[r] = r;
+    q->rlen[r] = (uint32_t)len;
+    q->sp.max_len = std::max(q->sp.max_len, q->rlen[r]);
+    q->sp.work += len;
+  }
+  memset(h + total - 64, 0, 64);
+  {
+    std::unique_lock<std::mutex> lk(S->mu);
+    if (total > S->arena.cap / 4) {
+      lk.unlock();
+      return fallback(S, sides, cfg, p, out);
+    }
+    S->cv_arena.wait(lk, [&] { return S->failed || arena_alloc(S, total, q->aoff); });
+    if (S->failed) {
+      lk.unlock();
+      return fallback(S, sides, cfg, p, out);
+    }
+  }
+  if (hipMemcpyAsync((uint8_t*)S->arena.p + q->aoff, h, total, hipMemcpyHostToDevice, ts.stream) != hipSuccess ||
+      hipStreamSynchronize(ts.stream) != hipSuccess) {
+    std::lock_guard<std::mutex> g(S->mu);
+    S->live.erase(q->aoff);
+    S->cv_arena.notify_all();
+    return fallback(S, sides, cfg, p, out);
+  }
+  for (uint32_t r = 0; r < n; ++r) q->roff[r] = q->aoff + rel[r];
+  {
+    std::unique_lock<std::mutex> lk(S->mu);
+    S->ready.push_back(q.get());
+    S->cv_svc.notify_one();
+    q->cv.wait(lk, [&] { return q->done; });
+    if (q->st != ~0u && !(q->st & ST_RETRY)) S->stats.served++;
+  }
+  if (q->st == ~0u || (q->st & ST_RETRY)) return fallback(S, sides, cfg, p, out);
+  std::unique_ptr<wc_results> R(new wc_results());
+  R->kind = sides == 1 ? 0 : 1;
+  R->probs.resize(1);
+  if (sides == 1) build_single(q->out, cfg->consensus_cost, R->probs[0]);
+  else build_dual(q->out, n, cfg->consensus_cost, R->probs[0]);
+  fill_stats(R.get(), 0.0, 0, std::chrono::duration<double, std::milli>(Clock::now() - t0).count());
+  *out = R.release();
+  return WC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wc_service_create(int device, uint64_t arena_bytes, wc_service** out) {
+  *out = nullptr;
+  std::unique_ptr<wc_service> S(new wc_service());
+  S->device = device;
+  int rc = wc_ctx_create(device, &S->ctx);
+  if (rc != WC_OK) return rc;
+  if (!S->arena.ensure(arena_bytes ? arena_bytes : kArenaDefault)) {
+    wc_ctx_destroy(S->ctx);
+    return WC_E_HIP;
+  }
+  S->th = std::thread(service_loop, S.get());
+  *out = S.release();
+  return WC_OK;
+}
+
+void wc_service_destroy(wc_service* S) {
+  if (!S) return;
+  {
+    std::lock_guard<std::mutex> g(S->mu);
+    S->stop = true;
+  }
+  S->cv_svc.notify_all();
+  S->th.join();
+  (void)hipSetDevice(S->device);
+  S->arena.release();
+  wc_ctx_destroy(S->ctx);
+  delete S;
+}
+
+int wc_service_consensus(wc_service* s, const wc_config* cfg, const wc_problem* problem, wc_results** out) {
+  return service_call(s, 1, cfg, problem, out);
+}
+
+int wc_service_dual_consensus(wc_service* s, const wc_config* cfg, const wc_problem* problem, wc_results** out) {
+  return service_call(s, 2, cfg, problem, out);
+}
+
+int wc_service_get_stats(wc_service* s, wc_service_stats* out) {
+  if (!s || !out) return WC_E_BAD_INPUT;
+  std::lock_guard<std::mutex> g(s->mu);
+  *out = s->stats;
+  return WC_OK;
+}
+
+const char* wc_service_last_error(wc_service* s) { return s ? s->err.c_str() : "no service"; }
+
+}  // extern "C"

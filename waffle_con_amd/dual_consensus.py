@@ -129,7 +129,11 @@ class DualConsensusDWFA:
     def consensus(self):
         """dual_consensus.rs:240-787 (on the GPU)."""
         offs = self._offsets if any(o is not None for o in self._offsets) else None
-        (res,), stats = dual_consensus_batch([(self._sequences, offs)], self._config)
+        if _lib.service_enabled():
+            from .consensus import _service_call
+            (res,), stats = _service_call("wc_service_dual_consensus", (self._sequences, offs), self._config)
+        else:
+            (res,), stats = dual_consensus_batch([(self._sequences, offs)], self._config)
         self.last_stats = stats
         return res
 
