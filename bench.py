@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--api-threads", type=int, default=64, help="cfg2-api: native caller threads")
+    ap.add_argument("--cfg5-loci", type=int, default=10000,
+                    help="cfg2 (default line): also run the fixed cfg5 batch of this many loci, strong-scaled "
+                         "over the ranks (0 = skip)")
     return ap.parse_args()
 
 
@@ -117,6 +120,19 @@ def gen_cfg2(seeds, L=10000, N=100, err=0.005):
         return list(ex.map(lambda s: w.generate_test(4, L, N, err, s)[1], seeds))
 
 
+def pool_map(fn, items):
+    """fn over items in worker processes forked before this process touches
+    the GPU (input generation of the large workloads; threads are GIL-bound)."""
+    n = max(1, min(16, usable_cpus()[0]))
+    if n == 1 or len(items) < 64:
+        return [fn(x) for x in items]
+    import multiprocessing as mp
+    import torch
+    assert not torch.cuda.is_initialized(), "pool_map must run before the GPU is initialised"
+    with mp.get_context("fork").Pool(n) as p:
+        return p.map(fn, items, chunksize=max(1, len(items) // (8 * n)))
+
+
 def orc():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi
@@ -141,7 +157,7 @@ class Cfg2:
     scaling = "weak"
     kernel = "wc::single_engine_kernel"
 
-    def __init__(self, a, rank, world, ctx):
+    def __init__(self, a, rank, world, ctx, pre=None):
         import waffle_con_amd as w
         from waffle_con_amd.cdwfa_config import CdwfaConfig
         self.a, self.ctx, self.rank, self.world = a, ctx, rank, world
@@ -252,12 +268,12 @@ class Cfg2Api(Cfg2):
     name = "cfg2-api"
     scaling = "weak"
 
-    def __init__(self, a, rank, world, ctx):
+    def __init__(self, a, rank, world, ctx, pre=None):
         import ctypes
         from waffle_con_amd import _lib
         from waffle_con_amd.consensus import _problems
         a.loci = a.loci or 1024
-        super().__init__(a, rank, world, ctx)
+        super().__init__(a, rank, world, ctx, pre)
         self.threads = a.api_threads
         path = os.path.join(ROOT, "tools", "libapibench.so")
         if not os.path.exists(path):
@@ -351,9 +367,9 @@ class Cfg2Latency(Cfg2):
     name = "cfg2-latency"
     scaling = "weak"
 
-    def __init__(self, a, rank, world, ctx):
+    def __init__(self, a, rank, world, ctx, pre=None):
         a.loci = 1
-        super().__init__(a, rank, world, ctx)
+        super().__init__(a, rank, world, ctx, pre)
 
     def config(self):
         c = super().config()
@@ -375,7 +391,7 @@ class Cfg3(Cfg2):
     name = "cfg3"
     kernel = "wc::dual_engine_kernel"
 
-    def __init__(self, a, rank, world, ctx):
+    def __init__(self, a, rank, world, ctx, pre=None):
         import waffle_con_amd as w
         from waffle_con_amd import synth
         from waffle_con_amd.cdwfa_config import CdwfaConfig
@@ -432,45 +448,92 @@ class Cfg3(Cfg2):
 
 
 class Cfg5:
-    """PriorityConsensusDWFA over a fixed batch of cfg5 loci, strong-scaled."""
+    """PriorityConsensusDWFA over a fixed batch of cfg5 loci, strong-scaled:
+    the heavy prefix of the cost-sorted order (75% of the estimated cost) is
+    split statically by LPT, the light tail is pulled in chunks through a
+    store-backed shared queue by whichever rank runs out of work first
+    (shard.prefix_tail_plan / SharedQueue; no collective on the data path)."""
     name = "cfg5"
     scaling = "strong"
     kernel = "wcn::dual_engine_kernel"
 
-    def __init__(self, a, rank, world, ctx):
+    @staticmethod
+    def pregen(a, rank, world, total=None):
+        """Plan and loci of this rank (its static prefix and every tail locus it
+        may pull), generated before the GPU is touched (forked workers)."""
         from waffle_con_amd import shard, synth
+        total = total or a.loci or 10000
+        t0 = time.perf_counter()
+        costs = [synth.cfg5_cost(s) for s in range(total)]
+        # one GPU runs everything in one call (the scheduler publishes largest
+        # first); several split the heavy 85% of the cost statically and share
+        # the light tail
+        static, tail = shard.prefix_tail_plan(costs, world, 1.0 if world == 1 else 0.85)
+        ids = static[rank] + tail
+        loci = dict(zip(ids, pool_map(synth.cfg5_locus, ids)))
+        return {"total": total, "static": static[rank], "tail": tail, "loci": loci, "costs": costs,
+                "gen_s": time.perf_counter() - t0}
+
+    def __init__(self, a, rank, world, ctx, pre=None):
+        from waffle_con_amd import shard
         from waffle_con_amd.cdwfa_config import CdwfaConfig
         self.a, self.ctx, self.rank, self.world = a, ctx, rank, world
-        self.total = a.loci or 10000
+        pre = pre or self.pregen(a, rank, world)
+        self.total = pre["total"]
+        self.static, self.tail, self.L = pre["static"], pre["tail"], pre["loci"]
+        # tail chunks large enough to fill the GPU, about four per rank
+        self.chunk = max(256, -(-len(self.tail) // (4 * world)))
+        self.costs = pre["costs"]
         self.cfg = CdwfaConfig(wildcard=ord("*"))
-        t0 = time.perf_counter()
-        # every rank computes the same cost-sorted assignment from the loci's
-        # parameters (no generation, no communication) and generates its own loci
-        costs = [synth.cfg5_cost(s) for s in range(self.total)]
-        self.assign = shard.cost_sorted_assignment(costs, world)
-        self.mine = self.assign[rank]
-        with ThreadPoolExecutor(max_workers=_threads()) as ex:
-            self.loci = list(ex.map(synth.cfg5_locus, self.mine))
-        self.gen_s = time.perf_counter() - t0
+        self.gen_s = pre["gen_s"]
         self.upload_s = 0.0
-        self.n = len(self.loci)
+        self.n = self.total
+        self.k = 0
+        if world > 1:
+            import torch.distributed as dist
+            self.store = dist.distributed_c10d._get_default_store()
+        else:
+            self.store = shard.LocalStore()
+        self.last, self.mine, self.busy_s, self.static_s = {}, [], 0.0, 0.0
 
-    def step(self):
+    def _run(self, ids):
         import waffle_con_amd as w
-        probs = [(c, None, None) for c in self.loci]
-        res, st = w.priority_consensus_batch(probs, self.cfg, context=self.ctx, return_errors=True)
+        res, st = w.priority_consensus_batch([(self.L[i], None, None) for i in ids], self.cfg, context=self.ctx,
+                                             return_errors=True)
         bad = [r for r in res if isinstance(r, Exception)]
         if bad:
             raise RuntimeError("engine error: %s" % bad[0])
-        self.last = res
-        return st, len(res)
+        self.last.update(zip(ids, res))
+        return st
+
+    def step(self):
+        from waffle_con_amd import shard
+        self.k += 1
+        q = shard.SharedQueue(self.store, len(self.tail), self.chunk, key="wc_cfg5_%d" % self.k)
+        self.last, self.mine = {}, list(self.static)
+        t0 = time.perf_counter()
+        tot = self._run(self.static)
+        self.static_s = time.perf_counter() - t0
+        keys = ("kernel_ms", "updates", "w_out", "compares", "launches")
+        while True:
+            c = q.next_chunk()
+            if c is None:
+                break
+            ids = self.tail[c[0]:c[1]]
+            st = self._run(ids)
+            for k in keys:
+                tot[k] += st[k]
+            self.mine += ids
+        self.busy_s = time.perf_counter() - t0
+        return tot, len(self.mine)
 
     def config(self):
         return {"workload": "PriorityConsensusDWFA cfg5: fixed batch of %d PGx loci (1-6 kb, 2 haplotypes, 15-40 reads "
-                            "each @ 0.5%%, [HPC(read), read] chains, wildcard '*'), cost-sorted queue over %d GPU(s)"
-                            % (self.total, self.world),
-                "loci_total": self.total, "loci_this_rank": self.n,
-                "parallelism": "loci-sharded x%d, cost-sorted LPT assignment (no collective)" % self.world}
+                            "each @ 0.5%%, [HPC(read), read] chains, wildcard '*'), LPT prefix + shared-queue tail "
+                            "over %d GPU(s)" % (self.total, self.world),
+                "loci_total": self.total, "loci_this_rank": len(self.mine),
+                "parallelism": "loci-sharded x%d, cost-sorted LPT prefix + store-backed shared queue (no collective)"
+                               % self.world}
 
     def data(self):
         return "synthetic: synth.cfg5_locus(seed) seeds 0..%d" % (self.total - 1)
@@ -478,17 +541,36 @@ class Cfg5:
     def e2e(self, steps):
         return None
 
+    def rank_report(self, dist, device):
+        """Per-rank busy time, static-prefix time and loci of the last step (every rank calls this)."""
+        vals = [self.busy_s, self.static_s, float(len(self.mine)), float(sum(self.costs[i] for i in self.mine))]
+        if dist is None:
+            rows = [vals]
+        else:
+            import torch
+            t = torch.zeros(self.world, len(vals), dtype=torch.float64, device=device)
+            t[self.rank] = torch.tensor(vals, dtype=torch.float64, device=device)
+            dist.all_reduce(t)
+            rows = t.tolist()
+        busy = [r[0] for r in rows]
+        return {"rank_busy_s": busy, "rank_static_s": [r[1] for r in rows], "rank_loci": [int(r[2]) for r in rows],
+                "rank_cost_share": [r[3] / max(1.0, float(sum(self.costs))) for r in rows],
+                "busy_max_s": max(busy), "busy_min_s": min(busy), "tail_s": max(busy) - min(busy),
+                "prefix_loci": None if dist is not None else len(self.static), "tail_loci": len(self.tail),
+                "chunk": self.chunk}
+
     def cpu(self, threads, target_s):
         o = orc()
-        # the rank's loci are in queue order (heaviest first): estimate the mean
+        mine = self.mine
+        # this rank's loci in queue order (heaviest first): estimate the mean
         # per-locus time from a few loci spread over that order, sample evenly
-        probe = [int(k * len(self.loci) / 4) for k in range(4)]
+        probe = [mine[int(k * len(mine) / 4)] for k in range(4)]
         t0 = time.perf_counter()
-        cpu_pool_run(lambda i: o.priority_consensus(self.loci[i], wildcard=ord("*")), probe, min(4, threads))
+        cpu_pool_run(lambda i: o.priority_consensus(self.L[i], wildcard=ord("*")), probe, min(4, threads))
         one = (time.perf_counter() - t0) * min(4, threads) / len(probe)
-        n = sample_size(one, threads, target_s, len(self.loci))
-        idx = [int(k * len(self.loci) / n) for k in range(n)]
-        dt, outs = cpu_pool_run(lambda i: o.priority_consensus(self.loci[i], counters=True, wildcard=ord("*")), idx,
+        n = sample_size(one, threads, target_s, len(mine))
+        idx = [mine[int(k * len(mine) / n)] for k in range(n)]
+        dt, outs = cpu_pool_run(lambda i: o.priority_consensus(self.L[i], counters=True, wildcard=ord("*")), idx,
                                 threads)
         upd = sum(c["updates"] for _, c in outs)
         ok = all([[c.sequence() for c in ch] for ch in self.last[i].consensuses()] ==
@@ -505,16 +587,29 @@ class Cfg4(Cfg5):
     name = "cfg4"
     scaling = "weak"
 
-    def __init__(self, a, rank, world, ctx):
+    @staticmethod
+    def pregen(a, rank, world, total=None):
+        return None
+
+    def __init__(self, a, rank, world, ctx, pre=None):
         from waffle_con_amd import synth
         from waffle_con_amd.cdwfa_config import CdwfaConfig
         self.a, self.ctx, self.rank, self.world = a, ctx, rank, world
         self.total = self.n = 1
         self.cfg = CdwfaConfig(wildcard=ord("*"))
         t0 = time.perf_counter()
-        self.loci = [[[r] for r in synth.cfg4_locus(4 + rank)]]
+        self.L = {0: [[r] for r in synth.cfg4_locus(4 + rank)]}
+        self.static, self.tail, self.costs = [0], [], [1]
         self.gen_s = time.perf_counter() - t0
         self.upload_s = 0.0
+        self.last, self.mine, self.busy_s, self.static_s = {}, [], 0.0, 0.0
+
+    def step(self):
+        self.last, self.mine = {}, [0]
+        t0 = time.perf_counter()
+        st = self._run([0])
+        self.busy_s = self.static_s = time.perf_counter() - t0
+        return st, 1
 
     def config(self):
         return {"workload": "PriorityConsensusDWFA cfg4: one locus, 4 haplotypes x 50 reads x 8 kb, inserted "
@@ -557,6 +652,10 @@ def main():
     if a.gpus != world:
         print("bench.py: --gpus %d but WORLD_SIZE %d" % (a.gpus, world), file=sys.stderr)
         sys.exit(2)
+    # large inputs are generated by forked workers before anything touches the GPU
+    cls = WORKLOADS[a.workload]
+    pre = cls.pregen(a, rank, world) if hasattr(cls, "pregen") else None
+    leg_pre = Cfg5.pregen(a, rank, world, total=a.cfg5_loci) if (a.workload == "cfg2" and a.cfg5_loci) else None
     # torch ships its own HIP runtime next to the one the library links: torch
     # must initialise the device first, or its later init finds no GPU
     import torch
@@ -576,7 +675,7 @@ def main():
         print("[bench rank %d] %s" % (rank, msg), file=sys.stderr, flush=True)
 
     note("generating %s" % a.workload)
-    W = WORKLOADS[a.workload](a, rank, world, ctx)
+    W = cls(a, rank, world, ctx, pre)
     note("generated in %.1f s; warmup" % W.gen_s)
 
     def sync():
@@ -609,6 +708,25 @@ def main():
     e2e = None
     if world == 1 and not a.no_e2e:
         e2e = W.e2e(max(3, a.steps))
+    # cfg5 strong-scaling leg of the default line (the fixed
+    # 10,000-locus PriorityConsensusDWFA batch the 8-GPU target is quoted on):
+    # one pass, barrier + device sync on both sides, max over ranks
+    cfg5_leg = None
+    if leg_pre is not None:
+        note("cfg5 strong-scaling leg: %d loci" % a.cfg5_loci)
+        C5 = Cfg5(a, rank, world, ctx, leg_pre)
+        with shard.Timer(dist, sync) as tm5:
+            st5, n5 = C5.step()
+        el5, upd5, loci5 = shard.reduce_run(dist, tm5.elapsed, st5["updates"], n5,
+                                            device="cuda" if dist is not None else None)
+        rep = C5.rank_report(dist, "cuda" if dist is not None else None)
+        cfg5_leg = {"workload": C5.config()["workload"], "loci": int(loci5), "elapsed_s": el5,
+                    "cfg5_loci_per_s": loci5 / el5, "cfg5_updates_per_s": upd5 / el5, "gen_s": C5.gen_s,
+                    "scaling": "strong", "n_gpus": world}
+        cfg5_leg.update(rep)
+        note("cfg5 leg done: %.2f s" % el5)
+
+    w_ranks = W.rank_report(dist, "cuda" if dist is not None else None) if hasattr(W, "rank_report") else None
 
     if rank != 0:
         if dist is not None:
@@ -663,6 +781,10 @@ def main():
     if hasattr(W, "extra"):
         note("extra legs")
         line.update(W.extra())
+    if cfg5_leg:
+        line["cfg5_strong"] = cfg5_leg
+    if w_ranks:
+        line["ranks"] = w_ranks
     if e2e:
         line["e2e_loci_per_s"], line["e2e_upload_ms"], line["e2e_compute_ms"] = e2e
         line["e2e_note"] = ("fresh batch every step: Python marshalling + pinned staging + H2D of the reads, "

@@ -139,3 +139,59 @@ def test_gloo_world2_cost_sorted_queue():
     dyn = [o[2] for o in out]
     assert sorted(static[0] + static[1]) == list(range(n)) and not set(static[0]) & set(static[1])
     assert sorted(dyn[0] + dyn[1]) == list(range(n)) and not set(dyn[0]) & set(dyn[1])
+
+
+def _bench_cfg5_worker(rank, world, port, total, q):
+    """bench.py's cfg5 code path (Cfg5.pregen, Cfg5.step, Cfg5.rank_report) at
+    world size 2 over gloo, with the engine call replaced by a recorder."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        import types
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        a = types.SimpleNamespace(loci=total)
+        pre = bench.Cfg5.pregen(a, rank, world)
+        C = bench.Cfg5(a, rank, world, None, pre)
+        C.chunk = 7  # many pulls
+        ran = []
+
+        def fake_run(ids):
+            ran.extend(ids)
+            C.last.update((i, None) for i in ids)
+            return {"kernel_ms": 0.0, "updates": len(ids), "w_out": 0, "compares": 0, "launches": 1}
+
+        C._run = fake_run
+        st, n = C.step()
+        rep = C.rank_report(dist, None)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ran)
+        q.put((rank, sorted(pre["loci"]), list(C.static), list(C.tail), gathered, st["updates"], n, rep))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_cfg5_partition():
+    """Done-when of the strong-scaling leg: the loci bench.py's cfg5 leg runs
+    over 2 ranks (LPT prefix + shared-queue tail) are a disjoint, complete
+    partition of the batch, and every rank generated what it ran."""
+    world, total = 2, 120
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_cfg5_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ran = out[0][4]
+    assert not set(ran[0]) & set(ran[1])
+    assert sorted(ran[0] + ran[1]) == list(range(total))
+    for rank, generated, static, tail, _, upd, n, rep in out:
+        assert set(ran[rank]) <= set(generated) and set(static) <= set(ran[rank])
+        assert upd == n == len(ran[rank])
+        assert rep["rank_loci"] == [len(ran[0]), len(ran[1])]
+    assert out[0][3] == out[1][3]  # both ranks see the same tail order

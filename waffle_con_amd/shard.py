@@ -46,6 +46,35 @@ def cost_sorted_assignment(costs, world):
     return out
 
 
+def prefix_tail_plan(costs, world, prefix_frac=0.75):
+    """Strong scaling of a fixed item list: the cost-sorted order (longest
+    first) is cut into a heavy prefix holding `prefix_frac` of the total cost,
+    assigned statically by LPT (cost_sorted_assignment; every rank computes the
+    same split), and the light tail, which ranks pull in chunks through a
+    SharedQueue as they run out of work. Returns (per-rank prefix item lists in
+    queue order, the tail item list in queue order)."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    target = prefix_frac * sum(costs)
+    k, cum = 0, 0
+    while k < len(order) and (cum < target or k < world):
+        cum += costs[order[k]]
+        k += 1
+    prefix, tail = order[:k], order[k:]
+    static = cost_sorted_assignment([costs[i] for i in prefix], world)
+    return [[prefix[j] for j in part] for part in static], tail
+
+
+class LocalStore:
+    """In-process stand-in for the process group's store (world size 1)."""
+
+    def __init__(self):
+        self.v = {}
+
+    def add(self, key, n):
+        self.v[key] = self.v.get(key, 0) + n
+        return self.v[key]
+
+
 class SharedQueue:
     """Dynamic form of the cost-sorted queue: ranks pull chunks of a fixed,
     cost-sorted item order through an atomic counter in the process group's
