@@ -209,6 +209,8 @@ typedef struct wc_stats {
   uint64_t nodes_explored;
   uint64_t nodes_ignored;
   uint64_t peak_queue_size; /* max over problems */
+  uint64_t row_bytes;       /* wavefront-row bytes read + written by updates (finalizes: read) that grow an
+                             * edit distance: the rows' share of the roofline model */
   uint64_t launches;        /* engine kernel launches (incl. capacity retries) */
   double kernel_ms;         /* device time of the engine launches (HIP events) */
   double wall_ms;           /* host wall time of the whole call */

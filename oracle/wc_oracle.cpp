@@ -71,6 +71,7 @@ size_t Dwfa::max_other() const { return offset + *std::max_element(wf.begin(), w
 // dynamic_wfa.rs:75-99
 size_t Dwfa::update(Seq b, Seq o, Counters* c) {
   extend(b, o, c);
+  const size_t w_in = wf.size();
   size_t mo = max_other();
   while (mo < o.n && !(early && reached_end(b))) {
     increase(b, o, c);
@@ -81,6 +82,9 @@ size_t Dwfa::update(Seq b, Seq o, Counters* c) {
   if (c) {
     c->updates++;
     c->w_out += wf.size();
+    // a grown wavefront is read and written whole (u32 entries): the row
+    // traffic of the roofline model
+    if (wf.size() != w_in) c->row_bytes += 4 * (w_in + wf.size());
   }
   return e;
 }
@@ -88,7 +92,9 @@ size_t Dwfa::update(Seq b, Seq o, Counters* c) {
 // dynamic_wfa.rs:201-210 (never sets is_finalized)
 void Dwfa::finalize(Seq b, Seq o, Counters* c) {
   if (c) c->finalizes++;
+  const size_t w_in = wf.size();
   while (max_baseline() < b.n) increase(b, o, c);
+  if (c && wf.size() != w_in) c->row_bytes += 4 * w_in;  // read once, grown on a copy
 }
 
 // dynamic_wfa.rs:241-255 — tips are diagonals at the consensus end; insertion

@@ -60,6 +60,7 @@ struct Counters {
   uint64_t nodes_ignored = 0;
   uint64_t peak_queue_size = 0;
   uint64_t pops = 0;
+  uint64_t row_bytes = 0;      // wavefront bytes read + written by updates/finalizes that grow e
 };
 
 struct Seq {

@@ -32,7 +32,8 @@ struct orc_config {
 };
 
 struct orc_counters {
-  uint64_t updates, w_out, compares, ed_increases, finalizes, nodes_explored, nodes_ignored, peak_queue_size, pops;
+  uint64_t updates, w_out, compares, ed_increases, finalizes, nodes_explored, nodes_ignored, peak_queue_size, pops,
+      row_bytes;
 };
 
 void orc_free(char* p) { free(p); }
@@ -109,6 +110,7 @@ void copy_counters(const Counters& c, orc_counters* o) {
   o->nodes_ignored = c.nodes_ignored;
   o->peak_queue_size = c.peak_queue_size;
   o->pops = c.pops;
+  o->row_bytes = c.row_bytes;
 }
 
 std::vector<Seq> to_seqs(uint32_t n, const uint8_t* const* seqs, const uint64_t* lens) {

@@ -37,7 +37,7 @@ class OrcConfig(ctypes.Structure):
 class OrcCounters(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "updates", "w_out", "compares", "ed_increases", "finalizes",
-        "nodes_explored", "nodes_ignored", "peak_queue_size", "pops")]
+        "nodes_explored", "nodes_ignored", "peak_queue_size", "pops", "row_bytes")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

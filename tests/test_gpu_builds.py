@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 hip = pytest.importorskip("hip_runner")
 
 KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored", "nodes_ignored",
-        "peak_queue_size")
+        "peak_queue_size", "row_bytes")
 BUILDS = {"wide": {"WC_NARROW": "0", "WC_LOWLAT": "0"}, "lowlat": {"WC_NARROW": "0"},
           "narrow-single": {"WC_NARROW": "1"}, "narrow-dual": {"WC_NARROW": "2"}, "narrow": {"WC_NARROW": "3"},
           "gstate": {"WC_GSTATE": "1"}}

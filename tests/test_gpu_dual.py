@@ -35,7 +35,7 @@ def test_dual_vs_oracle_full_equality(name):
     got, gc = hip.dual_consensus(seqs, offsets=offs, counters=True, **case["cfg"])
     assert got == exp
     for k in ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
-              "nodes_ignored", "peak_queue_size"):
+              "nodes_ignored", "peak_queue_size", "row_bytes"):
         assert gc[k] == ec[k], (k, gc[k], ec[k])
 
 

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 hip = pytest.importorskip("hip_runner")
 
 COUNTER_KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
-                "nodes_ignored", "peak_queue_size")
+                "nodes_ignored", "peak_queue_size", "row_bytes")
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 

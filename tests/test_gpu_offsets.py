@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 hip = pytest.importorskip("hip_runner")
 
 COUNTER_KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
-                "nodes_ignored", "peak_queue_size")
+                "nodes_ignored", "peak_queue_size", "row_bytes")
 
 
 def _truncated(L, N, err, seed, frac=0.5, jitter=3, min_cut=8):

@@ -15,7 +15,7 @@ def test_reference_single(name):
 
 
 COUNTER_KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
-                "nodes_ignored", "peak_queue_size")
+                "nodes_ignored", "peak_queue_size", "row_bytes")
 
 
 def _gen(L, N, err, seed):

@@ -91,7 +91,7 @@ def _chains(seed, n_hap=2, per=4, L=120, err=0.01):
 
 
 COUNTER_KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
-                "nodes_ignored", "peak_queue_size")
+                "nodes_ignored", "peak_queue_size", "row_bytes")
 
 
 def _cmp_priority(hip, chains, offsets=None, seed_groups=None, **cfg):

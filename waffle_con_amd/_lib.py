@@ -90,7 +90,7 @@ class WcDualView(ctypes.Structure):
 class WcStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
-        "nodes_ignored", "peak_queue_size", "launches")] + [("kernel_ms", ctypes.c_double),
+        "nodes_ignored", "peak_queue_size", "row_bytes", "launches")] + [("kernel_ms", ctypes.c_double),
                                                             ("wall_ms", ctypes.c_double)]
 
     def as_dict(self):

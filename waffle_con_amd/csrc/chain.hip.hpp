@@ -329,7 +329,7 @@ static_assert(kF == 8, "vote_unit covers split <= 8");
 __device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
                                              const Gm<uint8_t>* con, uint32_t olen, uint32_t sym, int wc, bool early,
                                              uint32_t wcap, Lo<uint64_t>* tot, Gm<uint32_t>* bak) {
-  WaveCounters cnt = {0, 0, 0, 0, 0};
+  WaveCounters cnt = {0, 0, 0, 0, 0, 0};
   uint32_t e_out = 0;
   const bool ok = wave_heavy(tmp, wf, rd, blen, con, olen, (uint8_t)sym, wc, early, wcap, cnt, e_out, bak);
   if (lane_id() == 0) {
@@ -337,6 +337,7 @@ __device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, 
     atomicAdd((unsigned long long*)&tot[1], (unsigned long long)cnt.w_out);
     atomicAdd((unsigned long long*)&tot[2], (unsigned long long)cnt.compares);
     atomicAdd((unsigned long long*)&tot[3], (unsigned long long)cnt.edinc);
+    atomicAdd((unsigned long long*)&tot[4], (unsigned long long)cnt.rowb);
   }
   return ok ? e_out : kInactive;
 }
@@ -753,7 +754,7 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
       ctl.chain_novf = 0;
       ctl.chain_nochain = 0;
       ctl.chain_nbak = 0;
-      for (int k = 0; k < 4; ++k) ctl.chain_tot[k] = 0;
+      for (int k = 0; k < 5; ++k) ctl.chain_tot[k] = 0;
       E.L.cpred[1] = (uint8_t)s1;
     }
   }
@@ -787,8 +788,9 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
         ctl.cnt[S_WOUT] += ctl.chain_tot[1];
         ctl.cnt[S_COMPARES] += ctl.chain_tot[2];
         ctl.cnt[S_EDINC] += ctl.chain_tot[3];
+        ctl.cnt[S_ROWB] += ctl.chain_tot[4];
       }
-      for (int k = 0; k < 4; ++k) ctl.chain_tot[k] = 0;
+      for (int k = 0; k < 5; ++k) ctl.chain_tot[k] = 0;
     }
   }
   __syncthreads();
@@ -845,6 +847,7 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
       ctl.cnt[S_WOUT] += ctl.chain_tot[1];
       ctl.cnt[S_COMPARES] += ctl.chain_tot[2];
       ctl.cnt[S_EDINC] += ctl.chain_tot[3];
+      ctl.cnt[S_ROWB] += ctl.chain_tot[4];
     }
 #ifdef WC_PHASE_PROF
     ctl.ph[15] += 1ull + ((jstar == K && Keff == K) ? (1ull << 20) : 0ull) + ((uint64_t)jstar << 40);

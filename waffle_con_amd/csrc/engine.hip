@@ -42,6 +42,10 @@ namespace WC_ENGINE_NS {
 #ifndef WC_WAVES_PER_EU
 #define WC_WAVES_PER_EU 4
 #endif
+// the single engine's register budget (default: WC_WAVES_PER_EU)
+#ifndef WC_SINGLE_WAVES_PER_EU
+#define WC_SINGLE_WAVES_PER_EU WC_WAVES_PER_EU
+#endif
 // The 256-thread dual engine (problems of more than 128 reads) at 3 waves per
 // SIMD: 168 VGPRs (40 spilled instead of 62 at 128), 3 workgroups per CU;
 // cfg3 (768 loci of 200 reads) +9%, cfg4 +1% (tools/gpu_r02_dw.sh)
@@ -61,6 +65,16 @@ constexpr uint32_t WC_E_LIMIT_CODE = 11;
 // WC_E_LIMIT with the overflow reasons (engine_shared LIM_*) in bits 16+
 __device__ inline uint32_t limit_status(uint32_t why) { return WC_E_LIMIT_CODE | (why << 16); }
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+// Cache of hashbrown iteration orders (votes): insertion-ordered keys (lo, hi |
+// nk << 56) -> order. Consecutive pops of a dual search rotate among a few
+// lineages whose votes see a few distinct key sequences; 16 entries per side
+// keep almost all of them (one LDS round trip instead of the table rebuild).
+constexpr int kFxCache = 16;
+struct FxCache {
+  uint64_t k0[kFxCache], k1[kFxCache], ord[kFxCache];
+  uint32_t next;
+};
 
 struct Ctl {
   uint32_t prob;
@@ -91,11 +105,11 @@ struct Ctl {
   uint32_t hot_prev, hot_load;
   // linear-chain run-ahead (run_chain)
   uint32_t chain_k, chain_slot, chain_stop, chain_novf, chain_nochain, chain_len, chain_nbak;
-  uint64_t chain_tot[4];  // updates, w_out, compares, ed increases of one chain pass
+  uint64_t chain_tot[5];  // updates, w_out, compares, ed increases, row bytes of one chain pass
   uint32_t nkeys[2];
   uint8_t keys[2][kKout];
   double vals[2][kKout];
-  uint64_t fxc[2][3];  // per side: the last votes' insertion-ordered keys (lo, hi | nk << 56) and their fx order
+  FxCache fxc[2];  // per side
   // thread-0 scratch for child enumeration (kept in LDS, not private memory)
   int16_t opt[2][kKout + 1];
   double srt_v[kKout];
@@ -377,6 +391,7 @@ __device__ inline void flush_counters(Lo<Ctl>& ctl, const WaveCounters& wc) {
     if (wc.compares) atomicAdd((unsigned long long*)&ctl.cnt[S_COMPARES], (unsigned long long)wc.compares);
     if (wc.edinc) atomicAdd((unsigned long long*)&ctl.cnt[S_EDINC], (unsigned long long)wc.edinc);
     if (wc.finalizes) atomicAdd((unsigned long long*)&ctl.cnt[S_FINALIZES], (unsigned long long)wc.finalizes);
+    if (wc.rowb) atomicAdd((unsigned long long*)&ctl.cnt[S_ROWB], (unsigned long long)wc.rowb);
   }
 }
 // per-thread counters (every lane its own): wave-reduce, then lane 0 adds
@@ -595,7 +610,10 @@ __device__ inline void init_problem(Eng& E, Lo<Ctl>& ctl) {
     ctl.cache_slot = kNoSlot;
     ctl.hot_slot = kNoSlot;
     ctl.hot_load = 0;
-    ctl.fxc[0][1] = ctl.fxc[1][1] = ~0ull;  // no cached fx order (nk <= 14)
+    for (int sd = 0; sd < 2; ++sd) {  // no cached fx orders (nk <= 14, so k1 = ~0 never matches)
+      for (int k = 0; k < kFxCache; ++k) ctl.fxc[sd].k1[k] = ~0ull;
+      ctl.fxc[sd].next = 0;
+    }
     for (int s = 0; s < S_NSTAT; ++s) ctl.cnt[s] = 0;
 #ifdef WC_PHASE_PROF
     for (int k = 0; k < kPhases; ++k) ctl.ph[k] = 0;
@@ -749,7 +767,7 @@ WC_SINGLE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1
   const bool early = cfg.early != 0;
   if (tid == 0) ctl.nheavy = 0;
   __syncthreads();
-  WaveCounters tc = {0, 0, 0, 0, 0};
+  WaveCounters tc = {0, 0, 0, 0, 0, 0};
   uint64_t cost = 0;
   uint32_t ends = 0, multi = 0;
   // work items over the pushed sides only: (side, read) with side >= first
@@ -816,7 +834,7 @@ WC_SINGLE_FN void push_sides(Eng& E, Lo<Ctl>& ctl, uint32_t slot, int s0, int s1
   __syncthreads();
   PH_MARK(5);
   const uint32_t nh = uni(ctl.nheavy);
-  WaveCounters cnt = {0, 0, 0, 0, 0};
+  WaveCounters cnt = {0, 0, 0, 0, 0, 0};
   for (uint32_t k = wave_id(); k < nh; k += kEW) {
     const uint32_t it = E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))];
     const uint32_t side = it >= E.n ? 1u : 0u, r = it - side * E.n;
@@ -919,7 +937,7 @@ WC_PHASE_FN void activate_side(Eng& E, Lo<Ctl>& ctl, uint32_t slot, uint32_t sid
   const uint32_t nh = uni(ctl.nheavy);
   SideView v = E.sv(slot, side);
   const auto dst = node_rs<kHot>(E, slot, side);
-  WaveCounters cnt = {0, 0, 0, 0, 0};
+  WaveCounters cnt = {0, 0, 0, 0, 0, 0};
   for (uint32_t k = wave_id(); k < nh; k += kEW) {
     const uint32_t r = E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))];
     if (uni(dst[r].e) != kInactive) {
@@ -1042,7 +1060,7 @@ struct SymSet {
 template <class Load, class Weight>
 __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, bool weighted, bool multi, int wc,
                                        uint32_t& m_out, uint32_t& key_out, double& val_out,
-                                       Lo<uint64_t>* ph = nullptr, Lo<uint64_t>* fxc = nullptr) {
+                                       Lo<uint64_t>* ph = nullptr, Lo<FxCache>* fxc = nullptr) {
   const int lane = lane_id();
 #ifdef WC_PHASE_PROF
   uint64_t vt = __builtin_amdgcn_s_memtime();
@@ -1095,16 +1113,21 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
   // 2. hashbrown iteration order, wildcard removed (consensus.rs:556-561);
   // consecutive pops mostly see the same keys in the same insertion order,
   // so the last order is kept (fxc) and reused on a match
-  uint64_t ord;
+  uint64_t ord = 0;
   const uint64_t tag = ins_hi | ((uint64_t)nk << 56);
-  if (fxc && fxc[0] == ins_lo && fxc[1] == tag) {
-    ord = fxc[2];
-  } else {
+  uint64_t hit = 0;
+  if (fxc) {  // lanes 0..15 probe one entry each
+    const uint32_t e = (uint32_t)lane & (kFxCache - 1);
+    hit = ballot(lane < kFxCache && fxc->k0[e] == ins_lo && fxc->k1[e] == tag);
+    if (hit) ord = fxc->ord[__builtin_ctzll(hit)];
+  }
+  if (!hit) {
     ord = fx_order_packed(nk, ins_at);
     if (fxc && lane == 0) {
-      fxc[0] = ins_lo;
-      fxc[1] = tag;
-      fxc[2] = ord;
+      const uint32_t e = fxc->next++ & (kFxCache - 1);
+      fxc->k0[e] = ins_lo;
+      fxc->k1[e] = tag;
+      fxc->ord[e] = ord;
     }
   }
   uint64_t k_lo = 0, k_hi = 0;
@@ -1230,7 +1253,7 @@ WC_PHASE_FN bool wave_votes(Lo<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, co
 #else
                                   nullptr,
 #endif
-                                  ctl.fxc[side]);
+                                  &ctl.fxc[side]);
   if (!ok) return false;
   if ((uint32_t)lane < m) {
     ctl.keys[side][lane] = (uint8_t)key;
@@ -1376,7 +1399,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     // kRow16, four reads per wave) or, for wide frontiers and long rows, to
     // the wave list (filled from the top of E.L.list)
     const uint32_t lend = (uint32_t)list_entries(2, E.nmax) - 1;
-    WaveCounters tc = {0, 0, 0, 0, 0};
+    WaveCounters tc = {0, 0, 0, 0, 0, 0};
     for (uint32_t q = 0; q < 2 * cn; ++q) {
       const uint32_t c = c0 + q / 2, sd = q & 1u;
       const int sym = uni((int32_t)ctl.ch_s[c][sd]);
@@ -1423,8 +1446,8 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     SUB_CNT(16, nh);
     SUB_CNT(17, nw);
     SUB_T0(tg);
-    WaveCounters cnt = {0, 0, 0, 0, 0};
-    GroupCnt gc = {0, 0, 0, 0};
+    WaveCounters cnt = {0, 0, 0, 0, 0, 0};
+    GroupCnt gc = {0, 0, 0, 0, 0};
     // (up to one item per wave the 64-lane path is quicker: it goes to the wave loop)
     const uint32_t ng = nh > (uint32_t)kEW ? nh : 0u;
     for (uint32_t b0 = wave_id() * 4u; b0 < ng; b0 += kEW * 4u) {
@@ -1442,6 +1465,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       gc.updates += go.updates;
       gc.w_out += go.w_out;
       gc.cmp += go.cmp;
+      gc.rowb += go.rowb;
       if (act && (lane & 15) == 0 && g == kG_WCAP) atomicOr(&ctl.ovf, 4u);
       // ... a row that outgrew the group finishes with the whole wave
       uint64_t mem = ballot(act && (lane & 15) == 0 && g == kG_MEM);
@@ -1468,6 +1492,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     cnt.updates += wave_sum_u32(gc.updates);
     cnt.w_out += wave_sum_u32(gc.w_out);
     cnt.compares += wave_sum_u32(gc.cmp);
+    cnt.rowb += wave_sum_u32(gc.rowb);
     // ... and wide frontiers / long rows (and a few group items) one read per wave
     const uint32_t nsolo = nw + (nh - ng);
     for (uint32_t k = wave_id(); k < nsolo; k += kEW) {
@@ -1574,7 +1599,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
 
 // single-engine phases out of line (see WC_SINGLE_FN)
 WC_SINGLE_FN WaveCounters single_finalize(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t len) {
-  WaveCounters cnt = {0, 0, 0, 0, 0};
+  WaveCounters cnt = {0, 0, 0, 0, 0, 0};
   finalize_side<true>(E, ctl, top, 0, len, E.L.fe, cnt);
   return cnt;
 }
@@ -1592,7 +1617,7 @@ WC_SINGLE_FN void single_activate(Eng& E, Lo<Ctl>& ctl, uint32_t slot, bool hot,
 // =====================================================================
 // ConsensusDWFA engine (consensus.rs:139-351)
 // =====================================================================
-__global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_WAVES_PER_EU))) single_engine_kernel(EngineArgs A) {
+__global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SINGLE_WAVES_PER_EU))) single_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
   Lo<Ctl>& ctl = *(Lo<Ctl>*)&ctl_lds;
@@ -1954,7 +1979,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
 
       // ---- finalize a clone (dual_consensus.rs:438-492) ----
       if (uni(ctl.reached)) {
-        WaveCounters cnt = {0, 0, 0, 0, 0};
+        WaveCounters cnt = {0, 0, 0, 0, 0, 0};
         finalize_side<false>(E, ctl, top, 0, tlens[0], E.L.fe, cnt);
         if (tdual) finalize_side<false>(E, ctl, top, 1, tlens[1], E.L.fe + E.nmax, cnt);
         flush_counters(ctl, cnt);
@@ -2165,7 +2190,7 @@ __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
   const Gm<uint8_t>* base = (const Gm<uint8_t>*)j.baseline;
   const Gm<uint8_t>* other = (const Gm<uint8_t>*)j.other;
   uint32_t e = j.e;
-  WaveCounters cnt = {0, 0, 0, 0, 0};
+  WaveCounters cnt = {0, 0, 0, 0, 0, 0};
   uint32_t status = 0;
   if (j.op == 0) {
     uint32_t mo = 0, mb = 0;

@@ -229,6 +229,7 @@ __device__ __forceinline__ uint32_t rraw_flags(const RRaw& s) { return s.a.w >> 
 
 struct WaveCounters {
   uint32_t updates, w_out, compares, edinc, finalizes;
+  uint32_t rowb;  // wavefront-row bytes read + written by updates (finalizes: read) that grow e
 };
 
 // ---- packed match runs (dynamic_wfa.rs:122-150) ----
@@ -423,6 +424,7 @@ __device__ inline bool wave_push_read(Gm<uint32_t>* wf, uint32_t& e, uint32_t of
   mo = wave_max_u32(mo) + off;
   mb = wave_max_u32(mb);
   uint32_t cmp = c;
+  const uint32_t w_in = W;
   while (mo < olen && !(early && mb == blen)) {
     if (W + 2 > wcap) return false;
     wave_grow(wf, W);
@@ -435,6 +437,7 @@ __device__ inline bool wave_push_read(Gm<uint32_t>* wf, uint32_t& e, uint32_t of
   }
   cnt.updates++;
   cnt.w_out += W;
+  if (W != w_in) cnt.rowb += 4 * (w_in + W);
   cnt.compares += wave_sum_u32(cmp);
   return true;
 }
@@ -445,6 +448,7 @@ __device__ inline bool wave_update_general(Gm<uint32_t>* wf, uint32_t& e, uint32
                                            uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc, bool early, uint32_t wcap,
                                            WaveCounters& cnt, uint32_t& mo, uint32_t& mb) {
   uint32_t W = 2 * e + 1, cmp = 0;
+  const uint32_t w_in = W;
   wave_extend_all(wf, W, e, off, rd, blen, con, olen, wc, mo, mb, cmp);
   mo += off;
   while (mo < olen && !(early && mb == blen)) {
@@ -458,6 +462,7 @@ __device__ inline bool wave_update_general(Gm<uint32_t>* wf, uint32_t& e, uint32
   }
   cnt.updates++;
   cnt.w_out += W;
+  if (W != w_in) cnt.rowb += 4 * (w_in + W);
   cnt.compares += wave_sum_u32(cmp);
   return true;
 }
@@ -470,6 +475,7 @@ __device__ inline bool wave_finalize_read(const Gm<uint32_t>* wf, uint32_t e, ui
                                           Gm<uint32_t>* scratch,
                                           uint32_t wcap, uint32_t& e_out, WaveCounters& cnt) {
   uint32_t W = 2 * e + 1;
+  const uint32_t w_in = W;
   uint32_t v[kRegQ];
   regs_load(v, wf, W);
   uint32_t mb = 0;
@@ -508,6 +514,7 @@ __device__ inline bool wave_finalize_read(const Gm<uint32_t>* wf, uint32_t e, ui
     }
     cnt.edinc++;
   }
+  if (W != w_in) cnt.rowb += 4 * w_in;
   cnt.compares += wave_sum_u32(cmp);
   e_out = e;
   return true;
@@ -909,6 +916,7 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
     return true;
   }
   uint32_t W = 2 * e + 1, mo, mb, cmp = 0;
+  const uint32_t w_in = W;
   uint32_t v[kRegQ];
   bool regs = W + 2 <= 64u * kRegQ;
   if (regs) regs_load(v, wf, W);
@@ -935,6 +943,7 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
   } while (mo + off < olen && !(early && mb == blen));
   cnt.updates++;
   cnt.w_out += W;
+  cnt.rowb += 4 * (w_in + W);
   cnt.compares += wave_sum_u32(cmp);
   if (regs) {
     regs_store(v, wf, W);
@@ -965,16 +974,16 @@ __device__ __forceinline__ uint32_t grp_sum(uint32_t v) { return row_sum_u32(v);
 // on in wave_edinc_mem). Counters are per lane (wave-sum them).
 constexpr uint32_t kG_DONE = 0, kG_WCAP = 1, kG_MEM = 2, kG_RUN = 3;
 struct GroupCnt {
-  uint32_t edinc, updates, w_out, cmp;
+  uint32_t edinc, updates, w_out, cmp, rowb;
 };
 // group_edinc's result, by value (registers): outcome, final e, per-lane counters
 struct GroupOut {
-  uint32_t st, e, edinc, updates, w_out, cmp;
+  uint32_t st, e, edinc, updates, w_out, cmp, rowb;
 };
 __device__ __noinline__ GroupOut group_edinc(bool act, Gm<RState>* rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd,
                                              uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc,
                                              bool early, uint32_t wcap) {
-  GroupOut go_ = {kG_DONE, 0, 0, 0, 0, 0};
+  GroupOut go_ = {kG_DONE, 0, 0, 0, 0, 0, 0};
   const int lane = lane_id();
   const uint32_t gl = (uint32_t)lane & 15u, gb = (uint32_t)lane & ~15u;
   uint32_t e = 0, off = 0;
@@ -983,6 +992,7 @@ __device__ __noinline__ GroupOut group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
     off = rsp->off;
   }
   uint32_t W = 2 * e + 1;
+  const uint32_t w_in = W;
   // wave-uniform bound on every group's row length: entry blocks q with
   // 16 q >= wlim are skipped (scalar branches) instead of predicated
 #ifdef WC_NO_WLIM
@@ -1085,6 +1095,9 @@ __device__ __noinline__ GroupOut group_edinc(bool act, Gm<RState>* rsp, Gm<uint3
     const uint32_t j = 16u * q + gl;
     if (16u * q < wlim && j < W) wf[j] = v[q];
   }
+  // row traffic: the load now; the store when the update ends here (a row
+  // that outgrew the group is stored by wave_edinc_mem)
+  go_.rowb = gl == 0 ? 4 * (w_in + (st == kG_MEM ? 0u : W)) : 0u;
   if (st == kG_MEM) return go_;
   go_.updates = gl == 0;
   go_.w_out = gl == 0 ? W : 0u;
@@ -1143,6 +1156,7 @@ __device__ inline bool wave_edinc_mem(P rsp, Gm<uint32_t>* wf, uint32_t e, const
   } while (mo + off < olen && !(early && mb == blen));
   cnt.updates++;
   cnt.w_out += W;
+  cnt.rowb += 4 * W;  // the final store (group_edinc counted the first load)
   cnt.compares += wave_sum_u32(cmp);
   __builtin_amdgcn_wave_barrier();
   wave_rebuild(wf, e, off, blen, olen, rsp);

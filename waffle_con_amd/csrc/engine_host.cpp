@@ -1087,6 +1087,7 @@ void fill_stats(wc_results* R, double kernel_ms, uint64_t launches, double wall_
     R->stats.nodes_explored += p.stats[S_EXPLORED];
     R->stats.nodes_ignored += p.stats[S_IGNORED];
     R->stats.peak_queue_size = std::max(R->stats.peak_queue_size, p.stats[S_PEAKQ]);
+    R->stats.row_bytes += p.stats[S_ROWB];
   }
   R->stats.kernel_ms = kernel_ms;
   R->stats.launches = launches;

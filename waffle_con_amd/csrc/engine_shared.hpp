@@ -38,6 +38,7 @@ enum StatIdx : int {
   S_EXPLORED,
   S_IGNORED,
   S_PEAKQ,
+  S_ROWB,  // wavefront-row bytes of updates/finalizes that grow e (roofline model)
   S_NSTAT
 };
 

@@ -594,6 +594,7 @@ int wc_results_problem_stats(const wc_results* r, uint32_t p, wc_stats* o) {
   o->nodes_explored = s[S_EXPLORED];
   o->nodes_ignored = s[S_IGNORED];
   o->peak_queue_size = s[S_PEAKQ];
+  o->row_bytes = s[S_ROWB];
   return WC_OK;
 }
 
