@@ -136,6 +136,8 @@ typedef struct wc_service_stats {
   uint64_t served;      /* answered by the persistent launches */
   uint64_t fallback;    /* answered by the batch path (offsets, > 256 reads, capacity retries) */
   uint64_t lane_starts; /* persistent launches started */
+  uint64_t retried;     /* of the fallbacks: problems that outgrew the launch's capacities */
+  uint64_t lane_failures; /* launches that could not start (their requests took the batch path) */
 } wc_service_stats;
 int wc_service_create(int device, uint64_t arena_bytes, wc_service** out);
 void wc_service_destroy(wc_service* s);

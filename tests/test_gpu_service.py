@@ -63,7 +63,9 @@ def test_threaded_single_calls_match_oracle():
         assert g == e
         for k in ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored"):
             assert gc[k] == ec[k], k
-    assert s1["served"] - s0["served"] == len(loci)
+    from waffle_con_amd import _lib
+    print("service stats before", s0, "after", s1, "last error", _lib.service().last_error())
+    assert s1["served"] - s0["served"] == len(loci), _lib.service().last_error()
 
 
 def test_threaded_dual_calls_match_oracle():

@@ -160,7 +160,7 @@ def _bench_cfg5_worker(rank, world, port, total, q):
         def fake_run(ids):
             ran.extend(ids)
             C.last.update((i, None) for i in ids)
-            return {"kernel_ms": 0.0, "updates": len(ids), "w_out": 0, "compares": 0, "launches": 1}
+            return {"kernel_ms": 0.0, "updates": len(ids), "w_out": 0, "compares": 0, "launches": 1, "row_bytes": 0}
 
         C._run = fake_run
         st, n = C.step()

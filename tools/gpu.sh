@@ -5,6 +5,7 @@
 #   bash tools/gpu.sh bench  <tag> [bench.py args]    one bench line -> gpurun_out/<tag>/bench.json
 #   bash tools/gpu.sh profile <tag> [bench.py args]   tools/profile_round.sh (kernel trace + PMC passes)
 #   bash tools/gpu.sh smoke  <tag>                    __graft_entry__.smoke()
+#   bash tools/gpu.sh cmd    <tag> <seconds> <cmd...> any command under its own time limit
 # Jobs can be chained: bash tools/gpu.sh tests t1 -- bench t1 --workload cfg5
 # Every GPU step has its own timeout; the first failing step ends the call.
 set -o pipefail
@@ -16,7 +17,7 @@ run_job() {
   mkdir -p $O
   case $job in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread "$@" \
         > $O/pytest_gpu.log 2>&1 || { echo "tests failed"; tail -40 $O/pytest_gpu.log; return 1; }
       tail -2 $O/pytest_gpu.log ;;
     check)
@@ -33,6 +34,11 @@ run_job() {
     profile)
       bash tools/profile_round.sh $tag "$@" > $O/profile.log 2>&1 || { echo "profile failed"; tail -30 $O/profile.log; return 1; }
       tail -3 $O/profile.log ;;
+    cmd)  # cmd <tag> <seconds> <command...>: any program, its own time limit, output in cmd.log
+      local lim=$1
+      shift
+      timeout -k 10 $lim "$@" > $O/cmd.log 2>&1 || { echo "cmd failed: $*"; tail -30 $O/cmd.log; return 1; }
+      tail -5 $O/cmd.log ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
         || { echo "smoke failed"; tail -30 $O/smoke.log; return 1; }

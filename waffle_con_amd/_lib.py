@@ -98,7 +98,8 @@ class WcStats(ctypes.Structure):
 
 
 class WcServiceStats(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_uint64) for n in ("calls", "served", "fallback", "lane_starts")]
+    _fields_ = [(n, ctypes.c_uint64) for n in ("calls", "served", "fallback", "lane_starts", "retried",
+                                               "lane_failures")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -46,19 +46,23 @@ namespace WC_ENGINE_NS {
 #ifndef WC_SINGLE_WAVES_PER_EU
 #define WC_SINGLE_WAVES_PER_EU WC_WAVES_PER_EU
 #endif
-// The 256-thread dual engine (problems of more than 128 reads) at 3 waves per
-// SIMD: 168 VGPRs (40 spilled instead of 62 at 128), 3 workgroups per CU;
-// cfg3 (768 loci of 200 reads) +9%, cfg4 +1% (tools/gpu_r02_dw.sh)
+// The dual engine's register budget. Not 3 waves per SIMD (168 VGPRs): that
+// budget measured cfg3 +9% in round 2, but both 256-thread dual builds
+// compiled for it have faulted on addresses outside every buffer (a pointer
+// with a wrong high dword; WC_FAULT_LOG) on inputs the 2- and 4-wave builds of
+// the same source and the bounds-checked 3-wave build run bit-exact (DESIGN.md
+// "3-wave dual builds")
 #ifndef WC_DUAL_WAVES_PER_EU
-#if defined(WC_NARROW) || defined(WC_GLOBAL_STATE)
 #define WC_DUAL_WAVES_PER_EU WC_WAVES_PER_EU
-#else
-#define WC_DUAL_WAVES_PER_EU 3
-#endif
 #endif
 
 constexpr int kMaxChild = 64;
-constexpr uint32_t kNCB = 4;  // dual engine: children built together (engine_shared list_entries)
+constexpr uint32_t kNCB = kDualChildBatch;  // dual engine: children built together (engine_shared list_entries)
+// children's edit distances (Lds::ce) as u16; e < wcap / 2, and the prune pass
+// reads the slots instead when wcap could exceed 2 * kCeNone
+constexpr uint32_t kCeNone = 0xFFFFu;
+__device__ __forceinline__ uint16_t ce16(uint32_t e) { return e == kInactive ? (uint16_t)kCeNone : (uint16_t)e; }
+__device__ __forceinline__ uint32_t ce32(uint32_t c) { return c == kCeNone ? kInactive : c; }
 constexpr uint32_t WC_E_COVERAGE_GAP_CODE = 3;  // include/waffle_con.h
 constexpr uint32_t WC_E_INVARIANT_CODE = 10;  // include/waffle_con.h
 constexpr uint32_t WC_E_LIMIT_CODE = 11;
@@ -180,7 +184,8 @@ struct Lds {
   Sh<SlotMeta>* meta;
   Sh<RInfo>* rinfo;    // [sides][nmax]
   Sh<uint32_t>* fe;    // [sides][nmax]
-  Sh<uint32_t>* list;  // [2*nmax] work list (heavy reads / wide analyses)
+  Sh<uint32_t>* list;  // [list_entries] work list (heavy reads / wide analyses)
+  Sh<uint16_t>* ce;    // dual: [kNCB * 2][nmax] edit distances of the children being built (prune + cost; kCeNone = None)
 };
 
 __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t K) {
@@ -224,6 +229,8 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
   l.fe = (Sh<uint32_t>*)p;
   p += align16((uint64_t)sides * nmax * 4);
   l.list = (Sh<uint32_t>*)p;
+  p += align16((uint64_t)list_entries(sides, nmax) * 4);
+  l.ce = sides == 2 ? (Sh<uint16_t>*)p : nullptr;
   return l;
 }
 
@@ -488,6 +495,53 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
   return E;
 }
 
+// ---- host-resident reads (service lanes, EngineArgs::hreads) ----
+// Copies the claimed problem's reads from host memory into this workgroup's
+// staging area (one rstage_stride slot per read: the bytes, zeros after) and
+// repoints the read table at the copies (offsets from A.rbytes = the
+// workspace base). Every chunk is a 16-byte load; each thread keeps four in
+// flight, so a locus costs a few PCIe round trips rather than one per chunk.
+__device__ __noinline__ void stage_reads(const EngineArgs& A, Eng& E, uint32_t n) {
+  const int tid = threadIdx.x;
+  Gm<uint64_t>* lroff = (Gm<uint64_t>*)E.roff;
+  const Gm<uint32_t>* lrlen = E.rlenp;
+  Gm<uint8_t>* stage = (Gm<uint8_t>*)E.roff + rtab_bytes(A.nmax);
+  const uint32_t cps = (uint32_t)(A.rstage_stride / 16);
+  const uint32_t total = n * cps;
+  constexpr uint32_t kU = 4;
+  for (uint32_t g0 = tid; g0 < total; g0 += kEB * kU) {
+    uint4 v[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t g = g0 + u * kEB;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (g < total) {
+        const uint32_t r = g / cps, c = g - r * cps;
+        if (c * 16 < lrlen[r]) v[u] = *(const Gm<uint4>*)((const Gm<uint8_t>*)A.hreads + lroff[r] + (uint64_t)c * 16);
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t g = g0 + u * kEB;
+      if (g < total) {
+        const uint32_t r = g / cps, c = g - r * cps;
+        *(Gm<uint4>*)(stage + (uint64_t)r * A.rstage_stride + (uint64_t)c * 16) = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const uint64_t rel = (uint64_t)(stage - (const Gm<uint8_t>*)A.rbytes);
+  for (uint32_t r = tid; r < n; r += kEB) lroff[r] = rel + (uint64_t)r * A.rstage_stride;
+  __syncthreads();
+}
+
+// stream mode: this workgroup has left its claim loop (the host's signal that
+// the launch is draining or done, read without any HIP call)
+__device__ inline void stream_exit(const EngineArgs& A) {
+  if (A.stream && A.exited && threadIdx.x == 0)
+    __hip_atomic_store(&A.exited[blockIdx.x], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---- work claiming ----
 // Static mode: the next problem of the launch's list. Stream mode: the next
 // sequence number of the host-fed ring; wait (bounded by idle_ticks) until the
@@ -577,6 +631,7 @@ __device__ inline uint32_t claim_problem(const EngineArgs& A, Lo<Ctl>& ctl, Eng&
   P.read_begin = 0;
   E.P = P;
   __syncthreads();
+  if (A.hreads) stage_reads(A, E, P.n_reads);
   return seq;
 }
 
@@ -1082,7 +1137,36 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
   uint32_t nk = 0;
   SymSet known = {0, 0, 0, 0};
   auto ins_at = [&](uint32_t j) { return j < 8 ? byte_at(ins_lo, j) : byte_at(ins_hi, j - 8); };
-  for (uint32_t base = 0; base < n; base += 64) {
+  // Unweighted votes where no read has two distinct tip symbols (`multi`
+  // false): every voter adds exactly 1.0 to its one symbol, so one ballot per
+  // distinct symbol gives both the insertion order and the (exact) per-key
+  // sums; lane i counts the reads of the i-th inserted key.
+  const bool single_sym = !weighted && !multi;
+  uint32_t cins = 0;
+  for (uint32_t base = 0; base < n && single_sym; base += 64) {
+    const uint32_t r = base + lane;
+    RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
+    if (r < n) x = load(r);
+    const uint32_t s0 = (x.e != kInactive && x.n) ? byte_at(x.sym, 0) : 0x100u;
+    uint64_t rem = ballot(s0 != 0x100u);
+    while (rem) {
+      const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)s0, __builtin_ctzll(rem));
+      const uint64_t mm = ballot(s0 == s);
+      rem &= ~mm;
+      uint32_t k = 0;
+      if (known.has(s)) {
+        while (ins_at(k) != s) ++k;
+      } else {
+        if (nk == (uint32_t)kKout) return false;
+        if (nk < 8) ins_lo |= (uint64_t)s << (8 * nk);
+        else ins_hi |= (uint64_t)s << (8 * (nk - 8));
+        k = nk++;
+        known.add(s);
+      }
+      if ((uint32_t)lane == k) cins += (uint32_t)__popcll((unsigned long long)mm);
+    }
+  }
+  for (uint32_t base = 0; base < n && !single_sym; base += 64) {
     const uint32_t r = base + lane;
     RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
     if (r < n) x = load(r);
@@ -1130,7 +1214,7 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
       fxc->ord[e] = ord;
     }
   }
-  uint64_t k_lo = 0, k_hi = 0;
+  uint64_t k_lo = 0, k_hi = 0, k_ins = 0;  // k_ins: nibble j = insertion index of output key j
   uint32_t m = 0;
   const bool drop_wc = wc >= 0 && nk > 1;
   for (uint32_t k = 0; k < nk; ++k) {
@@ -1138,6 +1222,7 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
     if (drop_wc && s == (uint32_t)(uint8_t)wc) continue;
     if (m < 8) k_lo |= (uint64_t)s << (8 * m);
     else k_hi |= (uint64_t)s << (8 * (m - 8));
+    k_ins |= (uint64_t)nib(ord, k) << (4 * m);
     m++;
   }
   auto key_at = [&](uint32_t j) { return j < 8 ? byte_at(k_lo, j) : byte_at(k_hi, j - 8); };
@@ -1152,7 +1237,12 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
   // (few) multi-symbol reads. Any other split (3, 5, 6, 7 or more than 8
   // tips) can round, and then every key takes the ordered fold below.
   bool fold = weighted;
-  if (!weighted) {
+  if (single_sym) {
+    // output key j (lane j) gets the read count of its insertion index
+    const uint32_t src = (uint32_t)lane < m ? nib(k_ins, (uint32_t)lane) : 0u;
+    const uint32_t c = (uint32_t)__shfl((int)cins, (int)src, 64);
+    accv = (uint32_t)lane < m ? (double)c : 0.0;
+  } else if (!weighted) {
     uint32_t c8 = 0;
     for (uint32_t base = 0; base < n && !fold; base += 64) {
       const uint32_t r = base + lane;
@@ -1253,7 +1343,11 @@ WC_PHASE_FN bool wave_votes(Lo<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, co
 #else
                                   nullptr,
 #endif
+#ifdef WC_NO_FXCACHE
+                                  nullptr);
+#else
                                   &ctl.fxc[side]);
+#endif
   if (!ok) return false;
   if ((uint32_t)lane < m) {
     ctl.keys[side][lane] = (uint8_t)key;
@@ -1403,7 +1497,15 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     for (uint32_t q = 0; q < 2 * cn; ++q) {
       const uint32_t c = c0 + q / 2, sd = q & 1u;
       const int sym = uni((int32_t)ctl.ch_s[c][sd]);
-      if (sym < 0) continue;
+      Sh<uint16_t>* ceq = E.L.ce + (uint64_t)q * E.nmax;
+      if (sym < 0) {
+        // a side this child does not push keeps the parent's edit distances
+        // (a locked side of a dual child); a single child has no side 1
+        const bool keep = tdual;
+        const Sh<RInfo>* par = E.L.rinfo + (sd ? E.nmax : 0u);  // the parent's analysis of this side
+        for (uint32_t r = tid; r < n; r += kEB) ceq[r] = ce16(keep ? par[r].e : kInactive);
+        continue;
+      }
       const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       const uint32_t olen = uni(E.L.meta[slot].len[sd]);
       SideView v = E.sv(slot, sd);
@@ -1412,6 +1514,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         uint32_t kind = 0;  // 1: group list, 2: wave list
         if (r < n) {
           const RRaw s = rstate_load(&v.rs[r]);
+          if (rraw_e(s) == kInactive) ceq[r] = (uint16_t)kCeNone;
           if (rraw_e(s) != kInactive) {
             if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
               kind = 2;
@@ -1428,6 +1531,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
               } else {
                 tc.updates++;
                 tc.w_out += 2 * f.e + 1;
+                ceq[r] = ce16(f.e);
               }
             }
           }
@@ -1461,6 +1565,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const GroupOut go = group_edinc(act, &v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
                                       E.L.meta[slot].len[sd], cfg.wildcard, early, E.wcap);
       const uint32_t g = go.st, e = go.e;
+      if (act && (lane & 15) == 0 && g == kG_DONE) E.L.ce[(uint64_t)q * E.nmax + r] = ce16(e);
       gc.edinc += go.edinc;
       gc.updates += go.updates;
       gc.w_out += go.w_out;
@@ -1483,6 +1588,8 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         if (!wave_edinc_mem(&v2.rs[r2], v2.wf + (uint64_t)r2 * E.wcap, e2, E.read(r2), E.rlen(r2), v2.con,
                             uni(E.L.meta[slot2].len[sd2]), cfg.wildcard, early, E.wcap, cnt, eo)) {
           if (lane == 0) atomicOr(&ctl.ovf, 4u);
+        } else if (lane == 0) {
+          E.L.ce[(uint64_t)q2 * E.nmax + r2] = ce16(eo);
         }
       }
     }
@@ -1506,6 +1613,8 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
                       uni(E.L.meta[slot].len[sd]), (uint8_t)uni((int32_t)ctl.ch_s[c][sd]), cfg.wildcard, early,
                       E.wcap, cnt, e)) {
         if (lane == 0) atomicOr(&ctl.ovf, 4u);
+      } else if (lane == 0) {
+        E.L.ce[(uint64_t)q * E.nmax + r] = ce16(e);
       }
     }
     SUB_T1(20, tw);
@@ -1514,10 +1623,12 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     PH_MARK(6);
     // reads whose offset activates at a child's new max length
     // (dual_consensus.rs:633-639): consensus 1 always, consensus 2 too when dual
+    bool activated = false;  // (uniform) then the prune pass reads the slots, not ce
     for (uint32_t c = c0; c < c0 + cn; ++c) {
       const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       const uint32_t nl0 = uni(E.L.meta[slot].len[0]), nl1 = uni(E.L.meta[slot].len[1]);
       if (max(nl0, nl1) > E.P.max_act) continue;
+      activated = true;
       activate_side<false>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
       if (uni(E.L.meta[slot].flags) & 1u) activate_side<false>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
     }
@@ -1533,6 +1644,9 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     }
     SUB_T1(22, tp0);
     SUB_T0(tp1);
+    // edit distances from the slots when an activation changed them, or when
+    // they might not fit the u16 array (wavefront rows past 2^17 entries)
+    const bool slot_e = activated || E.wcap > 2u * kCeNone;
     uint64_t ccost[kNCB] = {0, 0, 0, 0};
     uint32_t cn0[kNCB] = {0, 0, 0, 0}, cn1[kNCB] = {0, 0, 0, 0};
     for (uint32_t r = tid; r < n; r += kEB) {
@@ -1541,8 +1655,11 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       for (uint32_t k = 0; k < kNCB; ++k) {
         e1[k] = e2[k] = kInactive;
         if (k < cn) {
-          e1[k] = E.sv(cslot[k], 0).rs[r].e;
-          if (cdual & (1u << k)) e2[k] = E.sv(cslot[k], 1).rs[r].e;
+          // each child's edit distances as its pushes left them (LDS), or
+          // from its slot when an activation changed them
+          e1[k] = slot_e ? E.sv(cslot[k], 0).rs[r].e : ce32(E.L.ce[(uint64_t)(2 * k) * E.nmax + r]);
+          if (cdual & (1u << k))
+            e2[k] = slot_e ? E.sv(cslot[k], 1).rs[r].e : ce32(E.L.ce[(uint64_t)(2 * k + 1) * E.nmax + r]);
         }
       }
 #pragma unroll
@@ -1863,6 +1980,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
     }
     finish_problem(A, ctl, outp, prob, oslot);
   }
+  stream_exit(A);
 }
 
 // =====================================================================
@@ -2177,6 +2295,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
     }
     finish_problem(A, ctl, outp, prob, oslot);
   }
+  stream_exit(A);
 }
 
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT)

@@ -24,6 +24,10 @@
 #include <queue>
 #include <thread>
 
+#include <mutex>
+
+#include <hsa/hsa_ext_amd.h>
+
 #include "sched.hpp"
 
 using namespace wc;
@@ -78,7 +82,7 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   const uint64_t per_wg = std::max<uint64_t>(16ull << 20, hbm_budget / conc);
   const uint64_t budget = sides == 1 ? (16ull << 20) : std::min<uint64_t>(256ull << 20, per_wg);
   const uint32_t pmax = sides == 1 ? 256u : 1024u;
-  uint64_t lmax = sides == 1 ? 40 * 1024 : 48 * 1024;
+  uint64_t lmax = sides == 1 ? 40 * 1024 : 52 * 1024;  // dual: still 3 workgroups per CU
   if (const char* e = getenv("WC_DUAL_LDS_KB"))  // experiment hook: LDS budget of the dual node pool
     if (sides == 2) lmax = (uint64_t)atoi(e) * 1024;
   // WC_GSTATE=1 (test hook) forces the global-state build for every launch
@@ -165,6 +169,45 @@ void destroy_launches(wc_ctx* ctx) {
   ctx->launches.clear();
 }
 
+// WC_FAULT_LOG=1 (diagnostics): on a GPU memory fault, print the faulting
+// address against the buffers of the launches started last (which buffer,
+// which workgroup's workspace, the offset inside it)
+namespace {
+struct FaultRange {
+  const char* name;
+  uint64_t base, bytes, stride;
+};
+std::mutex g_fault_mu;
+std::vector<FaultRange> g_fault_ranges;
+hsa_status_t fault_event(const hsa_amd_event_t* ev, void*) {
+  if (ev->event_type != HSA_AMD_GPU_MEMORY_FAULT_EVENT) return HSA_STATUS_SUCCESS;
+  const uint64_t va = ev->memory_fault.virtual_address;
+  fprintf(stderr, "[wc] GPU memory fault at 0x%llx (reason mask 0x%x)\n", (unsigned long long)va,
+          ev->memory_fault.fault_reason_mask);
+  std::lock_guard<std::mutex> g(g_fault_mu);
+  for (const FaultRange& r : g_fault_ranges) {
+    const int64_t d = (int64_t)(va - r.base);
+    fprintf(stderr, "[wc]   %-8s base 0x%llx bytes %llu stride %llu: offset %lld", r.name, (unsigned long long)r.base,
+            (unsigned long long)r.bytes, (unsigned long long)r.stride, (long long)d);
+    if (r.stride && d >= 0) fprintf(stderr, " (workgroup %lld + %lld)", (long long)(d / (int64_t)r.stride), (long long)(d % (int64_t)r.stride));
+    fprintf(stderr, "\n");
+  }
+  return HSA_STATUS_SUCCESS;
+}
+void fault_log_record(const Launch& L, const EngineArgs& a, const Caps& caps) {
+  static std::once_flag once;
+  std::call_once(once, [] { (void)hsa_amd_register_system_event_handler(fault_event, nullptr); });
+  std::lock_guard<std::mutex> g(g_fault_mu);
+  if (g_fault_ranges.size() > 64) g_fault_ranges.erase(g_fault_ranges.begin(), g_fault_ranges.begin() + 32);
+  g_fault_ranges.push_back({"ws", (uint64_t)a.ws, (uint64_t)L.ws.cap, a.ws_stride});
+  if (caps.gstate) g_fault_ranges.push_back({"gstate", (uint64_t)a.gstate, (uint64_t)L.gst.cap, a.gstate_stride});
+  g_fault_ranges.push_back({"reads", (uint64_t)a.rbytes, 0, 0});
+  g_fault_ranges.push_back({"problems", (uint64_t)a.problems, 0, 0});
+  g_fault_ranges.push_back({"out", (uint64_t)a.out, (uint64_t)a.out_stride * L.P, a.out_stride});
+  if (a.act_scr) g_fault_ranges.push_back({"act", (uint64_t)a.act_scr, (uint64_t)L.act.cap, a.act_stride * 8});
+}
+}  // namespace
+
 // launches the engine of `caps` (LDS or global-state build) on L's stream
 int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
   if (caps.gstate) {
@@ -177,6 +220,7 @@ int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
   HIPCHK(hipMemsetAsync(L.ws.p, kGuardByte, a.ws_stride * L.grid, L.stream));
   if (caps.gstate) HIPCHK(hipMemsetAsync(L.gst.p, kGuardByte, a.gstate_stride * L.grid, L.stream));
 #endif
+  if (getenv("WC_FAULT_LOG")) fault_log_record(L, a, caps);
   HIPCHK(hipEventRecord(L.ev0, L.stream));
   if (caps.gstate) {
     if (caps.sides == 1) wcg::launch_single_engine(a, L.grid, 0, L.stream);
@@ -504,9 +548,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   L.P = 2 * L.grid;  // two output slots per workgroup
   L.kernel_ms = 0;
   const uint32_t P = L.P;
-  L.off_status = align16((uint64_t)P * 4);
-  L.off_stats = L.off_status + align16((uint64_t)P * 4);
-  L.off_out = L.off_stats + align16((uint64_t)P * S_NSTAT * 8);
+  L.stream_layout();
   if (!L.host.ensure(L.off_out + (uint64_t)P * caps.ob, true))
     return set_err(ctx, WC_E_HIP, "pinned host allocation failed (results)");
   memset(L.host.p, 0, L.off_out);
@@ -570,6 +612,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.sctl = (StreamCtl*)dr;
   a.qhead = (uint32_t*)L.counter.p;
   a.idle_ticks = (uint64_t)clk * 1000ull * 30ull;  // 30 s without a host heartbeat: the host is gone
+  a.exited = (uint32_t*)(dh + L.off_exit);
   const int krc = launch_kernel(ctx, L, a, caps);
   if (krc != WC_OK) return krc;
   L.busy = true;
@@ -677,12 +720,14 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
       continue;
     }
     // watchdog: the launch must not end (or give up) while problems are out
-    if (sc->abort || hipStreamQuery(L.stream) == hipSuccess) {
+    // (exit flags, no HIP call; a stream query only after seconds without
+    // progress, to notice a launch that faulted)
+    const double idle = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_idle).count();
+    if (sc->abort || L.all_exited() || (idle > 5.0 && hipStreamQuery(L.stream) != hipErrorNotReady)) {
       rc = set_err(ctx, WC_E_HIP, "stream launch ended with problems outstanding (abort=" +
                                       std::to_string(sc->abort) + ")");
       break;
     }
-    const double idle = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_idle).count();
     if (idle > 300.0) {
       rc = set_err(ctx, WC_E_HIP, "stream launch made no progress for 300 s");
       break;

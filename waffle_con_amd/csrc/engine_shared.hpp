@@ -113,6 +113,14 @@ struct EngineArgs {
   struct StreamCtl* sctl;
   uint32_t* qhead;
   uint64_t idle_ticks;   // wall-clock ticks without a host heartbeat before a waiting workgroup gives up
+  uint32_t* exited;      // stream mode: per-workgroup exit flags (host-mapped), set as a workgroup leaves
+  // stream mode with host-resident reads (service lanes): the claimed
+  // problem's reads are copied from `hreads` (host-mapped; roff/rlen index
+  // it) into the workgroup's staging area (rstage_stride bytes per read,
+  // after its read table), and read from there; rbytes is then the
+  // workspace base the staged offsets are relative to
+  const uint8_t* hreads;
+  uint64_t rstage_stride;
   // global-state build (engine_gstate.hip): per-workgroup HBM region holding
   // what lds_bytes() describes
   uint8_t* gstate;
@@ -129,6 +137,9 @@ struct alignas(16) StreamCtl {  // tail and stop form one 8-byte word (read toge
 __host__ __device__ inline uint64_t rtab_bytes(uint32_t nmax) {
   return ((uint64_t)nmax * 8 + 15) / 16 * 16 * 2 + ((uint64_t)nmax * 4 + 15) / 16 * 16;
 }
+// staging stride of one read pulled from host memory (EngineArgs::hreads): its
+// bytes rounded up to 16, then 64 zero bytes (the engine's over-read margin)
+__host__ __device__ inline uint64_t rstage_stride(uint32_t maxlen) { return ((uint64_t)maxlen + 15) / 16 * 16 + 64; }
 constexpr int kPhases = 32;
 // offset-activation scratch per workgroup (u64): per wave two lane-interleaved pair arrays of m entries
 __host__ __device__ inline uint64_t act_scr_u64(uint32_t m) { return (uint64_t)kWaves * 2 * m * 64; }  // 0..15 block phases, 16..31 wave-0 sub-phases
@@ -239,6 +250,8 @@ __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K) {
   return t;
 }
 
+// the dual engine builds up to this many children of a node in one pass (engine.hip kNCB)
+constexpr uint32_t kDualChildBatch = 4;
 // work list entries (u32): heavy (side, read) items; the dual engine builds up
 // to 4 children at once (engine.hip kNCB), so 2 sides x 4 children x nmax
 __host__ __device__ inline uint64_t list_entries(uint32_t sides, uint32_t nmax) {
@@ -247,7 +260,7 @@ __host__ __device__ inline uint64_t list_entries(uint32_t sides, uint32_t nmax) 
 // sides whose expanded node's RStates are held in LDS (single engine only)
 __host__ __device__ inline uint32_t hot_sides(uint32_t sides) { return sides == 1 ? 1u : 0u; }
 // LDS: hot RStates[hot_sides][nmax] | chain area | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
-//      heavy list[2*nmax] u32
+//      heavy list[list_entries] u32 | (dual) child e[kDualChildBatch][2][nmax] u16
 __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t chain) {
   uint64_t t = (uint64_t)hot_sides(sides) * nmax * sizeof(RState);
   t += chain_lds_bytes(nmax, chain);
@@ -257,6 +270,8 @@ __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uin
   t += (uint64_t)sides * nmax * sizeof(RInfo);
   t += align16((uint64_t)sides * nmax * 4);
   t += align16((uint64_t)list_entries(sides, nmax) * 4);
+  // dual engine: the children's edit distances per (child, side, read) of one build pass (prune + cost), u16
+  if (sides == 2) t += align16((uint64_t)kDualChildBatch * 2 * nmax * 2);
   return align16(t);
 }
 

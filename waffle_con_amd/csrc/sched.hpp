@@ -45,6 +45,7 @@ struct Launch {
   Caps caps;
   uint32_t P = 0, grid = 0;
   uint64_t off_status = 0, off_stats = 0, off_out = 0;
+  uint64_t off_exit = 0;  // stream launches: exited[grid] (between stats and out)
   std::vector<uint32_t> ids;  // launch problem k -> caller item id
   std::vector<uint8_t> taken;
   uint32_t n_taken = 0;
@@ -60,6 +61,23 @@ struct Launch {
   const uint32_t* status() const { return (const uint32_t*)((const uint8_t*)host.p + off_status); }
   const uint64_t* stats() const { return (const uint64_t*)((const uint8_t*)host.p + off_stats); }
   const uint8_t* out(uint32_t k) const { return (const uint8_t*)host.p + off_out + (uint64_t)k * caps.ob; }
+  // stream launches: the host-buffer layout (P output slots, grid exit flags)
+  void stream_layout() {
+    off_status = align16((uint64_t)P * 4);
+    off_stats = off_status + align16((uint64_t)P * 4);
+    off_exit = off_stats + align16((uint64_t)P * S_NSTAT * 8);
+    off_out = off_exit + align16((uint64_t)grid * 4);
+  }
+  // stream launches: every workgroup has left its claim loop. Read from the
+  // host-mapped flags, never through a HIP call: a stream query can wait on a
+  // runtime lock that another thread holds while its own work queues behind
+  // this (persistent) launch
+  bool all_exited() const {
+    const uint32_t* e = (const uint32_t*)((const uint8_t*)host.p + off_exit);
+    for (uint32_t k = 0; k < grid; ++k)
+      if (!__atomic_load_n(&e[k], __ATOMIC_ACQUIRE)) return false;
+    return true;
+  }
   ~Launch() {
     for (DevBuf* b : {&probs, &sroff, &srlen, &ract, &ws, &counter, &act, &phases, &gst}) b->release();
     host.release();
@@ -88,5 +106,11 @@ uint32_t harvest(const Launch& L, uint32_t k, const SubProb& s, EngineOut& o);
 void bump(SubProb& s, uint32_t st);
 // waits for the launch, records its kernel time (and, WC_CHECK, verifies guards)
 int launch_finish(wc_ctx* ctx, Launch& L);
+// frees the device and pinned buffers a (finished) launch keeps cached
+inline void launch_release_buffers(Launch& L) {
+  for (DevBuf* b : {&L.probs, &L.sroff, &L.srlen, &L.ract, &L.ws, &L.counter, &L.act, &L.phases, &L.gst}) b->release();
+  L.host.release();
+  L.ring.release();
+}
 
 }  // namespace wch

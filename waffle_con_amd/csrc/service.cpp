@@ -5,24 +5,39 @@
 // by persistent stream-mode engine launches instead of one small launch per
 // call.
 //
-// A caller packs its reads, reserves a range of the service's HBM read arena,
-// copies them there and queues the request; the service thread publishes it
-// into the host-mapped ring of a running launch ("lane": one persistent
-// launch of the single or dual engine for one CdwfaConfig; engine.hip stream
-// mode, the same machinery PriorityConsensusDWFA uses), whose workgroups claim
-// problems as they free up. The result comes back through the launch's
-// host-mapped result slots; the service builds the reference's result types
-// and wakes that caller. So any number of threads calling consensus() share
-// the whole GPU, one workgroup per in-flight locus, and a call costs one
-// locus's search latency plus a few tens of microseconds.
+// A caller writes its reads into a reservation of the service's pinned,
+// host-mapped arena and queues the request — no HIP call on the caller's
+// side; the service thread publishes it into the host-mapped ring of a
+// running launch ("lane": one persistent launch of the single or dual engine
+// for one CdwfaConfig; engine.hip stream mode, the same machinery
+// PriorityConsensusDWFA uses). The workgroup that claims it pulls the reads
+// into its HBM workspace (engine.hip stage_reads) and runs the search. The
+// result comes back through the launch's host-mapped result slots; the
+// service builds the reference's result types and wakes that caller. So any
+// number of threads calling consensus() share the whole GPU, one workgroup
+// per in-flight locus, and a call costs one locus's search latency plus a few
+// tens of microseconds.
 //
-// Lanes start on demand and stop after kIdleMs without work (their idle
-// workgroups would otherwise hold CUs). Requests a lane cannot take — read
-// counts or lengths beyond its planned capacities — make it drain and restart
-// with larger ones. Offsets (add_sequence_offset), problems that still ask for
-// more capacity (ST_RETRY) and any service failure take the batch path on a
+// While a lane runs, the service thread makes no HIP call either: the lane's
+// end is read from its workgroups' host-mapped exit flags. A persistent
+// kernel shares the process's few hardware queues with every other stream,
+// so other threads' work can queue behind it, and a HIP call that waits on
+// the runtime lock such a thread holds would stall the heartbeat the lane's
+// workgroups watch (they give up after 30 s without one).
+//
+// One lane runs at a time: it starts on demand and stops after kIdleMs
+// without work (its idle workgroups would otherwise hold CUs). A request it
+// cannot take — another kind or config, or read counts or lengths beyond its
+// planned capacities — makes it drain and restart for that request, in arrival
+// order. (Two concurrent lanes would each want the whole chip, and resizing
+// one lane's buffers while another runs deadlocks: hipFree waits for every
+// kernel on the device, and a lane's kernel only ends when the service thread
+// says so.) Offsets (add_sequence_offset), problems that still ask for more
+// capacity (ST_RETRY) and any service failure take the batch path on a
 // per-thread context (wc_consensus_batch with one problem), which plans and
-// retries capacities as usual: results never depend on the path.
+// retries capacities as usual: results never depend on the path. A lane that
+// cannot start (HBM) sends its requests there too, after one retry with the
+// lane's cached buffers released.
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -40,11 +55,10 @@ using namespace wch;
 
 namespace {
 
-constexpr uint32_t kLanes = 4;            // concurrent (kind, config) lanes
 constexpr uint32_t kQcap = 1u << 14;      // published, unfinished problems per lane
 constexpr uint32_t kQslots = 1u << 21;    // their read-table entries
 constexpr double kIdleMs = 2.0;           // a lane with nothing to do stops after this
-constexpr uint64_t kArenaDefault = 4ull << 30;
+constexpr uint64_t kArenaDefault = 1ull << 30;  // pinned host memory for in-flight callers' reads
 
 using Clock = std::chrono::steady_clock;
 
@@ -82,7 +96,7 @@ struct Lane {
   uint32_t grid_full = 0;  // workgroups a full-chip launch of this lane would ask for
   bool can_grow = false;   // a restart with more requests waiting would get more workgroups
   uint64_t rw = 0;
-  Clock::time_point idle_since;
+  Clock::time_point idle_since, started, last_result, last_query;
 };
 
 }  // namespace
@@ -94,13 +108,13 @@ struct wc_service {
   std::condition_variable cv_svc;    // requests arrived
   std::condition_variable cv_arena;  // arena space was released
   std::deque<Req*> ready;            // copied to the arena, not yet published (FIFO)
-  DevBuf arena;
+  HostBuf arena;                     // pinned, host-mapped: callers' reads (the lanes pull them)
+  const uint8_t* arena_dev = nullptr;  // its device address
   std::map<uint64_t, uint64_t> live;  // arena reservations: offset -> bytes
   uint64_t cursor = 0;
-  Lane lanes[kLanes];
+  Lane lane;  // at most one running launch (see service_loop)
   std::thread th;
   bool stop = false;
-  bool failed = false;  // a HIP failure disabled the service: every call takes the batch path
   std::string err;
   wc_service_stats stats{};
 };
@@ -153,10 +167,12 @@ bool lane_fits(const Lane& ln, const Req* q) {
          q->sp.gid.size() <= ln.nmax && q->sp.max_len <= ln.maxlen;
 }
 
-// starts lane k for the requests waiting with q's kind and config
-int lane_start(wc_service* S, uint32_t k, const Req* q) {
-  Lane& ln = S->lanes[k];
+// starts the lane for the requests waiting with q's kind and config
+int lane_start(wc_service* S, const Req* q) {
+  Lane& ln = S->lane;
+  Launch* const prev = ln.L;
   ln = Lane();
+  ln.L = prev;
   ln.sides = q->sides;
   ln.cfg = q->cfg;
   // capacity envelope: every waiting request of this kind and config, rounded up
@@ -172,7 +188,7 @@ int lane_start(wc_service* S, uint32_t k, const Req* q) {
   env[0].gid.assign(ln.nmax, 0);
   env[0].max_len = ln.maxlen;
   wc_ctx* ctx = S->ctx;
-  Launch* L = launch_slot(ctx, k);
+  Launch* L = launch_slot(ctx, 0);
   if (!L) return set_err(ctx, WC_E_HIP, "stream creation failed");
   ln.L = L;
   // workgroups: twice the requests waiting for this lane (callers block on
@@ -196,9 +212,7 @@ int lane_start(wc_service* S, uint32_t k, const Req* q) {
   L->P = 2 * L->grid;  // two output slots per workgroup
   L->kernel_ms = 0;
   const uint32_t P = L->P;
-  L->off_status = align16((uint64_t)P * 4);
-  L->off_stats = L->off_status + align16((uint64_t)P * 4);
-  L->off_out = L->off_stats + align16((uint64_t)P * S_NSTAT * 8);
+  L->stream_layout();
   if (!L->host.ensure(L->off_out + (uint64_t)P * caps.ob, true))
     return set_err(ctx, WC_E_HIP, "pinned host allocation failed (service results)");
   memset(L->host.p, 0, L->off_out);
@@ -218,7 +232,9 @@ int lane_start(wc_service* S, uint32_t k, const Req* q) {
   ln.qroff = (uint64_t*)(rh + off_roff);
   ln.qract = (int64_t*)(rh + off_ract);
   ln.qrlen = (uint32_t*)(rh + off_rlen);
-  const uint64_t wsb = caps.wsb + rtab_bytes(caps.nmax) + kGuard;
+  // workspace per workgroup: engine | read table | staged reads | guard
+  const uint64_t rstride = rstage_stride(ln.maxlen);
+  const uint64_t wsb = caps.wsb + rtab_bytes(caps.nmax) + (uint64_t)caps.nmax * rstride + kGuard;
   if (!L->ws.ensure(wsb * L->grid + 64) || !L->counter.ensure(4))
     return set_err(ctx, WC_E_HIP, "device allocation failed (service workspace)");
   HIPCHK(hipMemsetAsync(L->counter.p, 0, 4, L->stream));
@@ -234,7 +250,9 @@ int lane_start(wc_service* S, uint32_t k, const Req* q) {
   a.cfg = to_dev(ln.cfg);
   a.problems = (const DevProblem*)(dr + off_q);
   a.sides = ln.sides;
-  a.rbytes = (const uint8_t*)S->arena.p;
+  a.rbytes = (const uint8_t*)L->ws.p;  // staged reads are addressed from the workspace base
+  a.hreads = S->arena_dev;
+  a.rstage_stride = rstride;
   a.roff = (const uint64_t*)(dr + off_roff);
   a.rlen = (const uint32_t*)(dr + off_rlen);
   a.ractivate = (const int64_t*)(dr + off_ract);
@@ -257,15 +275,16 @@ int lane_start(wc_service* S, uint32_t k, const Req* q) {
   a.sctl = (StreamCtl*)dr;
   a.qhead = (uint32_t*)L->counter.p;
   a.idle_ticks = (uint64_t)clk * 1000ull * 30ull;  // 30 s without a heartbeat: the host is gone
+  a.exited = (uint32_t*)(dh + L->off_exit);
   rc = launch_kernel(ctx, *L, a, caps);
   if (rc != WC_OK) return rc;
   L->busy = true;
   ln.running = true;
-  ln.idle_since = Clock::now();
+  ln.idle_since = ln.started = ln.last_result = Clock::now();
   S->stats.lane_starts++;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] service lane %u: sides=%u grid=%u per_cu=%d nmax=%u maxlen=%u pcap=%u wcap=%u lcap=%u chain=%u\n",
-            k, ln.sides, L->grid, caps.per_cu, caps.nmax, ln.maxlen, caps.pcap, caps.wcap, caps.lcap, caps.chain);
+    fprintf(stderr, "[wc] service lane: sides=%u grid=%u per_cu=%d nmax=%u maxlen=%u pcap=%u wcap=%u lcap=%u chain=%u\n",
+            ln.sides, L->grid, caps.per_cu, caps.nmax, ln.maxlen, caps.pcap, caps.wcap, caps.lcap, caps.chain);
   return WC_OK;
 }
 
@@ -318,9 +337,17 @@ uint32_t lane_poll(wc_service* S, Lane& ln) {
   return got;
 }
 
-// ends the lane's launch (nothing may be outstanding unless it failed)
+// ends the lane's launch (nothing may be outstanding unless it failed): every
+// workgroup leaves its claim loop (exit flags, heartbeat kept up) before the
+// one HIP call that retires the launch
 void lane_stop(wc_service* S, Lane& ln, bool failed) {
   __atomic_store_n(&ln.sc->stop, 1u, __ATOMIC_RELEASE);
+  const auto t0 = Clock::now();
+  while (!ln.L->all_exited() && !ln.sc->abort &&
+         std::chrono::duration<double>(Clock::now() - t0).count() < 60.0) {
+    __atomic_store_n(&ln.sc->heartbeat, ++ln.beat, __ATOMIC_RELAXED);
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
   (void)launch_finish(S->ctx, *ln.L);
   if (failed)
     for (uint32_t s = ln.oldest; s < ln.seq_req.size(); ++s)
@@ -335,66 +362,75 @@ void lane_stop(wc_service* S, Lane& ln, bool failed) {
 void service_loop(wc_service* S) {
   (void)hipSetDevice(S->device);
   std::unique_lock<std::mutex> lk(S->mu);
+  Lane& ln = S->lane;
+  const bool trace = getenv("WC_SVC_TRACE") != nullptr;  // diagnostics: report stalls of this loop
+  Clock::time_point last_beat = Clock::now();
   for (;;) {
     bool progress = false;
-    // 1. publish in arrival order: each request to the running lane of its kind
-    //    and config; one that no lane can take starts a lane (a free one, or an
-    //    idle one is replaced), or makes its lane drain and restart with larger
-    //    capacities. A request that has to wait holds back the ones after it
-    //    only for its own lane.
-    std::vector<uint8_t> blocked(kLanes, 0);
-    for (auto it = S->ready.begin(); it != S->ready.end();) {
-      Req* q = *it;
-      int k = -1;
-      for (uint32_t j = 0; j < kLanes; ++j)
-        if (S->lanes[j].running && S->lanes[j].sides == q->sides && same_cfg(S->lanes[j].cfg, q->cfg)) k = (int)j;
-      if (k >= 0 && !blocked[k] && lane_fits(S->lanes[k], q)) {
-        if (lane_publish(S->lanes[k], q)) {
-          it = S->ready.erase(it);
-          progress = true;
-          continue;
+    if (ln.running) {
+      // 1. publish in arrival order; the first request the lane cannot take
+      //    (another kind or config, or larger capacities) makes it drain, and
+      //    nothing behind that request is published before the restart
+      while (!ln.draining && !S->ready.empty()) {
+        Req* q = S->ready.front();
+        if (!lane_fits(ln, q)) {
+          ln.draining = true;
+          break;
         }
-        blocked[k] = 1;  // ring full
-      } else if (k >= 0) {
-        if (!lane_fits(S->lanes[k], q) && !S->lanes[k].draining) S->lanes[k].draining = true;
-        blocked[k] = 1;
-      } else if (!S->failed) {
-        int f = -1;
-        for (uint32_t j = 0; j < kLanes && f < 0; ++j)
-          if (!S->lanes[j].running) f = (int)j;
-        for (uint32_t j = 0; j < kLanes && f < 0; ++j)  // replace an idle lane of another config
-          if (S->lanes[j].outstanding == 0) {
-            lane_stop(S, S->lanes[j], false);
-            f = (int)j;
+        if (!lane_publish(ln, q)) break;  // ring full
+        S->ready.pop_front();
+        progress = true;
+      }
+    } else if (!S->ready.empty()) {
+      // a lane for the oldest request's kind and config. Buffers are only
+      // resized here, with no lane running: hipFree waits for every kernel on
+      // the device, the lane's own included, and that one only ends when this
+      // thread tells it to.
+      const Req* q = S->ready.front();
+      int rc = lane_start(S, q);
+      if (rc != WC_OK && ln.L) {  // most often HBM: drop the cached buffers and try once more
+        launch_release_buffers(*ln.L);
+        rc = lane_start(S, q);
+      }
+      if (rc != WC_OK) {
+        // this request and the others of its kind and config take the batch path
+        S->stats.lane_failures++;
+        S->err = S->ctx->err;
+        if (getenv("WC_LAUNCH_LOG")) fprintf(stderr, "[wc] service lane start failed: %s\n", S->err.c_str());
+        const uint32_t sides = q->sides;
+        const wc_config cfg = q->cfg;
+        for (auto jt = S->ready.begin(); jt != S->ready.end();) {
+          if ((*jt)->sides == sides && same_cfg((*jt)->cfg, cfg)) {
+            complete(S, *jt, ~0u);
+            jt = S->ready.erase(jt);
+          } else {
+            ++jt;
           }
-        if (f >= 0) {
-          if (lane_start(S, (uint32_t)f, q) != WC_OK) {
-            S->failed = true;
-            S->err = S->ctx->err;
-            continue;  // the request is completed below as a service failure
-          }
-          progress = true;
-          continue;  // publish it (and its companions) on the next pass
         }
       }
-      ++it;
+      progress = true;
+      continue;  // publish on the next pass
     }
-    if (S->failed) {
-      for (Req* q : S->ready) complete(S, q, ~0u);
-      S->ready.clear();
-    }
-    // 2. harvest, 3. stop lanes that are done (idle, draining and empty, failed)
-    for (uint32_t j = 0; j < kLanes; ++j) {
-      Lane& ln = S->lanes[j];
-      if (!ln.running) continue;
+    // 2. heartbeat, tail, harvest; 3. stop the lane when it is done (idle,
+    //    draining and empty, or failed)
+    if (ln.running) {
       __atomic_store_n(&ln.sc->heartbeat, ++ln.beat, __ATOMIC_RELAXED);
+      if (trace) {
+        const auto now = Clock::now();
+        const double gap = std::chrono::duration<double, std::milli>(now - last_beat).count();
+        if (ln.beat > 1 && gap > 20.0) fprintf(stderr, "[wc] service loop: %.1f ms between heartbeats\n", gap);
+        last_beat = now;
+      }
       const uint32_t ntail = (uint32_t)ln.seq_req.size();
       if (ntail != ln.published_tail) {
         std::atomic_thread_fence(std::memory_order_release);
         __atomic_store_n(&ln.sc->tail, ntail, __ATOMIC_RELEASE);
         ln.published_tail = ntail;
       }
-      if (lane_poll(S, ln)) progress = true;
+      if (lane_poll(S, ln)) {
+        progress = true;
+        ln.last_result = Clock::now();
+      }
       // a lane planned for fewer workgroups than its callers keep busy drains
       // and restarts with a larger grid
       if (!ln.draining && ln.can_grow) {
@@ -404,23 +440,38 @@ void service_loop(wc_service* S) {
       }
       if (ln.outstanding > 0) {
         ln.idle_since = Clock::now();
-        if (ln.sc->abort || hipStreamQuery(ln.L->stream) == hipSuccess) {  // ended with problems out: fail them over
+        // ended (gave up, or every workgroup left) with problems out. No HIP
+        // call while the lane runs (see Launch::all_exited); a stream query
+        // only after seconds without a result, to notice a faulted launch
+        const uint32_t ab = ln.sc->abort;
+        bool ended = ab || ln.L->all_exited();
+        const auto now = Clock::now();
+        if (!ended && std::chrono::duration<double>(now - ln.last_result).count() > 5.0 &&
+            std::chrono::duration<double>(now - ln.last_query).count() > 1.0) {
+          ln.last_query = now;
+          ended = hipStreamQuery(ln.L->stream) != hipErrorNotReady;
+        }
+        if (ended) {  // ended with problems out: fail them over
+          char buf[160];
+          snprintf(buf, sizeof(buf), "service lane ended with %u problems outstanding (abort %u, %.1f ms after its start)",
+                   ln.outstanding, ab, std::chrono::duration<double, std::milli>(Clock::now() - ln.started).count());
+          S->err = buf;
+          if (getenv("WC_LAUNCH_LOG")) fprintf(stderr, "[wc] %s\n", buf);
           lane_stop(S, ln, true);
+          S->stats.lane_failures++;
           progress = true;
         }
-        continue;
-      }
-      const double idle = std::chrono::duration<double, std::milli>(Clock::now() - ln.idle_since).count();
-      if (ln.draining || S->stop || idle > kIdleMs) {
-        lane_stop(S, ln, false);
-        progress = true;
+      } else {
+        const double idle = std::chrono::duration<double, std::milli>(Clock::now() - ln.idle_since).count();
+        if (ln.draining || S->stop || idle > kIdleMs) {
+          lane_stop(S, ln, false);
+          progress = true;
+        }
       }
     }
-    bool any = false;
-    for (const Lane& ln : S->lanes) any |= ln.running;
-    if (S->stop && S->ready.empty() && !any) break;
+    if (S->stop && S->ready.empty() && !ln.running) break;
     if (!progress) {
-      if (!any && S->ready.empty()) S->cv_svc.wait(lk, [&] { return S->stop || !S->ready.empty(); });
+      if (!ln.running && S->ready.empty()) S->cv_svc.wait(lk, [&] { return S->stop || !S->ready.empty(); });
       else S->cv_svc.wait_for(lk, std::chrono::microseconds(20));
     }
   }
@@ -455,23 +506,6 @@ int fallback(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_probl
   return rc;
 }
 
-// a caller thread's pinned staging buffer and copy stream (per device)
-struct ThreadStage {
-  HostBuf buf;
-  hipStream_t stream = nullptr;
-  ~ThreadStage() {
-    buf.release();
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-};
-ThreadStage& thread_stage(int device) {
-  static thread_local std::map<int, ThreadStage> tl;
-  ThreadStage& ts = tl[device];
-  if (!ts.stream && hipSetDevice(device) == hipSuccess)
-    if (hipStreamCreateWithFlags(&ts.stream, hipStreamNonBlocking) != hipSuccess) ts.stream = nullptr;
-  return ts;
-}
-
 int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p, wc_results** out) {
   *out = nullptr;
   if (!S || !cfg || !p) return WC_E_BAD_INPUT;
@@ -488,28 +522,33 @@ int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_p
     for (uint32_t r = 0; r < n; ++r) offs[r] = p->offsets[r] < 0 ? -1 : p->offsets[r];
   std::string aerr;
   const int arc = activation_plan(*cfg, offs, q->sp, aerr);
-  bool failed;
   {
     std::lock_guard<std::mutex> g(S->mu);
-    failed = S->failed;
     S->stats.calls++;
   }
-  // offsets (activation scratch), deep problems (> 256 reads: the batch path
-  // gives them a launch of their own) and a disabled service take the batch path
-  if (arc != WC_OK || q->sp.max_act > 0 || n > (uint32_t)kBlock || failed) return fallback(S, sides, cfg, p, out);
-  // reads back to back (16-byte aligned) plus 64 bytes of tail padding,
-  // staged in this thread's pinned buffer and copied on its own stream (DMA at
-  // full link speed, overlapping other callers' copies)
+  // offsets (activation scratch) and deep problems (> 256 reads: the batch
+  // path gives them a launch of their own) take the batch path
+  if (arc != WC_OK || q->sp.max_act > 0 || n > (uint32_t)kBlock) return fallback(S, sides, cfg, p, out);
+  // reads back to back (16-byte aligned) in a reservation of the pinned
+  // arena, written straight from the caller's buffers: the lane's workgroups
+  // pull them into HBM when they claim the locus, so a call makes no HIP
+  // call at all (a copy on a stream could queue behind the running lane)
   std::vector<uint64_t> rel(n);
   uint64_t total = 0;
   for (uint32_t r = 0; r < n; ++r) {
     rel[r] = total;
     total += (p->lens[r] + 15) & ~15ull;
   }
-  total += 64;
-  ThreadStage& ts = thread_stage(S->device);
-  if (!ts.stream || !ts.buf.ensure(total)) return fallback(S, sides, cfg, p, out);
-  uint8_t* h = (uint8_t*)ts.buf.p;
+  total = std::max<uint64_t>(total, 16);
+  {
+    std::unique_lock<std::mutex> lk(S->mu);
+    if (total > S->arena.cap / 4) {
+      lk.unlock();
+      return fallback(S, sides, cfg, p, out);
+    }
+    S->cv_arena.wait(lk, [&] { return arena_alloc(S, total, q->aoff); });
+  }
+  uint8_t* h = (uint8_t*)S->arena.p + q->aoff;
   q->sp.gid.resize(n);
   q->rlen.resize(n);
   q->roff.resize(n);
@@ -519,30 +558,10 @@ int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_p
     if (pad) memset(h + rel[r] + len, 0, pad);
     q->sp.gid[r] = r;
     q->rlen[r] = (uint32_t)len;
+    q->roff[r] = q->aoff + rel[r];
     q->sp.max_len = std::max(q->sp.max_len, q->rlen[r]);
     q->sp.work += len;
   }
-  memset(h + total - 64, 0, 64);
-  {
-    std::unique_lock<std::mutex> lk(S->mu);
-    if (total > S->arena.cap / 4) {
-      lk.unlock();
-      return fallback(S, sides, cfg, p, out);
-    }
-    S->cv_arena.wait(lk, [&] { return S->failed || arena_alloc(S, total, q->aoff); });
-    if (S->failed) {
-      lk.unlock();
-      return fallback(S, sides, cfg, p, out);
-    }
-  }
-  if (hipMemcpyAsync((uint8_t*)S->arena.p + q->aoff, h, total, hipMemcpyHostToDevice, ts.stream) != hipSuccess ||
-      hipStreamSynchronize(ts.stream) != hipSuccess) {
-    std::lock_guard<std::mutex> g(S->mu);
-    S->live.erase(q->aoff);
-    S->cv_arena.notify_all();
-    return fallback(S, sides, cfg, p, out);
-  }
-  for (uint32_t r = 0; r < n; ++r) q->roff[r] = q->aoff + rel[r];
   {
     std::unique_lock<std::mutex> lk(S->mu);
     S->ready.push_back(q.get());
@@ -550,7 +569,13 @@ int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_p
     q->cv.wait(lk, [&] { return q->done; });
     if (q->st != ~0u && !(q->st & ST_RETRY)) S->stats.served++;
   }
-  if (q->st == ~0u || (q->st & ST_RETRY)) return fallback(S, sides, cfg, p, out);
+  if (q->st == ~0u || (q->st & ST_RETRY)) {
+    {
+      std::lock_guard<std::mutex> g(S->mu);
+      if (q->st != ~0u) S->stats.retried++;
+    }
+    return fallback(S, sides, cfg, p, out);
+  }
   std::unique_ptr<wc_results> R(new wc_results());
   R->kind = sides == 1 ? 0 : 1;
   R->probs.resize(1);
@@ -571,10 +596,14 @@ int wc_service_create(int device, uint64_t arena_bytes, wc_service** out) {
   S->device = device;
   int rc = wc_ctx_create(device, &S->ctx);
   if (rc != WC_OK) return rc;
-  if (!S->arena.ensure(arena_bytes ? arena_bytes : kArenaDefault)) {
+  void* dev = nullptr;
+  if (!S->arena.ensure(arena_bytes ? arena_bytes : kArenaDefault, true) ||
+      hipHostGetDevicePointer(&dev, S->arena.p, 0) != hipSuccess) {
+    S->arena.release();
     wc_ctx_destroy(S->ctx);
     return WC_E_HIP;
   }
+  S->arena_dev = (const uint8_t*)dev;
   S->th = std::thread(service_loop, S.get());
   *out = S.release();
   return WC_OK;
