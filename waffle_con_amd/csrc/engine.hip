@@ -52,6 +52,10 @@ namespace WC_ENGINE_NS {
 // with a wrong high dword; WC_FAULT_LOG) on inputs the 2- and 4-wave builds of
 // the same source and the bounds-checked 3-wave build run bit-exact (DESIGN.md
 // "3-wave dual builds")
+#if !defined(WC_DUAL_WAVES_PER_EU) && defined(WC_WIDE_DUAL_WPE) && !defined(WC_NARROW) && \
+    !defined(WC_GLOBAL_STATE) && !defined(WC_LOWLAT)
+#define WC_DUAL_WAVES_PER_EU WC_WIDE_DUAL_WPE  // variant builds (tools/gpu.sh w3)
+#endif
 #ifndef WC_DUAL_WAVES_PER_EU
 #define WC_DUAL_WAVES_PER_EU WC_WAVES_PER_EU
 #endif
@@ -449,11 +453,13 @@ struct Eng {
 // workgroup-uniform, so each 32-bit word goes through readfirstlane.
 __device__ inline Eng eng_uniform(const Eng& s) {
   static_assert(sizeof(Eng) % 4 == 0, "Eng is copied as words");
-  Eng d;
-  const uint32_t* sp = reinterpret_cast<const uint32_t*>(&s);
-  uint32_t* dp = reinterpret_cast<uint32_t*>(&d);
+  // words through memcpy (no type-punned access to the pointer fields)
+  uint32_t w[sizeof(Eng) / 4];
+  __builtin_memcpy(w, &s, sizeof(Eng));
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(Eng) / 4); ++i) dp[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sp[i]);
+  for (int i = 0; i < (int)(sizeof(Eng) / 4); ++i) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[i]);
+  Eng d;
+  __builtin_memcpy(&d, w, sizeof(Eng));
   return d;
 }
 
@@ -501,12 +507,12 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
 // repoints the read table at the copies (offsets from A.rbytes = the
 // workspace base). Every chunk is a 16-byte load; each thread keeps four in
 // flight, so a locus costs a few PCIe round trips rather than one per chunk.
-__device__ __noinline__ void stage_reads(const EngineArgs& A, Eng& E, uint32_t n) {
+// Out of line and with scalar arguments only: a reference to the engine
+// context or the kernel arguments would escape and move them to scratch.
+__device__ __noinline__ void stage_reads(const uint8_t* hreads, Gm<uint64_t>* lroff, const Gm<uint32_t>* lrlen,
+                                         Gm<uint8_t>* stage, uint64_t stride, uint64_t rel, uint32_t n) {
   const int tid = threadIdx.x;
-  Gm<uint64_t>* lroff = (Gm<uint64_t>*)E.roff;
-  const Gm<uint32_t>* lrlen = E.rlenp;
-  Gm<uint8_t>* stage = (Gm<uint8_t>*)E.roff + rtab_bytes(A.nmax);
-  const uint32_t cps = (uint32_t)(A.rstage_stride / 16);
+  const uint32_t cps = (uint32_t)(stride / 16);
   const uint32_t total = n * cps;
   constexpr uint32_t kU = 4;
   for (uint32_t g0 = tid; g0 < total; g0 += kEB * kU) {
@@ -517,7 +523,7 @@ __device__ __noinline__ void stage_reads(const EngineArgs& A, Eng& E, uint32_t n
       v[u] = make_uint4(0, 0, 0, 0);
       if (g < total) {
         const uint32_t r = g / cps, c = g - r * cps;
-        if (c * 16 < lrlen[r]) v[u] = *(const Gm<uint4>*)((const Gm<uint8_t>*)A.hreads + lroff[r] + (uint64_t)c * 16);
+        if (c * 16 < lrlen[r]) v[u] = *(const Gm<uint4>*)((const Gm<uint8_t>*)hreads + lroff[r] + (uint64_t)c * 16);
       }
     }
 #pragma unroll
@@ -525,13 +531,12 @@ __device__ __noinline__ void stage_reads(const EngineArgs& A, Eng& E, uint32_t n
       const uint32_t g = g0 + u * kEB;
       if (g < total) {
         const uint32_t r = g / cps, c = g - r * cps;
-        *(Gm<uint4>*)(stage + (uint64_t)r * A.rstage_stride + (uint64_t)c * 16) = v[u];
+        *(Gm<uint4>*)(stage + (uint64_t)r * stride + (uint64_t)c * 16) = v[u];
       }
     }
   }
   __syncthreads();
-  const uint64_t rel = (uint64_t)(stage - (const Gm<uint8_t>*)A.rbytes);
-  for (uint32_t r = tid; r < n; r += kEB) lroff[r] = rel + (uint64_t)r * A.rstage_stride;
+  for (uint32_t r = tid; r < n; r += kEB) lroff[r] = rel + (uint64_t)r * stride;
   __syncthreads();
 }
 
@@ -631,7 +636,11 @@ __device__ inline uint32_t claim_problem(const EngineArgs& A, Lo<Ctl>& ctl, Eng&
   P.read_begin = 0;
   E.P = P;
   __syncthreads();
-  if (A.hreads) stage_reads(A, E, P.n_reads);
+  if (A.hreads) {
+    Gm<uint8_t>* stage = (Gm<uint8_t>*)lroff + rtab_bytes(A.nmax);
+    stage_reads((const uint8_t*)A.hreads, lroff, lrlen, stage, A.rstage_stride,
+                (uint64_t)(stage - (const Gm<uint8_t>*)A.rbytes), P.n_reads);
+  }
   return seq;
 }
 
