@@ -963,6 +963,9 @@ static uint64_t fx_hash_opt(int64_t v) {
 }
 
 std::vector<int64_t> seed_group_order(const std::vector<int64_t>& groups) {
+  // PARITY UNPINNED: no reference fixture observes this order. It restates
+  // hashbrown on x86_64 with SSE2 (probe group width 16; NEON/generic builds
+  // of the reference use 8 and would iterate differently).
   // hashbrown table of Option<usize> keys (16-B entries): same placement rules as
   // FxByteMap but with a 64-bit hash
   // built by `.collect()` (priority_consensus.rs:180): hashbrown's extend

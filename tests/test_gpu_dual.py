@@ -133,3 +133,50 @@ def test_alphabet_limit_is_a_clear_error():
     with pytest.raises(w.WaffleConError) as e:
         hip.consensus(reads, min_count=1)
     assert e.value.code == 11 and "limit" in str(e.value)
+
+
+DUAL_KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
+             "nodes_ignored", "peak_queue_size", "row_bytes")
+
+
+def _dual_inputs(kind, seed):
+    import waffle_con_amd as w
+    from waffle_con_amd import synth
+    if kind == "split":  # two haplotypes: single-consensus chains, then dual nodes
+        return synth.cfg3_locus(seed, length=700, reads=12, err=0.01), {}
+    if kind == "mono":  # one haplotype: the search stays single-consensus (long chains)
+        return w.generate_test(4, 900, 20, 0.01, seed)[1], dict(min_count=4)
+    if kind == "queue":  # a small queue limit: the PQueueTracker threshold moves inside chains
+        return synth.cfg3_locus(seed, length=500, reads=10, err=0.02), dict(max_queue_size=3)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("chain", ["0", "2", "7", "16", "40"])
+@pytest.mark.parametrize("kind,seed", [("split", 1), ("mono", 2), ("queue", 3)])
+def test_dual_chain_length_invariance(chain, kind, seed, monkeypatch):
+    """The dual engine's linear-chain run-ahead over single-consensus nodes
+    (WC_DUAL_CHAIN = max steps, 0 = off) changes neither results nor any work
+    counter: every length is bit-exact vs the oracle (per-call launches, so
+    each call plans its own chain length)."""
+    monkeypatch.setenv("WAFFLE_CON_SERVICE", "0")
+    monkeypatch.setenv("WC_DUAL_CHAIN", chain)
+    seqs, cfg = _dual_inputs(kind, seed)
+    exp, ec = orc.dual_consensus(seqs, counters=True, **cfg)
+    got, gc = hip.dual_consensus(seqs, counters=True, **cfg)
+    assert got == exp
+    for k in DUAL_KEYS:
+        assert gc[k] == ec[k], (k, gc[k], ec[k])
+
+
+@pytest.mark.parametrize("chain", ["0", "16"])
+def test_priority_chain_invariance(chain, monkeypatch):
+    """PriorityConsensusDWFA sub-problems (stream mode) with and without dual chains."""
+    from waffle_con_amd import synth
+    monkeypatch.setenv("WAFFLE_CON_SERVICE", "0")
+    monkeypatch.setenv("WC_DUAL_CHAIN", chain)
+    chains = synth.cfg5_locus(11)
+    exp, ec = orc.priority_consensus(chains, counters=True, wildcard=ord("*"))
+    got, gc = hip.priority_consensus(chains, counters=True, wildcard=ord("*"))
+    assert got == exp
+    for k in DUAL_KEYS:
+        assert gc[k] == ec[k], (k, gc[k], ec[k])

@@ -91,7 +91,11 @@ class _Owned:
 def _single_results(res, n, cost, L, return_errors):
     """Per problem: a list of Consensus, or its WaffleConError. The results
     stay in the library's arenas (wc_results_single_view, no copy); takes
-    ownership of `res` (freed when no Consensus refers to it any more)."""
+    ownership of `res` (freed when no Consensus refers to it any more).
+    Retention: one surviving Consensus that was never read keeps the whole
+    result set (every problem's arenas) alive; reading it (sequence(),
+    scores(), pickling) unpacks it into plain values and drops the reference.
+    A caller that keeps a few results of many batches should read them."""
     owner = _Owned(res)
     u64 = ctypes.c_uint64
     nr, sb, ns = u64(), u64(), u64()

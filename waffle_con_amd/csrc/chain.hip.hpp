@@ -408,7 +408,10 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
 #ifdef WC_NO_FF
   const bool ffon = false;
 #else
-  const bool ffon = wc < 0;  // a wildcard read byte matches but nominates itself: no quiet runs
+  // (a wildcard read byte matches any push but nominates itself; it never
+  // equals another prediction byte, so the byte compare ends a run there and
+  // the step path takes it)
+  const bool ffon = true;
 #endif
   for (uint32_t j = 1; j <= K; ++j) {
     const uint32_t stopv =
@@ -572,18 +575,22 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
       const uint32_t pred = nsym;
       uint32_t vp = 0, vo = 0;
       bool frac = false;
+      // (votes for the wildcard symbol count in neither: chain_votes)
+      const uint32_t wsym = wc >= 0 ? (uint32_t)(uint8_t)wc : 0x100u;
       if (active && o.n > 0) {
         if (o.n == 1) {
-          if ((uint32_t)(o.sym & 0xFF) == pred) vp = kVoteDen;
-          else vo = kVoteDen;
+          const uint32_t s0 = (uint32_t)(o.sym & 0xFF);
+          if (s0 == pred) vp = kVoteDen;
+          else if (s0 != wsym) vo = kVoteDen;
         } else {
           const uint32_t unit = vote_unit(o.split);
           for (uint32_t k = 0; k < o.n; ++k) {
             const uint32_t c = unit * (uint32_t)((o.occ >> (8 * k)) & 0xFF);
-            if ((uint32_t)((o.sym >> (8 * k)) & 0xFF) == pred) {
+            const uint32_t sk = (uint32_t)((o.sym >> (8 * k)) & 0xFF);
+            if (sk == pred) {
               vp += c;
               frac = true;
-            } else {
+            } else if (sk != wsym) {
               vo += c;
             }
           }
@@ -635,10 +642,10 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
 }
 
 // (D) per chain node N_j, j < K: ok[j] = exactly one passing candidate and it
-// is the predicted symbol j+1 (consensus.rs:283-321). Without a wildcard the
-// walk's exact rational vote totals (prediction vs everything else) decide
-// almost every step; the rest take the exact path (per-key f64 sums in read
-// order, hashbrown key order).
+// is the predicted symbol j+1 (consensus.rs:283-321). Unless the wildcard is
+// predicted, the walk's exact rational vote totals (prediction vs every other
+// non-wildcard symbol) decide almost every step; the rest take the exact path
+// (per-key f64 sums in read order, hashbrown key order).
 __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t K) {
   const int lane = lane_id();
   const DevConfig& cfg = E.cfg;
@@ -653,7 +660,10 @@ __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t K) {
     // differ from them by far less than 1/840, so strict inequalities carry
     // over. Only exact ties with fractional terms need the f64 path.
     int dec = -1;  // 1 ok, 0 not ok, -1 undecided
-    if (cfg.wildcard < 0) {
+    // With a wildcard (not predicted here), its votes are left out of O: any
+    // other key present drops it from the candidates (consensus.rs:556-561),
+    // and P > 0 is one.
+    if (cfg.wildcard < 0 || (uint32_t)E.L.cpred[j + 1] != (uint32_t)(uint8_t)cfg.wildcard) {
       if (P == 0) dec = 0;  // the prediction is not a candidate
       else if (O < P && O < M) {
         // thr = min(min_count, max) and max = P when P < M: the prediction
@@ -685,38 +695,48 @@ __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t K) {
 }
 
 // (E) wave 0: replay the pops of N_1.. on the scalar search state
-// (consensus.rs:224-251 with the queue holding only the chain node) and
-// commit the accepted prefix. Returns j* = number of chain nodes generated.
-// The step-local tests (max_err, capacity, reached_end, one passing candidate)
-// are evaluated by lanes over j at once; only the PQueueTracker threshold walk
-// is sequential, on registers.
+// (consensus.rs:224-251 / dual_consensus.rs:340-397) and commit the accepted
+// prefix. Returns j* = number of chain nodes generated. The step-local tests
+// (max_err, capacity, reached_end, one passing candidate, and N_j popping
+// next: strictly above the best other queued node, whatever the heap's tie
+// order) are evaluated by lanes over j at once; only the PQueueTracker
+// threshold walk is sequential, on registers. Other queued nodes of the
+// tracker count in its total: when the threshold passes a length, their
+// count there (HBM) leaves the total, as increment_threshold does. A dual
+// search's consensus-2 tracker does not change during a chain of
+// single-consensus nodes (its loop at N_0's pop already left it stable).
 __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint32_t Keff) {
   const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
   const uint32_t lane = (uint32_t)lane_id();
+  const Gm<uint32_t>* lc = E.trk;  // PQueueTracker length counts of the queued nodes
   Gm<uint32_t>* pc = E.trk + (E.lcap + 2);
   const uint32_t jl = 1 + lane;  // Keff <= kChainMax < 64: one step per lane
+  const uint32_t hn = ctl.heap_n;  // other queued nodes (N_0 is popped)
   bool bad = true;
   if (jl < Keff) {
     const auto& st = E.L.cstep[jl];
     const uint32_t n_end = step_nend(st.ef);
     const bool reached = early ? (n_end == E.n) : (n_end > 0);
     bad = st.cost > ctl.max_err || (uint64_t)E.L.cpc[jl] >= cfg.max_capacity_per_size || reached || !st.ok;
+    if (hn > 0) bad |= !prio_less(E.L.heap[0], HeapEntry{st.cost, L0 + jl, 0u});
   }
   const uint32_t jbad = 1 + (uint32_t)__builtin_ctzll(ballot(bad));  // lane 63 is always bad
   uint32_t jstar = Keff >= 1 ? 1u : 0u;
   uint64_t thr = ctl.trk_thr[0], farthest = ctl.farthest[0], lcnst = ctl.last_constraint[0];
+  uint64_t others = ctl.trk_total[0];
   for (uint32_t j = 1; j < Keff && j < jbad; ++j) {
     const uint64_t L = L0 + j;
-    uint64_t t_thr = thr, t_l = lcnst;
-    uint64_t total = L >= t_thr ? 1u : 0u;  // the queue holds N_j only
-    while ((total > cfg.max_queue_size || t_l >= cfg.max_nodes_wo_constraint) && t_thr < farthest) {
-      if (t_thr == L) total--;
+    uint64_t t_thr = thr, t_l = lcnst, t_oth = others;
+    while ((t_oth + (L >= t_thr ? 1u : 0u) > cfg.max_queue_size || t_l >= cfg.max_nodes_wo_constraint) &&
+           t_thr < farthest) {
+      if (t_oth) t_oth -= trk_load(&lc[t_thr]);
       t_thr++;
       t_l = 0;
     }
     if (L < t_thr) break;
     thr = t_thr;
+    others = t_oth;
     lcnst = t_l + 1;
     farthest = max(farthest, L);
     jstar = j + 1;
@@ -724,12 +744,13 @@ __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint3
   if (jl < jstar) pc[L0 + jl] = E.L.cpc[jl] + 1;
   if (lane == 0) {
     ctl.trk_thr[0] = thr;
+    ctl.trk_total[0] = others;
     ctl.farthest[0] = farthest;
     ctl.last_constraint[0] = lcnst;
     if (jstar > 1) {
       ctl.cnt[S_POPS] += jstar - 1;
       ctl.cnt[S_EXPLORED] += jstar - 1;
-      ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)1);
+      ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)hn + 1);
     }
   }
   return jstar;
@@ -737,12 +758,17 @@ __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint3
 
 // Not inlined: the chain has its own register allocation (no spills in the
 // walk); the caller saves its live registers once per chain.
-// Run one chain from the popped node `top` (length L0, hot in LDS, queue
-// otherwise empty) whose single child symbol is s1. Returns j* (uniform); for
-// j* > 0 the chain node N_j* is in slot `top`/LDS, queued, with its
-// nominations cached; j* == 0 leaves everything as it was.
-__device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
-  Eng E = eng_uniform(Eref);  // scalar-register copy of the caller's context
+// Run one chain from the popped node `top` (length L0, hot in LDS) whose
+// single child symbol is s1. Returns j* (uniform); for j* > 0 the chain node
+// N_j* is in slot `top`/LDS, queued, with its nominations cached; j* == 0
+// leaves everything as it was. kDual: `top` is a single-consensus node of a
+// DualConsensusDWFA search (its stay-single children, dual_consensus.rs:
+// 655-679); the virtual pops also grow the active-read minimum per length
+// (:497-513).
+template <bool kDual>
+__device__ __noinline__ uint32_t run_chain(DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top, uint32_t L0,
+                                           int s1) {
+  Eng E = callee_eng(P, sbase);  // scalar registers
   const int tid = threadIdx.x;
   if (tid == 0) {
     const uint32_t K = min(E.chain, E.lcap - L0);
@@ -853,6 +879,27 @@ __device__ __noinline__ uint32_t run_chain(Eng& Eref, Lo<Ctl>& ctl, uint32_t top
     ctl.ph[15] += 1ull + ((jstar == K && Keff == K) ? (1ull << 20) : 0ull) + ((uint64_t)jstar << 40);
 #endif
     E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = S;
+    // the queue as the literal pops leave it: each N_j (j < j*) was pushed,
+    // then popped as the maximum, which moves the other entries along its
+    // path (their tie order depends on the layout)
+    if (ctl.heap_n > 1)
+      for (uint32_t j = 1; j < jstar; ++j) {
+        heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{E.L.cstep[j].cost, L0 + j, top});
+        (void)heap_pop(E.L.heap, ctl.heap_n, E.pcap);
+      }
+    if (kDual) {
+      // every explored N_j (j < j*) extends the per-length active counts
+      // (no read activates past the last activation point)
+      for (uint32_t j = 1; j < jstar; ++j) {
+        const uint32_t tl = L0 + j;
+        if (ctl.am_len == tl + 1 && tl + 1 < E.lcap + 2) {
+          const uint32_t nt = E.total_active[tl];
+          E.total_active[tl + 1] = nt;
+          E.active_min[tl + 1] = (uint32_t)max(E.cfg.min_count, ceil_u64(E.cfg.min_af * (double)nt));
+          ctl.am_len++;
+        }
+      }
+    }
     if (jstar > 0) {
       const auto& st = E.L.cstep[jstar];
       const uint32_t clen = L0 + jstar;

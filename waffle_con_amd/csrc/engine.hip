@@ -196,7 +196,7 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
   Lds l;
   Sh<uint8_t>* p = smem;
   l.hot = (Sh<RState>*)p;
-  p += (uint64_t)hot_sides(sides) * nmax * sizeof(RState);
+  p += (uint64_t)hot_sides(sides, K) * nmax * sizeof(RState);
   l.cstep = (Sh<ChainStep>*)p;
   l.covf = nullptr;
   l.ctmp = nullptr;
@@ -206,21 +206,24 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
   l.cpc = nullptr;
   l.cpred = nullptr;
   if (K) {
-    p += align16((uint64_t)(K + 1) * sizeof(ChainStep));
+    // (engine_shared chain_lds_bytes; side s of a per-side array at s * its
+    // one-side size, the dual chain's steps are DualSteps)
+    const uint64_t S = chain_sides(sides);
+    p += align16((uint64_t)(K + 1) * (S == 2 ? sizeof(DualStep) : sizeof(ChainStep)));
     l.covf = (Sh<ChainOvf>*)p;
     p += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
     l.ctmp = (Sh<RState>*)p;
-    p += (uint64_t)kEW * 64;
+    p += (uint64_t)kWaves * 64;
     l.cnom = (Sh<uint16_t>*)p;
-    p += align16((uint64_t)(K + 1) * nmax * 2);
+    p += align16(S * (K + 1) * nmax * 2);
     l.cwin = p;
-    p += align16((uint64_t)4 * win_m4(nmax) * kWinStride);
+    p += align16(S * 4 * win_m4(nmax) * kWinStride);
     l.cwb = (Sh<uint32_t>*)p;
-    p += align16((uint64_t)nmax * 4);
+    p += align16(S * nmax * 4);
     l.cpc = (Sh<uint32_t>*)p;
     p += align16((uint64_t)(K + 1) * 4);
     l.cpred = p;
-    p += align16((uint64_t)(K + 2));
+    p += align16(S * (K + 2));
   }
   l.heap = (Sh<HeapEntry>*)p;
   p += (uint64_t)pcap * sizeof(HeapEntry);
@@ -499,6 +502,18 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
     E.rlenp = (const Gm<uint32_t>*)(t + 2 * align16((uint64_t)A.nmax * 8));
   }
   return E;
+}
+
+// The engine context inside an out-of-line phase (the chain walks): rebuilt
+// from the kernel arguments (kernarg segment) and the claimed problem, so the
+// kernel's own context never has its address taken (that would move it, with
+// every pointer in it, to scratch memory for the whole kernel).
+__device__ inline Eng callee_eng(const DevProblem& P, Sh<uint8_t>* sbase) {
+  const EngineArgs& A = *(const EngineArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  Eng E = make_eng(A, sbase);
+  E.P = P;
+  E.n = P.n_reads;
+  return eng_uniform(E);
 }
 
 // ---- host-resident reads (service lanes, EngineArgs::hreads) ----
@@ -1368,6 +1383,7 @@ WC_PHASE_FN bool wave_votes(Lo<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, co
 }
 
 #include "chain.hip.hpp"
+#include "dual_chain.hip.hpp"
 
 // ---- write one result record (finalized node) ----
 WC_PHASE_FN void store_record(Eng& E, Lo<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t slot, uint32_t nsides,
@@ -1928,7 +1944,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
       // ---- one child and nothing else queued: linear-chain run-ahead ----
       // (past the last activation point every read of this lineage is active)
       if (nc == 1 && A.chain && uni(ctl.heap_n) == 0 && (E.P.n_active == E.n || len >= E.P.max_act)) {
-        const uint32_t jstar = run_chain(E, ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
+        const uint32_t jstar = run_chain<false>(E.P, state_base(A, smem), ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
         PH_MARK(14);
         if (jstar) continue;
       }
@@ -2286,6 +2302,30 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
         if (tid == 0) ctl.status = ST_RETRY | ST_RETRY_LCAP;
         __syncthreads();
         break;
+      }
+
+      // ---- one child: linear-chain run-ahead (chain.hip.hpp, dual_chain.hip.hpp) ----
+      // Past the last activation point. A single-consensus node's stay-single
+      // child: the single engine's walk; a dual node's child: the two-sided
+      // walk (unweighted votes; a walking side must be the longer one, so the
+      // max length grows with every step).
+      if (E.chain && nc == 1 && (E.P.n_active == E.n || tlen >= E.P.max_act)) {
+        const int x0 = uni((int32_t)ctl.ch_s[0][0]), x1 = uni((int32_t)ctl.ch_s[0][1]);
+        uint32_t kind = 0, walk = 0;
+        if (!tdual) {
+          if (uni((uint32_t)ctl.ch_kind[0]) == 1) kind = 1;
+        } else if (!weighted) {
+          walk = (x0 >= 0 ? 1u : 0u) | (x1 >= 0 ? 2u : 0u);
+          const uint32_t L0 = max(tlens[0], tlens[1]);
+          if (((walk & 1u) && tlens[0] == L0) || ((walk & 2u) && tlens[1] == L0)) kind = 2;
+        }
+        if (kind) {
+          const uint32_t flags = tm.flags | (x0 < 0 ? 2u : 0u) | (x1 < 0 ? 4u : 0u);
+          const uint32_t jstar = run_engine_chain(E.P, state_base(A, smem), ctl, top, kind, tlens[0], tlens[1], walk,
+                                                  (uint32_t)max(x0, 0), (uint32_t)max(x1, 0), flags);
+          PH_MARK(14);
+          if (jstar) continue;
+        }
       }
 
       // ---- build every child: clones first, the last child in place ----

@@ -68,11 +68,16 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   const uint32_t ecap = std::max<uint32_t>(31, maxlen / 64);
   c.wcap = (((2 * ecap + 1 + 63) / 64) * 64) << wx;
   c.lcap = (((maxlen + maxlen / 8 + 64 + 15) / 16) * 16) << lx;
-  // single engine: linear-chain run-ahead length (WC_CHAIN=<k> overrides, 0 = off)
-  uint32_t chain = (sides == 1 && nmax <= (uint32_t)kBlock) ? kChainDefault : 0;
-  const char* chain_env = getenv("WC_CHAIN");
-  if (chain_env) chain = std::min<uint32_t>((uint32_t)atoi(chain_env), kChainMax);
-  if (sides != 1 || nmax > (uint32_t)kBlock) chain = 0;
+  // linear-chain run-ahead length (WC_CHAIN=<k> overrides, 0 = off). The dual
+  // engine runs chains from single-consensus nodes (WC_DUAL_CHAIN=<k>, 0 =
+  // off) when min_af is 0: its child threshold is then the single engine's
+  // (dual_consensus.rs:655-679 with min_count = cfg.min_count)
+  uint32_t chain = 0;
+  const char* chain_env = getenv(sides == 1 ? "WC_CHAIN" : "WC_DUAL_CHAIN");
+  if (nmax <= (uint32_t)kBlock && (sides == 1 || cfg.min_af == 0.0)) {
+    chain = sides == 1 ? kChainDefault : kDualChainDefault;
+    if (chain_env) chain = std::min<uint32_t>((uint32_t)atoi(chain_env), kChainMax);
+  }
   // node pool. A dual search keeps far more nodes queued than a single one
   // (children of both consensuses, both sides' DWFAs per node: cfg3 loci peak
   // at ~480 queued nodes), so the dual pool gets the launch's HBM share over
@@ -87,10 +92,25 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
     if (sides == 2) lmax = (uint64_t)atoi(e) * 1024;
   // WC_GSTATE=1 (test hook) forces the global-state build for every launch
   bool gstate = getenv("WC_GSTATE") != nullptr;
-  uint32_t pcap = 16;
-  while (pcap < pmax && (uint64_t)(pcap * 2) * sb <= budget &&
-         (gstate || lds_bytes(sides, pcap * 2, nmax, chain) <= lmax))
-    pcap *= 2;
+  auto base_pool = [&]() {
+    uint32_t p = 16;
+    while (p < pmax && (uint64_t)(p * 2) * sb <= budget && (gstate || lds_bytes(sides, p * 2, nmax, chain) <= lmax))
+      p *= 2;
+    return p;
+  };
+  // the dual engine's chain area (both sides' windows, nominations and hot
+  // RStates) comes out of the node pool's LDS: a launch with chains gets its
+  // own LDS budget (WC_DUAL_CHAIN_LDS_KB) and keeps them while the pool
+  // still has 128 slots (a pool that outgrows it retries larger, as always)
+  const uint64_t lmax0 = lmax;
+  if (sides == 2 && chain > 0 && !gstate)
+    if (const char* e = getenv("WC_DUAL_CHAIN_LDS_KB")) lmax = (uint64_t)atoi(e) * 1024;
+  uint32_t pcap = base_pool();
+  if (sides == 2 && chain > 0 && !gstate && pcap < 128) {
+    chain = 0;
+    lmax = lmax0;
+    pcap = base_pool();
+  }
   // a retried (pool-exhausted) item gets 4x per retry, as HBM allows; past
   // what LDS holds, the search state moves to HBM
   c.pool_short = false;
@@ -103,6 +123,7 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
     pcap = np;
   }
   if (lds_bytes(sides, pcap, nmax, chain) > kLdsMax) gstate = true;
+  if (gstate && sides == 2) chain = 0;  // the global-state dual build runs no chains
   // 128-thread workgroups for problems of <= 128 reads (engine_narrow.hip):
   // for the dual engine (WC_NARROW: bit 0 single engine, bit 1 dual engine;
   // default 2). The single engine's chain walk is faster with 4 waves of
@@ -121,7 +142,7 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   // longer chains amortise the per-chain work (prediction, acceptance, the
   // literal pop between chains); take the longest one whose LDS still gives
   // the workgroups per CU of the default length (results do not depend on it)
-  if (!chain_env && chain > 0 && !gstate) {
+  if (sides == 1 && !chain_env && chain > 0 && !gstate) {
     const int occ = occupancy((size_t)lds_bytes(sides, pcap, nmax, chain));
     for (uint32_t k = chain + 1; k <= kChainMax; ++k) {
       const uint64_t l = lds_bytes(sides, pcap, nmax, k);
@@ -597,7 +618,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.lcap = caps.lcap;
   a.nmax = caps.nmax;
   a.rmax = caps.rmax;
-  a.chain = 0;
+  a.chain = caps.chain;  // the device carves LDS from it: must match caps.lds
   a.out = dh + L.off_out;
   a.out_stride = caps.ob;
   a.status = (uint32_t*)(dh + L.off_status);

@@ -211,6 +211,7 @@ struct RInfo {
 // ---- linear-chain run-ahead (single engine, engine.hip run_chain) ----
 constexpr uint32_t kChainMax = 40;      // steps per chain (upper bound; WC_CHAIN); longer chains outrun the 64-B read windows
 constexpr uint32_t kChainDefault = 16;  // steps per chain by default
+constexpr uint32_t kDualChainDefault = 16;  // dual engine (single-consensus nodes): steps per chain
 constexpr uint32_t kChainOvf = 192;  // multi-symbol nominations stored per chain
 static_assert(kChainOvf <= 256, "ChainOvf index is the low byte of a u16 nomination code");
 struct ChainStep {  // aggregates of one speculative step (node N_j), LDS atomics (one per wave)
@@ -235,18 +236,30 @@ struct ChainOvf {  // nominations of a read with >= 2 distinct tip symbols
 constexpr uint32_t kWinStride = 68;
 __host__ __device__ inline uint32_t win_m4(uint32_t nmax) { return (nmax + 3) / 4; }
 __host__ __device__ inline uint32_t win_slot(uint32_t r, uint32_t m4) { return (r & 3u) * m4 + (r >> 2); }
-// chain LDS: steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[K+1][nmax] u16 |
-//            win[4*m4][68 B] (read windows) | wb[nmax] u32 | pc[K+1] u32 | pred[K+2] u8
-__host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K) {
+// aggregates of one speculative step of the dual-node chain (dual_chain.hip.hpp)
+struct DualStep {
+  uint64_t cost;   // sum over reads of the cheaper side's cost
+  uint64_t po[2];  // per side: ChainStep::po
+  uint64_t ef[2];  // per side: ChainStep::ef
+  uint32_t some;   // Some(dwfa) side 1 [0,10) | side 2 [10,20) | reads at the end of either side [20,30)
+  uint32_t ok;
+};
+static_assert(sizeof(DualStep) == 48, "DualStep layout");
+__host__ __device__ inline uint32_t chain_sides(uint32_t sides) { return sides == 2 ? 2u : 1u; }
+// chain LDS (per side S = chain_sides: the dual engine's chains walk both):
+//   steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[S][K+1][nmax] u16 |
+//   win[S][4*m4][68 B] (read windows) | wb[S][nmax] u32 | pc[K+1] u32 | pred[S][K+2] u8
+__host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K, uint32_t sides = 1) {
   if (K == 0) return 0;
-  uint64_t t = align16((uint64_t)(K + 1) * sizeof(ChainStep));
+  const uint64_t S = chain_sides(sides);
+  uint64_t t = align16((uint64_t)(K + 1) * (S == 2 ? sizeof(DualStep) : sizeof(ChainStep)));
   t += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
   t += (uint64_t)kWaves * 64;
-  t += align16((uint64_t)(K + 1) * nmax * 2);
-  t += align16((uint64_t)4 * win_m4(nmax) * kWinStride);
-  t += align16((uint64_t)nmax * 4);
+  t += align16(S * (K + 1) * nmax * 2);
+  t += align16(S * 4 * win_m4(nmax) * kWinStride);
+  t += align16(S * nmax * 4);
   t += align16((uint64_t)(K + 1) * 4);
-  t += align16((uint64_t)(K + 2));
+  t += align16(S * (K + 2));
   return t;
 }
 
@@ -257,13 +270,17 @@ constexpr uint32_t kDualChildBatch = 4;
 __host__ __device__ inline uint64_t list_entries(uint32_t sides, uint32_t nmax) {
   return (uint64_t)(sides == 2 ? 8 : 2) * nmax;
 }
-// sides whose expanded node's RStates are held in LDS (single engine only)
-__host__ __device__ inline uint32_t hot_sides(uint32_t sides) { return sides == 1 ? 1u : 0u; }
+// sides whose expanded node's RStates are held in LDS: the single engine's
+// popped node; in the dual engine side 1 of a single-consensus node for its
+// chain walk (chain > 0; the two-sided walk reads the slot)
+__host__ __device__ inline uint32_t hot_sides(uint32_t sides, uint32_t chain) {
+  return (sides == 1 || chain > 0) ? 1u : 0u;
+}
 // LDS: hot RStates[hot_sides][nmax] | chain area | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
 //      heavy list[list_entries] u32 | (dual) child e[kDualChildBatch][2][nmax] u16
 __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t chain) {
-  uint64_t t = (uint64_t)hot_sides(sides) * nmax * sizeof(RState);
-  t += chain_lds_bytes(nmax, chain);
+  uint64_t t = (uint64_t)hot_sides(sides, chain) * nmax * sizeof(RState);
+  t += chain_lds_bytes(nmax, chain, sides);
   t += (uint64_t)pcap * sizeof(HeapEntry);
   t += align16((uint64_t)pcap * 4);
   t += (uint64_t)pcap * sizeof(SlotMeta);
