@@ -609,6 +609,7 @@ class Cfg4(Cfg5):
         t0 = time.perf_counter()
         self.L = {0: [[r] for r in synth.cfg4_locus(4 + rank)]}
         self.static, self.tail, self.costs = [0], [], [1]
+        self.chunk = 0  # (rank_report: no shared queue for one locus)
         self.gen_s = time.perf_counter() - t0
         self.upload_s = 0.0
         self.last, self.mine, self.busy_s, self.static_s = {}, [], 0.0, 0.0

@@ -102,6 +102,12 @@ def main():
                 30: "votes-sums(w0)", 31: "active-min-growth(t0)", 22: "prune-setup(t0)", 23: "prune-loop(t0)",
                 24: "prune-atomics(t0)", 25: "prune-barrier1(t0)", 26: "prune-tail(t0)"}
         rep["dual_sub_per_pop"] = {DSUB[k]: round(cyc[k] / np_, 2) for k in DSUB if k < len(cyc)}
+        if len(cyc) >= 40:  # chain statistics per kind (engine.hip dual chain call site)
+            for kind, b in (("single_consensus_chains", 32), ("dual_chains", 35)):
+                n = max(1, cyc[b])
+                rep[kind] = {"attempts": cyc[b], "accepted_nodes": cyc[b + 1], "nodes_per_attempt": round(cyc[b + 1] / n, 2),
+                             "speculative_steps_per_attempt": round(cyc[b + 2] / n, 2),
+                             "cycles_per_attempt(t0)": round(cyc[b + 6 - (b - 32) // 3 * 2] / n, 1)}
         print(json.dumps(rep, indent=1))
         with open(os.path.join(a.out, "report.json"), "w") as f:
             json.dump(rep, f, indent=1)

@@ -766,12 +766,14 @@ __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint3
 // 655-679); the virtual pops also grow the active-read minimum per length
 // (:497-513).
 template <bool kDual>
-__device__ __noinline__ uint32_t run_chain(DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top, uint32_t L0,
-                                           int s1) {
-  Eng E = callee_eng(P, sbase);  // scalar registers
+__device__ __noinline__ uint32_t run_chain(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top,
+                                           uint32_t L0, int s1) {
+  Eng E = callee_eng(kp, P, sbase);  // scalar registers
   const int tid = threadIdx.x;
   if (tid == 0) {
-    const uint32_t K = min(E.chain, E.lcap - L0);
+    // (the dual engine's chains end at forks of its search more often: their
+    // length adapts, so a chain that ends early wastes few speculative steps)
+    const uint32_t K = min(kDual ? min(E.chain, ctl.chain_kcur) : E.chain, E.lcap - L0);
     ctl.chain_k = 0;
     if (K >= 2 && ctl.nfree > 0) {
       ctl.chain_k = K;
@@ -879,6 +881,7 @@ __device__ __noinline__ uint32_t run_chain(DevProblem P, Sh<uint8_t>* sbase, Lo<
     ctl.ph[15] += 1ull + ((jstar == K && Keff == K) ? (1ull << 20) : 0ull) + ((uint64_t)jstar << 40);
 #endif
     E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = S;
+    if (kDual) ctl.chain_kcur = (jstar == K && Keff == K) ? min(2 * K, E.chain) : max(4u, jstar + 1);
     // the queue as the literal pops leave it: each N_j (j < j*) was pushed,
     // then popped as the maximum, which moves the other entries along its
     // path (their tie order depends on the layout)
@@ -890,12 +893,17 @@ __device__ __noinline__ uint32_t run_chain(DevProblem P, Sh<uint8_t>* sbase, Lo<
     if (kDual) {
       // every explored N_j (j < j*) extends the per-length active counts
       // (no read activates past the last activation point)
+      // (one HBM load: the count repeats along the chain)
+      uint32_t nt = ~0u, amv = 0;
       for (uint32_t j = 1; j < jstar; ++j) {
         const uint32_t tl = L0 + j;
         if (ctl.am_len == tl + 1 && tl + 1 < E.lcap + 2) {
-          const uint32_t nt = E.total_active[tl];
+          if (nt == ~0u) {
+            nt = E.total_active[tl];
+            amv = (uint32_t)max(E.cfg.min_count, ceil_u64(E.cfg.min_af * (double)nt));
+          }
           E.total_active[tl + 1] = nt;
-          E.active_min[tl + 1] = (uint32_t)max(E.cfg.min_count, ceil_u64(E.cfg.min_af * (double)nt));
+          E.active_min[tl + 1] = amv;
           ctl.am_len++;
         }
       }

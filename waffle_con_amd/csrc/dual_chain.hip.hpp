@@ -488,16 +488,16 @@ __device__ inline uint32_t dual_chain_accept(Eng& E, Lo<Ctl>& ctl, const DualCha
 // whose only child pushes syms[s] on the sides in `walk` (the others stay
 // locked; `flags` = the child's flags). Returns j* (uniform): for j* > 0 the
 // node N_j* is in slot `top`, queued.
-__device__ __noinline__ uint32_t run_dual_chain(DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top,
+__device__ __noinline__ uint32_t run_dual_chain(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top,
                                                 uint32_t tl0, uint32_t tl1, uint32_t walk, uint32_t sym0, uint32_t sym1,
                                                 uint32_t flags) {
-  Eng E = callee_eng(P, sbase);
+  Eng E = callee_eng(kp, P, sbase);
   const int tid = threadIdx.x;
   const uint32_t l0[2] = {tl0, tl1};
   const uint32_t L0 = max(tl0, tl1);
   const DualChainArea A = dual_area(E);
   if (tid == 0) {
-    uint32_t K = min(E.chain, E.lcap - L0);
+    uint32_t K = min(min(E.chain, ctl.chain_kcur), E.lcap - L0);  // (adaptive, as in run_chain)
     ctl.chain_k = 0;
     if (K >= 2 && ctl.nfree > 0) {
       ctl.chain_k = K;
@@ -588,17 +588,22 @@ __device__ __noinline__ uint32_t run_dual_chain(DevProblem P, Sh<uint8_t>* sbase
       ctl.cnt[S_ROWB] += ctl.chain_tot[4];
     }
     E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = S;
+    ctl.chain_kcur = (jstar == K && Keff == K) ? min(2 * K, E.chain) : max(4u, jstar + 1);
     if (ctl.heap_n > 1)
       for (uint32_t j = 1; j < jstar; ++j) {
         heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{A.step[j].cost, L0 + j, top});
         (void)heap_pop(E.L.heap, ctl.heap_n, E.pcap);
       }
+    uint32_t nt = ~0u, amv = 0;  // (one HBM load: the count repeats along the chain)
     for (uint32_t j = 1; j < jstar; ++j) {
       const uint32_t tl = L0 + j;
       if (ctl.am_len == tl + 1 && tl + 1 < E.lcap + 2) {
-        const uint32_t nt = E.total_active[tl];
+        if (nt == ~0u) {
+          nt = E.total_active[tl];
+          amv = (uint32_t)max(E.cfg.min_count, ceil_u64(E.cfg.min_af * (double)nt));
+        }
         E.total_active[tl + 1] = nt;
-        E.active_min[tl + 1] = (uint32_t)max(E.cfg.min_count, ceil_u64(E.cfg.min_af * (double)nt));
+        E.active_min[tl + 1] = amv;
         ctl.am_len++;
       }
     }
@@ -624,14 +629,14 @@ __device__ __noinline__ uint32_t run_dual_chain(DevProblem P, Sh<uint8_t>* sbase
 // single-consensus walk of chain.hip.hpp on an LDS copy of side 1; kind 2: the
 // two-sided walk): one call site keeps the kernel's register allocation
 // around it small.
-__device__ __noinline__ uint32_t run_engine_chain(DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top,
-                                                  uint32_t kind, uint32_t tl0, uint32_t tl1, uint32_t walk,
-                                                  uint32_t sym0, uint32_t sym1, uint32_t flags) {
-  if (kind == 2) return run_dual_chain(P, sbase, ctl, top, tl0, tl1, walk, sym0, sym1, flags);
-  Eng E = callee_eng(P, sbase);
+__device__ __noinline__ uint32_t run_engine_chain(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl,
+                                                  uint32_t top, uint32_t kind, uint32_t tl0, uint32_t tl1,
+                                                  uint32_t walk, uint32_t sym0, uint32_t sym1, uint32_t flags) {
+  if (kind == 2) return run_dual_chain(kp, P, sbase, ctl, top, tl0, tl1, walk, sym0, sym1, flags);
+  Eng E = callee_eng(kp, P, sbase);
   hot_fetch(E, top, 0);
   __syncthreads();
-  const uint32_t jstar = run_chain<true>(P, sbase, ctl, top, tl0, (int)sym0);
+  const uint32_t jstar = run_chain<true>(kp, P, sbase, ctl, top, tl0, (int)sym0);
   if (jstar) {
     hot_store(E, top, 0);
     __syncthreads();

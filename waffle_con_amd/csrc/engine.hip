@@ -113,6 +113,7 @@ struct Ctl {
   uint32_t hot_prev, hot_load;
   // linear-chain run-ahead (run_chain)
   uint32_t chain_k, chain_slot, chain_stop, chain_novf, chain_nochain, chain_len, chain_nbak;
+  uint32_t chain_kcur;  // dual engine: the next chain's length (doubles after a fully accepted chain)
   uint64_t chain_tot[5];  // updates, w_out, compares, ed increases, row bytes of one chain pass
   uint32_t nkeys[2];
   uint8_t keys[2][kKout];
@@ -508,8 +509,17 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
 // from the kernel arguments (kernarg segment) and the claimed problem, so the
 // kernel's own context never has its address taken (that would move it, with
 // every pointer in it, to scratch memory for the whole kernel).
-__device__ inline Eng callee_eng(const DevProblem& P, Sh<uint8_t>* sbase) {
-  const EngineArgs& A = *(const EngineArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+// (The kernel passes its kernarg segment pointer: a callee's own
+// __builtin_amdgcn_kernarg_segment_ptr() is null.)
+#if defined(__HIP_DEVICE_COMPILE__)
+using KArgs = const __attribute__((address_space(4))) EngineArgs*;
+__device__ __forceinline__ KArgs kernel_args() { return (KArgs)__builtin_amdgcn_kernarg_segment_ptr(); }
+#else
+using KArgs = const EngineArgs*;
+__device__ __forceinline__ KArgs kernel_args() { return nullptr; }
+#endif
+__device__ inline Eng callee_eng(KArgs kp, const DevProblem& P, Sh<uint8_t>* sbase) {
+  const EngineArgs A = *kp;  // scalar loads; the copy is split into registers
   Eng E = make_eng(A, sbase);
   E.P = P;
   E.n = P.n_reads;
@@ -689,6 +699,7 @@ __device__ inline void init_problem(Eng& E, Lo<Ctl>& ctl) {
     ctl.cache_slot = kNoSlot;
     ctl.hot_slot = kNoSlot;
     ctl.hot_load = 0;
+    ctl.chain_kcur = 4;
     for (int sd = 0; sd < 2; ++sd) {  // no cached fx orders (nk <= 14, so k1 = ~0 never matches)
       for (int k = 0; k < kFxCache; ++k) ctl.fxc[sd].k1[k] = ~0ull;
       ctl.fxc[sd].next = 0;
@@ -1944,7 +1955,8 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
       // ---- one child and nothing else queued: linear-chain run-ahead ----
       // (past the last activation point every read of this lineage is active)
       if (nc == 1 && A.chain && uni(ctl.heap_n) == 0 && (E.P.n_active == E.n || len >= E.P.max_act)) {
-        const uint32_t jstar = run_chain<false>(E.P, state_base(A, smem), ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
+        const uint32_t jstar =
+            run_chain<false>(kernel_args(), E.P, state_base(A, smem), ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
         PH_MARK(14);
         if (jstar) continue;
       }
@@ -2309,24 +2321,32 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
       // child: the single engine's walk; a dual node's child: the two-sided
       // walk (unweighted votes; a walking side must be the longer one, so the
       // max length grows with every step).
+#ifndef WC_NO_DUAL_CHAIN
       if (E.chain && nc == 1 && (E.P.n_active == E.n || tlen >= E.P.max_act)) {
         const int x0 = uni((int32_t)ctl.ch_s[0][0]), x1 = uni((int32_t)ctl.ch_s[0][1]);
         uint32_t kind = 0, walk = 0;
         if (!tdual) {
-          if (uni((uint32_t)ctl.ch_kind[0]) == 1) kind = 1;
-        } else if (!weighted) {
+          if (uni((uint32_t)ctl.ch_kind[0]) == 1 && (A.chain_kinds & 1u)) kind = 1;
+        } else if (!weighted && (A.chain_kinds & 2u)) {
           walk = (x0 >= 0 ? 1u : 0u) | (x1 >= 0 ? 2u : 0u);
           const uint32_t L0 = max(tlens[0], tlens[1]);
           if (((walk & 1u) && tlens[0] == L0) || ((walk & 2u) && tlens[1] == L0)) kind = 2;
         }
         if (kind) {
           const uint32_t flags = tm.flags | (x0 < 0 ? 2u : 0u) | (x1 < 0 ? 4u : 0u);
-          const uint32_t jstar = run_engine_chain(E.P, state_base(A, smem), ctl, top, kind, tlens[0], tlens[1], walk,
-                                                  (uint32_t)max(x0, 0), (uint32_t)max(x1, 0), flags);
+          SUB_T0(tch);
+          const uint32_t jstar = run_engine_chain(kernel_args(), E.P, state_base(A, smem), ctl, top, kind, tlens[0],
+                                                  tlens[1], walk, (uint32_t)max(x0, 0), (uint32_t)max(x1, 0), flags);
           PH_MARK(14);
+          // (phase builds) per chain kind: attempts, accepted nodes, speculative steps, cycles
+          SUB_CNT(kind == 1 ? 32 : 35, 1);
+          SUB_CNT(kind == 1 ? 33 : 36, jstar);
+          SUB_CNT(kind == 1 ? 34 : 37, uni(ctl.chain_stop));
+          SUB_T1(kind == 1 ? 38 : 39, tch);
           if (jstar) continue;
         }
       }
+#endif
 
       // ---- build every child: clones first, the last child in place ----
       SUB_CNT(21, nc);

@@ -77,6 +77,7 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   if (nmax <= (uint32_t)kBlock && (sides == 1 || cfg.min_af == 0.0)) {
     chain = sides == 1 ? kChainDefault : kDualChainDefault;
     if (chain_env) chain = std::min<uint32_t>((uint32_t)atoi(chain_env), kChainMax);
+    if (chain == 1) chain = 0;  // a chain takes at least 2 steps
   }
   // node pool. A dual search keeps far more nodes queued than a single one
   // (children of both consensuses, both sides' DWFAs per node: cfg3 loci peak
@@ -346,6 +347,7 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   a.nmax = caps.nmax;
   a.rmax = caps.rmax;
   a.chain = caps.chain;
+  a.chain_kinds = env_chain_kinds();
   a.out = dh + L.off_out;
   a.out_stride = caps.ob;
   a.status = (uint32_t*)(dh + L.off_status);
@@ -619,6 +621,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.nmax = caps.nmax;
   a.rmax = caps.rmax;
   a.chain = caps.chain;  // the device carves LDS from it: must match caps.lds
+  a.chain_kinds = env_chain_kinds();
   a.out = dh + L.off_out;
   a.out_stride = caps.ob;
   a.status = (uint32_t*)(dh + L.off_status);

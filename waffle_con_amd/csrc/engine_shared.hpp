@@ -2,6 +2,7 @@
 // engines (engine.hip). Plain data only.
 #pragma once
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace wc {
 
@@ -89,7 +90,8 @@ struct EngineArgs {
   uint32_t lcap;         // consensus capacity per side
   uint32_t nmax;         // max reads per problem in this batch
   uint32_t rmax;         // result records per problem
-  uint32_t chain;        // single engine: max linear-chain run-ahead steps (0 = off)
+  uint32_t chain;        // max linear-chain run-ahead steps (0 = off); sizes the LDS chain area
+  uint32_t chain_kinds;  // dual engine: bit 0 chains over single-consensus nodes, bit 1 over dual nodes
   uint8_t* out;
   uint64_t out_stride;
   uint32_t* status;      // per problem
@@ -140,7 +142,7 @@ __host__ __device__ inline uint64_t rtab_bytes(uint32_t nmax) {
 // staging stride of one read pulled from host memory (EngineArgs::hreads): its
 // bytes rounded up to 16, then 64 zero bytes (the engine's over-read margin)
 __host__ __device__ inline uint64_t rstage_stride(uint32_t maxlen) { return ((uint64_t)maxlen + 15) / 16 * 16 + 64; }
-constexpr int kPhases = 32;
+constexpr int kPhases = 40;  // 32..39: chain statistics of the dual engine (engine.hip, dual chain call site)
 // offset-activation scratch per workgroup (u64): per wave two lane-interleaved pair arrays of m entries
 __host__ __device__ inline uint64_t act_scr_u64(uint32_t m) { return (uint64_t)kWaves * 2 * m * 64; }  // 0..15 block phases, 16..31 wave-0 sub-phases
 
@@ -211,7 +213,10 @@ struct RInfo {
 // ---- linear-chain run-ahead (single engine, engine.hip run_chain) ----
 constexpr uint32_t kChainMax = 40;      // steps per chain (upper bound; WC_CHAIN); longer chains outrun the 64-B read windows
 constexpr uint32_t kChainDefault = 16;  // steps per chain by default
-constexpr uint32_t kDualChainDefault = 16;  // dual engine (single-consensus nodes): steps per chain
+// dual engine: chains off by default (WC_DUAL_CHAIN=<k> enables them, up to k
+// steps): its searches' chains are short (cfg5 median 4 pops), and the
+// speculation costs more than it saves on cfg3/cfg4/cfg5
+constexpr uint32_t kDualChainDefault = 0;
 constexpr uint32_t kChainOvf = 192;  // multi-symbol nominations stored per chain
 static_assert(kChainOvf <= 256, "ChainOvf index is the low byte of a u16 nomination code");
 struct ChainStep {  // aggregates of one speculative step (node N_j), LDS atomics (one per wave)
@@ -246,6 +251,11 @@ struct DualStep {
 };
 static_assert(sizeof(DualStep) == 48, "DualStep layout");
 __host__ __device__ inline uint32_t chain_sides(uint32_t sides) { return sides == 2 ? 2u : 1u; }
+// dual engine chain kinds (EngineArgs::chain_kinds; WC_DUAL_CHAIN_KINDS overrides, default both)
+inline uint32_t env_chain_kinds() {
+  const char* e = getenv("WC_DUAL_CHAIN_KINDS");
+  return e ? (uint32_t)atoi(e) & 3u : 3u;
+}
 // chain LDS (per side S = chain_sides: the dual engine's chains walk both):
 //   steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[S][K+1][nmax] u16 |
 //   win[S][4*m4][68 B] (read windows) | wb[S][nmax] u32 | pc[K+1] u32 | pred[S][K+2] u8

@@ -264,6 +264,7 @@ int lane_start(wc_service* S, const Req* q) {
   a.nmax = caps.nmax;
   a.rmax = caps.rmax;
   a.chain = caps.chain;
+  a.chain_kinds = env_chain_kinds();
   a.out = dh + L->off_out;
   a.out_stride = caps.ob;
   a.status = (uint32_t*)(dh + L->off_status);
