@@ -2321,7 +2321,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
       // child: the single engine's walk; a dual node's child: the two-sided
       // walk (unweighted votes; a walking side must be the longer one, so the
       // max length grows with every step).
-#ifndef WC_NO_DUAL_CHAIN
+#ifdef WC_DUAL_CHAIN_CALL  // (engine_dchain.hip: the default builds carry no call)
       if (E.chain && nc == 1 && (E.P.n_active == E.n || tlen >= E.P.max_act)) {
         const int x0 = uni((int32_t)ctl.ch_s[0][0]), x1 = uni((int32_t)ctl.ch_s[0][1]);
         uint32_t kind = 0, walk = 0;

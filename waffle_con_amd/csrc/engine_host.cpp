@@ -136,7 +136,9 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   // (no spills: each workgroup's latency is what counts); WC_LOWLAT=0 disables
   const char* lenv = getenv("WC_LOWLAT");
   c.lowlat = !gstate && !c.narrow && ids.size() <= 2ull * (uint64_t)ctx->n_cu && !(lenv && atoi(lenv) == 0);
+  if (sides == 2 && chain > 0 && !gstate) c.narrow = c.lowlat = false;  // the chain build (wcd)
   auto occupancy = [&](size_t l) {
+    if (sides == 2 && chain > 0 && !gstate) return wcd::engine_blocks_per_cu(sides, l);
     return c.narrow ? wcn::engine_blocks_per_cu(sides, l)
                     : (c.lowlat ? wcl::engine_blocks_per_cu(sides, l) : engine_blocks_per_cu(sides, l));
   };
@@ -247,6 +249,8 @@ int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
   if (caps.gstate) {
     if (caps.sides == 1) wcg::launch_single_engine(a, L.grid, 0, L.stream);
     else wcg::launch_dual_engine(a, L.grid, 0, L.stream);
+  } else if (caps.sides == 2 && caps.chain > 0) {
+    wcd::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else if (caps.narrow) {
     if (caps.sides == 1) wcn::launch_single_engine(a, L.grid, caps.lds, L.stream);
     else wcn::launch_dual_engine(a, L.grid, caps.lds, L.stream);
