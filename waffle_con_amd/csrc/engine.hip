@@ -519,7 +519,12 @@ using KArgs = const EngineArgs*;
 __device__ __forceinline__ KArgs kernel_args() { return nullptr; }
 #endif
 __device__ inline Eng callee_eng(KArgs kp, const DevProblem& P, Sh<uint8_t>* sbase) {
-  const EngineArgs A = *kp;  // scalar loads; the copy is split into registers
+  // the pointer arrives in vector registers (call ABI): made uniform, the
+  // argument loads are scalar loads
+  const uint64_t kv = (uint64_t)kp;
+  const uint64_t ku = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)kv) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(kv >> 32)) << 32;
+  const EngineArgs A = *(KArgs)ku;  // the copy is split into registers
   Eng E = make_eng(A, sbase);
   E.P = P;
   E.n = P.n_reads;
