@@ -766,9 +766,7 @@ __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint3
 // 655-679); the virtual pops also grow the active-read minimum per length
 // (:497-513).
 template <bool kDual>
-__device__ __noinline__ uint32_t run_chain(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top,
-                                           uint32_t L0, int s1) {
-  Eng E = callee_eng(kp, P, sbase);  // scalar registers
+__device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
   const int tid = threadIdx.x;
   if (tid == 0) {
     // (the dual engine's chains end at forks of its search more often: their
@@ -921,4 +919,18 @@ __device__ __noinline__ uint32_t run_chain(KArgs kp, DevProblem P, Sh<uint8_t>* 
   }
   __syncthreads();
   return jstar;
+}
+// the out-of-line entries (plain functions: their register allocation is
+// fitted to the one caller, so the call saves no callee-saved registers)
+// The single engine passes its context by reference: measured faster on cfg2
+// than rebuilding it in the callee (34.5 vs 33.3 ms per launch; the callee
+// then saves ~45 callee-saved VGPRs per chain), at the price of the context
+// living in scratch in that kernel. The dual engine's chain builds (wcd)
+// rebuild it from the kernel arguments (callee_eng).
+__device__ __noinline__ uint32_t run_chain_single(Eng& Eref, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
+  return run_chain_impl<false>(eng_uniform(Eref), ctl, top, L0, s1);
+}
+__device__ __noinline__ uint32_t run_chain_dual_single(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl,
+                                                       uint32_t top, uint32_t L0, int s1) {
+  return run_chain_impl<true>(callee_eng(kp, P, sbase), ctl, top, L0, s1);
 }

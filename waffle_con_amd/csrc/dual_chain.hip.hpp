@@ -636,7 +636,7 @@ __device__ __noinline__ uint32_t run_engine_chain(KArgs kp, DevProblem P, Sh<uin
   Eng E = callee_eng(kp, P, sbase);
   hot_fetch(E, top, 0);
   __syncthreads();
-  const uint32_t jstar = run_chain<true>(kp, P, sbase, ctl, top, tl0, (int)sym0);
+  const uint32_t jstar = run_chain_dual_single(kp, P, sbase, ctl, top, tl0, (int)sym0);
   if (jstar) {
     hot_store(E, top, 0);
     __syncthreads();

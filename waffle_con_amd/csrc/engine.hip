@@ -1961,7 +1961,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
       // (past the last activation point every read of this lineage is active)
       if (nc == 1 && A.chain && uni(ctl.heap_n) == 0 && (E.P.n_active == E.n || len >= E.P.max_act)) {
         const uint32_t jstar =
-            run_chain<false>(kernel_args(), E.P, state_base(A, smem), ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
+            run_chain_single(E, ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
         PH_MARK(14);
         if (jstar) continue;
       }
