@@ -15,6 +15,11 @@ ARGS="$@"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
+# heartbeat: a pass writes nothing until it ends (a 10,000-locus cfg5 pass runs
+# minutes), and gpurun takes 3 silent minutes for a hang
+( while sleep 30; do date >> $OUT/heartbeat.log; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
   python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e $ARGS > $OUT/kt_bench.json
 echo "kt done"
