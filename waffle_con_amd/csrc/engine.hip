@@ -1181,7 +1181,11 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
   // false): every voter adds exactly 1.0 to its one symbol, so one ballot per
   // distinct symbol gives both the insertion order and the (exact) per-key
   // sums; lane i counts the reads of the i-th inserted key.
+#ifdef WC_NO_SINGLE_SYM  // (diagnostic variant: every vote takes the general path)
+  const bool single_sym = false;
+#else
   const bool single_sym = !weighted && !multi;
+#endif
   uint32_t cins = 0;
   for (uint32_t base = 0; base < n && single_sym; base += 64) {
     const uint32_t r = base + lane;
@@ -1687,7 +1691,11 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     SUB_T0(tp1);
     // edit distances from the slots when an activation changed them, or when
     // they might not fit the u16 array (wavefront rows past 2^17 entries)
+#ifdef WC_NO_CE  // (diagnostic variant: the prune pass reads every edit distance from the slots)
+    const bool slot_e = true;
+#else
     const bool slot_e = activated || E.wcap > 2u * kCeNone;
+#endif
     uint64_t ccost[kNCB] = {0, 0, 0, 0};
     uint32_t cn0[kNCB] = {0, 0, 0, 0}, cn1[kNCB] = {0, 0, 0, 0};
     for (uint32_t r = tid; r < n; r += kEB) {
