@@ -669,17 +669,28 @@ def main():
     # torch ships its own HIP runtime next to the one the library links: torch
     # must initialise the device first, or its later init finds no GPU
     import torch
+    # WC_BENCH_SHARE_GPU=1: a rehearsal of the N-rank path on a box with fewer
+    # GPUs (ranks share devices round-robin, gloo for the barrier and the
+    # reductions); the line says so and is not a scaling measurement
+    share = world > 1 and os.environ.get("WC_BENCH_SHARE_GPU") == "1"
+    device_index = local_rank % max(1, torch.cuda.device_count()) if share else local_rank
     torch.cuda.init()
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(device_index)
     dist = None
+    rdev = None  # device of the reduction tensors
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if share:
+            dist.init_process_group("gloo")
+            rdev = "cpu"
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            rdev = "cuda"
 
     import waffle_con_amd as w
     from waffle_con_amd import shard
 
-    ctx = w.Context(local_rank)
+    ctx = w.Context(device_index)
 
     def note(msg):  # progress on stderr (long workloads must not look hung)
         print("[bench rank %d] %s" % (rank, msg), file=sys.stderr, flush=True)
@@ -714,7 +725,7 @@ def main():
             readb += W.read_bytes()
             loci += nl
     elapsed, total_upd, total_loci = shard.reduce_run(
-        dist, tm.elapsed, upd, loci, device="cuda" if dist is not None else None)
+        dist, tm.elapsed, upd, loci, device=rdev)
 
     note("timed region done: %.2f s" % tm.elapsed)
     e2e = None
@@ -730,15 +741,15 @@ def main():
         with shard.Timer(dist, sync) as tm5:
             st5, n5 = C5.step()
         el5, upd5, loci5 = shard.reduce_run(dist, tm5.elapsed, st5["updates"], n5,
-                                            device="cuda" if dist is not None else None)
-        rep = C5.rank_report(dist, "cuda" if dist is not None else None)
+                                            device=rdev)
+        rep = C5.rank_report(dist, rdev)
         cfg5_leg = {"workload": C5.config()["workload"], "loci": int(loci5), "elapsed_s": el5,
                     "cfg5_loci_per_s": loci5 / el5, "cfg5_updates_per_s": upd5 / el5, "gen_s": C5.gen_s,
                     "scaling": "strong", "n_gpus": world}
         cfg5_leg.update(rep)
         note("cfg5 leg done: %.2f s" % el5)
 
-    w_ranks = W.rank_report(dist, "cuda" if dist is not None else None) if hasattr(W, "rank_report") else None
+    w_ranks = W.rank_report(dist, rdev) if hasattr(W, "rank_report") else None
 
     if rank != 0:
         if dist is not None:
@@ -811,6 +822,9 @@ def main():
     if hasattr(W, "extra"):
         note("extra legs")
         line.update(W.extra())
+    if share:
+        line["rehearsal"] = "%d ranks sharing %d GPU(s) (WC_BENCH_SHARE_GPU, gloo): exercises the N-rank path, " \
+                            "not a scaling measurement" % (world, max(1, torch.cuda.device_count()))
     if cfg5_leg:
         line["cfg5_strong"] = cfg5_leg
     if w_ranks:
