@@ -195,12 +195,18 @@ void destroy_launches(wc_ctx* ctx) {
 
 // WC_FAULT_LOG=1 (diagnostics): on a GPU memory fault, print the faulting
 // address against the buffers of the launches started last (which buffer,
-// which workgroup's workspace, the offset inside it)
+// which workgroup's workspace, the offset inside it). WC_FAULT_SENTINELS=1
+// also gives every pointer argument a batch launch does not use a distinct
+// unmapped address (kSentinel + field << 32) instead of null, so that a
+// fault through one of them names the field (the device code is unchanged:
+// these fields are only read behind A.stream or in other builds).
 namespace {
 struct FaultRange {
   const char* name;
   uint64_t base, bytes, stride;
 };
+constexpr uint64_t kSentinel = 0x1e0000000000ull;
+const char* const kSentinelNames[] = {"sctl", "qhead", "exited", "act_scr", "gstate", "hreads"};
 std::mutex g_fault_mu;
 std::vector<FaultRange> g_fault_ranges;
 hsa_status_t fault_event(const hsa_amd_event_t* ev, void*) {
@@ -208,12 +214,16 @@ hsa_status_t fault_event(const hsa_amd_event_t* ev, void*) {
   const uint64_t va = ev->memory_fault.virtual_address;
   fprintf(stderr, "[wc] GPU memory fault at 0x%llx (reason mask 0x%x)\n", (unsigned long long)va,
           ev->memory_fault.fault_reason_mask);
+  if (va >= kSentinel && va < kSentinel + (6ull << 32))
+    fprintf(stderr, "[wc]   sentinel of EngineArgs::%s + %llu\n", kSentinelNames[(va - kSentinel) >> 32],
+            (unsigned long long)((va - kSentinel) & 0xFFFFFFFFull));
   std::lock_guard<std::mutex> g(g_fault_mu);
   for (const FaultRange& r : g_fault_ranges) {
     const int64_t d = (int64_t)(va - r.base);
     fprintf(stderr, "[wc]   %-8s base 0x%llx bytes %llu stride %llu: offset %lld", r.name, (unsigned long long)r.base,
             (unsigned long long)r.bytes, (unsigned long long)r.stride, (long long)d);
     if (r.stride && d >= 0) fprintf(stderr, " (workgroup %lld + %lld)", (long long)(d / (int64_t)r.stride), (long long)(d % (int64_t)r.stride));
+    if (d >= 0 && (uint64_t)d < r.bytes) fprintf(stderr, "  <== inside");
     fprintf(stderr, "\n");
   }
   return HSA_STATUS_SUCCESS;
@@ -222,13 +232,27 @@ void fault_log_record(const Launch& L, const EngineArgs& a, const Caps& caps) {
   static std::once_flag once;
   std::call_once(once, [] { (void)hsa_amd_register_system_event_handler(fault_event, nullptr); });
   std::lock_guard<std::mutex> g(g_fault_mu);
-  if (g_fault_ranges.size() > 64) g_fault_ranges.erase(g_fault_ranges.begin(), g_fault_ranges.begin() + 32);
+  if (g_fault_ranges.size() > 96) g_fault_ranges.erase(g_fault_ranges.begin(), g_fault_ranges.begin() + 48);
   g_fault_ranges.push_back({"ws", (uint64_t)a.ws, (uint64_t)L.ws.cap, a.ws_stride});
   if (caps.gstate) g_fault_ranges.push_back({"gstate", (uint64_t)a.gstate, (uint64_t)L.gst.cap, a.gstate_stride});
-  g_fault_ranges.push_back({"reads", (uint64_t)a.rbytes, 0, 0});
-  g_fault_ranges.push_back({"problems", (uint64_t)a.problems, 0, 0});
+  g_fault_ranges.push_back({"reads", (uint64_t)a.rbytes, L.reads_bytes, 0});
+  g_fault_ranges.push_back({"problems", (uint64_t)a.problems, (uint64_t)L.probs.cap, sizeof(DevProblem)});
+  g_fault_ranges.push_back({"roff", (uint64_t)a.roff, (uint64_t)L.sroff.cap, 8});
+  g_fault_ranges.push_back({"rlen", (uint64_t)a.rlen, (uint64_t)L.srlen.cap, 4});
+  g_fault_ranges.push_back({"ract", (uint64_t)a.ractivate, (uint64_t)L.ract.cap, 8});
+  g_fault_ranges.push_back({"counter", (uint64_t)a.work_counter, (uint64_t)L.counter.cap, 0});
+  g_fault_ranges.push_back({"done", (uint64_t)a.done, (uint64_t)L.host.cap, 0});
   g_fault_ranges.push_back({"out", (uint64_t)a.out, (uint64_t)a.out_stride * L.P, a.out_stride});
   if (a.act_scr) g_fault_ranges.push_back({"act", (uint64_t)a.act_scr, (uint64_t)L.act.cap, a.act_stride * 8});
+}
+// WC_FAULT_SENTINELS: the unused pointer arguments of a batch launch
+void fault_sentinels(EngineArgs& a, const Caps& caps) {
+  if (!getenv("WC_FAULT_SENTINELS") || a.stream) return;
+  a.sctl = (StreamCtl*)(kSentinel + (0ull << 32));
+  a.qhead = (uint32_t*)(kSentinel + (1ull << 32));
+  a.exited = (uint32_t*)(kSentinel + (2ull << 32));
+  if (!a.act_scr) a.act_scr = (uint64_t*)(kSentinel + (3ull << 32));  // read only by offset activation
+  if (!caps.gstate) a.gstate = (uint8_t*)(kSentinel + (4ull << 32));
 }
 }  // namespace
 
@@ -244,6 +268,7 @@ int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
   HIPCHK(hipMemsetAsync(L.ws.p, kGuardByte, a.ws_stride * L.grid, L.stream));
   if (caps.gstate) HIPCHK(hipMemsetAsync(L.gst.p, kGuardByte, a.gstate_stride * L.grid, L.stream));
 #endif
+  fault_sentinels(a, caps);
   if (getenv("WC_FAULT_LOG")) fault_log_record(L, a, caps);
   HIPCHK(hipEventRecord(L.ev0, L.stream));
   if (caps.gstate) {
@@ -340,6 +365,7 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   a.n_problems = P;
   a.sides = caps.sides;
   a.rbytes = (const uint8_t*)b->reads.p;
+  L.reads_bytes = b->reads.cap;
   a.roff = (const uint64_t*)L.sroff.p;
   a.rlen = (const uint32_t*)L.srlen.p;
   a.ractivate = (const int64_t*)L.ract.p;

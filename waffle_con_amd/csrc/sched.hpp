@@ -51,6 +51,7 @@ struct Launch {
   uint32_t n_taken = 0;
   bool busy = false;
   double kernel_ms = 0;
+  uint64_t reads_bytes = 0;  // WC_FAULT_LOG: bytes of the read arena the launch reads
   uint64_t ws_stride = 0;  // WC_CHECK: workspace bytes per workgroup (guard zone at the end)
   std::vector<DevProblem> dp;
   std::vector<uint64_t> h_sroff;
