@@ -10,6 +10,10 @@ Workloads (--workload, default cfg2):
   cfg5          PriorityConsensusDWFA over a FIXED batch of --loci cfg5 PGx loci
                 (default 10,000) split over the ranks by a cost-sorted queue
                 (strong scaling, no collective on the data path).
+  cfg2-api      cfg2 loci through the per-locus API (ConsensusDWFA.consensus)
+                from --api-threads native threads (the submission service).
+  cfg5-api      cfg5 loci through PriorityConsensusDWFA.consensus from
+                --api-threads native threads (the submission service).
 
 One step = one pass of the engine over the rank's batch, reads resident in HBM
 (ResidentBatch uploaded before timing; priority workloads upload per call and
@@ -501,15 +505,23 @@ class Cfg5:
         else:
             self.store = shard.LocalStore()
         self.last, self.mine, self.busy_s, self.static_s = {}, [], 0.0, 0.0
+        self.t0, self.done, self.lat = 0.0, {}, {}
 
     def _run(self, ids):
+        """One priority_consensus_batch call over loci `ids`; records each
+        locus's completion time (from the step's start: done) and its latency
+        inside the call (from the call's start: lat)."""
         import waffle_con_amd as w
+        t_call = time.perf_counter()
         res, st = w.priority_consensus_batch([(self.L[i], None, None) for i in ids], self.cfg, context=self.ctx,
-                                             return_errors=True)
+                                             return_errors=True, per_problem=True)
         bad = [r for r in res if isinstance(r, Exception)]
         if bad:
             raise RuntimeError("engine error: %s" % bad[0])
         self.last.update(zip(ids, res))
+        for i, pp in zip(ids, st.pop("per_problem")):
+            self.lat[i] = pp["wall_ms"] / 1e3
+            self.done[i] = t_call - self.t0 + self.lat[i]
         return st
 
     def read_bytes(self):
@@ -519,8 +531,8 @@ class Cfg5:
         from waffle_con_amd import shard
         self.k += 1
         q = shard.SharedQueue(self.store, len(self.tail), self.chunk, key="wc_cfg5_%d" % self.k)
-        self.last, self.mine = {}, list(self.static)
-        t0 = time.perf_counter()
+        self.last, self.mine, self.done, self.lat = {}, list(self.static), {}, {}
+        t0 = self.t0 = time.perf_counter()
         tot = self._run(self.static)
         self.static_s = time.perf_counter() - t0
         keys = ("kernel_ms", "updates", "w_out", "compares", "launches", "row_bytes")
@@ -567,6 +579,37 @@ class Cfg5:
                 "busy_max_s": max(busy), "busy_min_s": min(busy), "tail_s": max(busy) - min(busy),
                 "prefix_loci": None if dist is not None else len(self.static), "tail_loci": len(self.tail),
                 "chunk": self.chunk}
+
+    def tail_report(self, dist):
+        """Completion-time quantiles over every locus of the batch (all ranks;
+        seconds from the leg's start) and the heaviest locus (largest cost)
+        under load: its latency inside its call and when it finished."""
+        import math
+        h = max(range(self.total), key=lambda i: (self.costs[i], -i))
+        mine = {"done": [self.done[i] for i in self.mine],
+                "slowest": max(((self.lat[i], i) for i in self.mine), default=(0.0, -1)),
+                "heaviest": (self.lat[h], self.done[h]) if h in self.lat else None}
+        if dist is None:
+            rows = [mine]
+        else:
+            rows = [None] * self.world
+            dist.all_gather_object(rows, mine)
+        done = sorted(d for r in rows for d in r["done"])
+
+        def q(f):
+            return done[min(len(done) - 1, max(0, int(math.ceil(f * len(done))) - 1))] if done else None
+        hv = next((r["heaviest"] for r in rows if r["heaviest"] is not None), (None, None))
+        slow = max(r["slowest"] for r in rows)
+        return {"t50_s": q(0.50), "t95_s": q(0.95), "t100_s": q(1.0),
+                "heaviest_locus": h, "heaviest_cost": self.costs[h],
+                "heaviest_latency_under_load_s": hv[0], "heaviest_done_s": hv[1],
+                "slowest_latency_under_load_s": slow[0], "slowest_locus": slow[1]}
+
+    def heaviest_alone(self, h):
+        """The heaviest locus alone on the GPU (one call, nothing else queued): s."""
+        t0 = time.perf_counter()
+        self._run([h])
+        return time.perf_counter() - t0
 
     def cpu(self, threads, target_s):
         o = orc()
@@ -633,8 +676,141 @@ class Cfg4(Cfg5):
         return None  # the oracle needs ~2 min for this locus; measured separately
 
 
+class Cfg5Api:
+    """PriorityConsensusDWFA::consensus through the reference's per-locus API
+    (priority_consensus.rs:172, `&self`, one instance per thread: the PGx
+    caller pattern behind cfg5) from T native host threads, each calling it on
+    its own cfg5 loci one at a time (tools/api_bench.cpp api_bench_priority_run
+    -> wc_service_priority_consensus: every caller unwinds its own LIFO stack,
+    all sub-problems share the service's persistent launches). One step =
+    every locus once. Reported beside the value: a thread sweep, per-call
+    launches (one wc_priority_consensus_batch per call) at 16 and 64 threads,
+    and the batch path (wc_priority_consensus_batch over all loci at once) on
+    the same loci; every API result is checked against the batch path's."""
+    name = "cfg5-api"
+    scaling = "weak"
+    kernel = "wcn::dual_engine_kernel"
+
+    @staticmethod
+    def pregen(a, rank, world, total=None):
+        from waffle_con_amd import synth
+        n = a.loci or 1024
+        ids = list(range(rank * n, (rank + 1) * n))
+        t0 = time.perf_counter()
+        loci = pool_map(synth.cfg5_locus, ids)
+        return {"ids": ids, "loci": loci, "gen_s": time.perf_counter() - t0}
+
+    def __init__(self, a, rank, world, ctx, pre=None):
+        import ctypes
+        from waffle_con_amd import _lib
+        from waffle_con_amd.cdwfa_config import CdwfaConfig
+        from waffle_con_amd.priority_consensus import _chain_problems
+        self.a, self.ctx, self.rank, self.world = a, ctx, rank, world
+        pre = pre or self.pregen(a, rank, world)
+        self.ids, self.L, self.gen_s = pre["ids"], pre["loci"], pre["gen_s"]
+        self.n = len(self.L)
+        self.upload_s = 0.0
+        self.threads = a.api_threads
+        self.cfg = CdwfaConfig(wildcard=ord("*"))
+        path = os.path.join(ROOT, "tools", "libapibench.so")
+        if not os.path.exists(path):
+            raise RuntimeError("tools/libapibench.so is missing: build it with `make -C tools`")
+        self.H = ctypes.CDLL(path)
+        self.H.api_bench_priority_run.argtypes = [
+            ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.POINTER(_lib.WcChainProblem), ctypes.POINTER(_lib.WcConfig), ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_lib.WcServiceStats)]
+        self.arr, self.keep = _chain_problems([(ch, None, None) for ch in self.L])
+        self.ccfg = _lib.make_config(self.cfg)
+        self.last, self.lat, self.svc = None, [], {}
+        self._readb = sum(len(x) for ch in self.L for c in ch for x in c)
+
+    def read_bytes(self):
+        return self._readb
+
+    def run(self, mode, threads, n=None):
+        """n loci on `threads` native threads: (wall s, latencies ms, results, summed stats, service stats)."""
+        import ctypes
+        from waffle_con_amd import _lib
+        from waffle_con_amd.consensus import _stats
+        from waffle_con_amd.priority_consensus import _priority_results
+        n = n or self.n
+        res = (ctypes.c_void_p * n)()
+        lat = (ctypes.c_double * n)()
+        wall = ctypes.c_double()
+        sst = _lib.WcServiceStats()
+        L = _lib.lib()
+        rc = self.H.api_bench_priority_run(_lib.LIB_PATH.encode(), self.ctx.device, mode, threads, n, self.arr,
+                                           ctypes.byref(self.ccfg), res, lat, ctypes.byref(wall), ctypes.byref(sst))
+        if rc != 0:
+            raise RuntimeError("api_bench_priority_run failed (rc %d)" % rc)
+        tot = {"kernel_ms": 0.0, "updates": 0, "w_out": 0, "compares": 0, "launches": 0, "row_bytes": 0}
+        out = []
+        try:
+            for i in range(n):
+                st = _stats(res[i], L)
+                for k in ("updates", "w_out", "compares", "launches", "row_bytes"):
+                    tot[k] += st[k]
+                tot["kernel_ms"] += st["kernel_ms"]
+                out.append(_priority_results(res[i], 1, self.cfg, L, True)[0])
+        finally:
+            for i in range(n):
+                if res[i]:
+                    L.wc_results_free(res[i])
+        return wall.value, list(lat), out, tot, sst.as_dict()
+
+    def step(self):
+        wall, lat, res, tot, sst = self.run(0, self.threads)
+        bad = [r for r in res if isinstance(r, Exception)]
+        if bad:
+            raise RuntimeError("engine error: %s" % bad[0])
+        self.last, self.lat, self.svc = res, lat, sst
+        return tot, len(res)
+
+    def extra(self):
+        import waffle_con_amd as w
+        t0 = time.perf_counter()
+        bres, _ = w.priority_consensus_batch([(ch, None, None) for ch in self.L], self.cfg, context=self.ctx)
+        batch_s = time.perf_counter() - t0
+        out = {"api_threads": self.threads, "api_matches_batch_path": self.last == bres,
+               "api_latency_ms_median": statistics.median(self.lat),
+               "api_latency_ms_p90": sorted(self.lat)[int(0.9 * (len(self.lat) - 1))],
+               "api_latency_ms_max": max(self.lat),
+               "api_service_stats": self.svc, "batch_path_loci_per_s": self.n / batch_s}
+        sweep = {}
+        for t in sorted({16, 64, 256, self.threads}):
+            wt, _, r, _, _ = self.run(0, t)
+            sweep[str(t)] = self.n / wt
+            out["api_matches_batch_path"] &= r == bres
+        out["api_service_loci_per_s_by_threads"] = sweep
+        per_call = {}
+        for t in (16, 64):
+            n = min(self.n, 128)
+            wt, _, r, _, _ = self.run(1, t, n)
+            per_call[str(t)] = n / wt
+            out["api_matches_batch_path"] &= r == bres[:n]
+        out["api_per_call_launch_loci_per_s_by_threads"] = per_call
+        return out
+
+    def config(self):
+        return {"workload": "PriorityConsensusDWFA cfg5 through the reference's per-locus API: %d PGx loci/GPU "
+                            "(1-6 kb, 2 haplotypes, 15-40 reads each @ 0.5%%, [HPC(read), read] chains, wildcard "
+                            "'*'), %d native caller threads, one locus per call" % (self.n, self.threads),
+                "loci_per_gpu": self.n, "api_threads": self.threads,
+                "parallelism": "loci-sharded x%d (no collective)" % self.world}
+
+    def data(self):
+        return "synthetic: synth.cfg5_locus(seed) seeds %d..%d" % (self.ids[0], self.ids[-1])
+
+    def e2e(self, steps):
+        return None
+
+    def cpu(self, threads, target_s):
+        return None  # the cfg5 CPU baseline is in the default line's cfg5_strong leg (same loci generator)
+
+
 WORKLOADS = {"cfg2": Cfg2, "cfg2-api": Cfg2Api, "cfg2-latency": Cfg2Latency, "cfg3": Cfg3, "cfg4": Cfg4,
-             "cfg5": Cfg5}
+             "cfg5": Cfg5, "cfg5-api": Cfg5Api}
 
 
 # ---------------------------------------------------------------------------
@@ -736,17 +912,56 @@ def main():
     # one pass, barrier + device sync on both sides, max over ranks
     cfg5_leg = None
     if leg_pre is not None:
-        note("cfg5 strong-scaling leg: %d loci" % a.cfg5_loci)
+        note("cfg5 strong-scaling leg: %d loci (untimed warm-up pass)" % a.cfg5_loci)
         C5 = Cfg5(a, rank, world, ctx, leg_pre)
+        C5.step()  # warm-up: first-pass allocations and planning stay out of the timed pass
+        note("cfg5 leg: timed pass")
         with shard.Timer(dist, sync) as tm5:
             st5, n5 = C5.step()
         el5, upd5, loci5 = shard.reduce_run(dist, tm5.elapsed, st5["updates"], n5,
                                             device=rdev)
         rep = C5.rank_report(dist, rdev)
+        tail = C5.tail_report(dist)
         cfg5_leg = {"workload": C5.config()["workload"], "loci": int(loci5), "elapsed_s": el5,
                     "cfg5_loci_per_s": loci5 / el5, "cfg5_updates_per_s": upd5 / el5, "gen_s": C5.gen_s,
-                    "scaling": "strong", "n_gpus": world}
+                    "scaling": "strong", "n_gpus": world, "warmup": "one untimed pass of the same batch",
+                    "tail": tail}
         cfg5_leg.update(rep)
+        # roofline of this rank's engine launches (the dual engine): the
+        # compulsory-byte model (read bytes once + row bytes) over their kernel
+        # time, with the committed PMC profile of the same workload beside it
+        kms5 = st5["kernel_ms"]
+        model5 = C5.read_bytes() + st5["row_bytes"]
+        rl5 = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": Cfg5.kernel,
+               "achieved": model5 / (kms5 / 1e3) / 1e9 if kms5 > 0 else None, "frac": None,
+               "model": "compulsory bytes: read bytes (each once) + wavefront-row bytes (engine row_bytes)",
+               "model_bytes": model5, "kernel_ms": kms5, "launches": st5["launches"],
+               "note": "rank 0's launches; kernel_ms sums the stream epochs' HIP-event times"}
+        if rl5["achieved"] is not None:
+            rl5["frac"] = rl5["achieved"] / HBM_PEAK_GBS
+        pmc5 = profile_record("pmc_traffic", C5.config()["workload"]) if world == 1 else None
+        if pmc5:
+            rl5["pmc_traffic_bytes_per_launch"] = pmc5["traffic_bytes_per_launch"]
+            rl5["pmc_kernel_ms_per_launch"] = pmc5.get("kernel_ms_per_launch_bench_events")
+            if rl5["pmc_kernel_ms_per_launch"]:
+                rl5["pmc_frac"] = (pmc5["traffic_bytes_per_launch"] / (rl5["pmc_kernel_ms_per_launch"] / 1e3) / 1e9
+                                   / HBM_PEAK_GBS)
+            rl5["pmc_source"] = pmc5["_file"]
+        cfg5_leg["roofline"] = rl5
+        if rank == 0 and tail["heaviest_latency_under_load_s"] is not None:
+            cfg5_leg["tail"]["heaviest_latency_alone_s"] = C5.heaviest_alone(tail["heaviest_locus"])
+        if rank == 0 and not a.no_cpu:
+            # bounded oracle check of sampled loci (and, at N=1, the CPU baseline)
+            cores, aff, quota = usable_cpus()
+            threads = a.cpu_threads or cores
+            cb = C5.cpu(threads, a.cpu_seconds if world == 1 else 3.0)
+            cfg5_leg["gpu_matches_cpu_on_sample"] = cb["gpu_matches_cpu_on_sample"]
+            cfg5_leg["check_sample"] = cb["sample"]
+            if world == 1:
+                cb.update({"cores": threads, "kind": "port", "cpu_model": cpu_model(), "affinity_cpus": aff,
+                           "cgroup_quota_cpus": quota})
+                cfg5_leg["cpu_baseline"] = cb
+                cfg5_leg["gpu_vs_cpu_loci"] = cfg5_leg["cfg5_loci_per_s"] / cb["loci_per_s"]
         note("cfg5 leg done: %.2f s" % el5)
 
     w_ranks = W.rank_report(dist, rdev) if hasattr(W, "rank_report") else None

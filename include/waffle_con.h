@@ -129,7 +129,15 @@ int wc_batch_dual_consensus(wc_ctx* ctx, wc_batch* b, const wc_config* cfg, wc_r
  * blocks until its own result is ready and returns a one-problem result set
  * (free with wc_results_free), exactly what wc_consensus_batch /
  * wc_dual_consensus_batch with that one problem return. Thread-safe; one
- * service per device. arena_bytes: HBM for in-flight reads (0 = 4 GiB). */
+ * service per device. arena_bytes: pinned host memory for the reads of the
+ * calls in flight (0 = 256 MiB; a locus larger than a quarter of it takes the
+ * batch path). wc_service_priority_consensus serves
+ * PriorityConsensusDWFA::consensus (priority_consensus.rs:172-341) the same
+ * way: the calling thread unwinds the reference's LIFO work stack and every
+ * DualConsensusDWFA sub-problem runs in the shared launches; the result is
+ * what wc_priority_consensus_batch with that one problem returns. Calls made
+ * while wc_service_destroy runs fail with WC_E_HIP; calls already inside
+ * complete first. */
 typedef struct wc_service wc_service;
 typedef struct wc_service_stats {
   uint64_t calls;       /* consensus calls */
@@ -143,6 +151,8 @@ int wc_service_create(int device, uint64_t arena_bytes, wc_service** out);
 void wc_service_destroy(wc_service* s);
 int wc_service_consensus(wc_service* s, const wc_config* cfg, const wc_problem* problem, wc_results** out);
 int wc_service_dual_consensus(wc_service* s, const wc_config* cfg, const wc_problem* problem, wc_results** out);
+int wc_service_priority_consensus(wc_service* s, const wc_config* cfg, const wc_chain_problem* problem,
+                                  wc_results** out);
 int wc_service_get_stats(wc_service* s, wc_service_stats* out);
 const char* wc_service_last_error(wc_service* s);
 
@@ -218,7 +228,8 @@ typedef struct wc_stats {
   double wall_ms;           /* host wall time of the whole call */
 } wc_stats;
 int wc_results_stats(const wc_results* r, wc_stats* out);
-/* per-problem counters (same fields; kernel_ms/wall_ms/launches zero) */
+/* per-problem counters (same fields; kernel_ms and launches zero; wall_ms =
+ * time from the start of the call until this problem's result was final) */
 int wc_results_problem_stats(const wc_results* r, uint32_t p, wc_stats* out);
 
 /* Standalone DWFALite (dynamic_wfa.rs:48-265) on the device: one job = one

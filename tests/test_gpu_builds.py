@@ -2,7 +2,7 @@
 build at 4 waves/SIMD (WC_NARROW=0 WC_LOWLAT=0), the same at 2 waves/SIMD
 (engine_lowlat.hip, the default for launches of at most 2 problems per CU),
 the 128-thread build (engine_narrow.hip; WC_NARROW bit 0 = single engine,
-bit 1 = dual engine, default 2) and the global-state build (WC_GSTATE). The build is
+bit 1 = dual engine, default 2) and the global-state build (WC_GSTATE), and each dual build with dual_hot forced on. The build is
 picked per launch from the environment (engine_host.cpp plan_caps), so one
 process exercises all of them. Sequences, scores and every work counter must
 equal the oracle's."""
@@ -20,12 +20,16 @@ KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "no
         "peak_queue_size", "row_bytes")
 BUILDS = {"wide": {"WC_NARROW": "0", "WC_LOWLAT": "0"}, "lowlat": {"WC_NARROW": "0"},
           "narrow-single": {"WC_NARROW": "1"}, "narrow-dual": {"WC_NARROW": "2"}, "narrow": {"WC_NARROW": "3"},
-          "gstate": {"WC_GSTATE": "1"}}
+          "gstate": {"WC_GSTATE": "1"},
+          # the dual engine with the popped node's RStates in LDS (dual_hot: an
+          # opt-in knob, measured not to pay; forced here in every dual build)
+          "wide-hot": {"WC_NARROW": "0", "WC_LOWLAT": "0", "WC_DUAL_HOT": "2"},
+          "lowlat-hot": {"WC_NARROW": "0", "WC_DUAL_HOT": "2"}, "narrow-hot": {"WC_NARROW": "2", "WC_DUAL_HOT": "2"}}
 
 
 @pytest.fixture(params=sorted(BUILDS))
 def build(request):
-    old = {k: os.environ.get(k) for k in ("WC_NARROW", "WC_GSTATE", "WC_LOWLAT")}
+    old = {k: os.environ.get(k) for k in ("WC_NARROW", "WC_GSTATE", "WC_LOWLAT", "WC_DUAL_HOT")}
     for k in old:
         os.environ.pop(k, None)
     os.environ.update(BUILDS[request.param])

@@ -117,3 +117,61 @@ def test_service_off_uses_per_call_launches(monkeypatch):
     s0 = _stats()
     assert hip.consensus(p, min_count=3) == orc.consensus(p, min_count=3)
     assert _stats()["calls"] == s0["calls"]
+
+
+def test_threaded_priority_calls_match_oracle():
+    """PriorityConsensusDWFA.consensus() from many threads at once
+    (wc_service_priority_consensus: each caller unwinds its own LIFO stack, the
+    dual sub-problems share the service's lanes): results and every counter
+    equal the oracle's."""
+    from waffle_con_amd import synth
+    loci = [synth.cfg5_locus(s) for s in range(10)]
+    s0 = _stats()
+    got = _run_threads([lambda ch=ch: hip.priority_consensus(ch, counters=True, wildcard=ord("*")) for ch in loci], 10)
+    s1 = _stats()
+    for ch, (g, gc) in zip(loci, got):
+        e, ec = orc.priority_consensus(ch, counters=True, wildcard=ord("*"))
+        assert g == e
+        for k in ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
+                  "nodes_ignored", "peak_queue_size"):
+            assert gc[k] == ec[k], k
+    assert s1["served"] > s0["served"]
+
+
+def test_priority_call_with_offsets_and_seed_groups():
+    """Sub-problems with offsets take the batch path on the service thread;
+    seed groups fix the root order (priority_consensus.rs:180)."""
+    from waffle_con_amd import synth
+    chains = synth.cfg5_locus(3)
+    offs = [[None, None if i % 3 else 10 + i] for i in range(len(chains))]
+    groups = [i % 3 if i % 4 else None for i in range(len(chains))]
+    kw = dict(wildcard=ord("*"))
+    s0 = _stats()
+    got = hip.priority_consensus(chains, offsets=offs, seed_groups=groups, **kw)
+    assert got == orc.priority_consensus(chains, offsets=offs, seed_groups=groups, **kw)
+    assert _stats()["fallback"] > s0["fallback"]
+
+
+def test_batch_path_requests_under_lane_traffic():
+    """Offsets and > 256-read problems (the batch path, run by the service
+    thread while no lane runs) mixed with steady lane traffic from many
+    threads: every result equals the oracle's and the batch-path count is
+    exactly the number of such calls."""
+    plain = [_gen(900, 12, 0.02, 700 + s) for s in range(40)]
+    base = _gen(700, 10, 0.02, 61)
+    offs = [None] * 8 + [100, 150]
+    deep = _gen(300, 300, 0.01, 62)
+    jobs, exp = [], []
+    for i, p in enumerate(plain):
+        jobs.append(lambda p=p: hip.consensus(p, min_count=3))
+        exp.append(orc.consensus(p, min_count=3))
+        if i % 10 == 5:
+            jobs.append(lambda: hip.consensus(base, offsets=offs, min_count=3))
+            exp.append(orc.consensus(base, offsets=offs, min_count=3))
+        if i % 20 == 9:
+            jobs.append(lambda: hip.consensus(deep, min_count=50))
+            exp.append(orc.consensus(deep, min_count=50))
+    s0 = _stats()
+    assert _run_threads(jobs, 16) == exp
+    s1 = _stats()
+    assert s1["fallback"] - s0["fallback"] == 4 + 2

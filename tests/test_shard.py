@@ -158,16 +158,21 @@ def _bench_cfg5_worker(rank, world, port, total, q):
         ran = []
 
         def fake_run(ids):
+            import time
             ran.extend(ids)
             C.last.update((i, None) for i in ids)
+            for i in ids:  # as Cfg5._run records them
+                C.lat[i] = 0.001 * (i % 7)
+                C.done[i] = time.perf_counter() - C.t0 + C.lat[i]
             return {"kernel_ms": 0.0, "updates": len(ids), "w_out": 0, "compares": 0, "launches": 1, "row_bytes": 0}
 
         C._run = fake_run
         st, n = C.step()
         rep = C.rank_report(dist, None)
+        tail = C.tail_report(dist)
         gathered = [None] * world
         dist.all_gather_object(gathered, ran)
-        q.put((rank, sorted(pre["loci"]), list(C.static), list(C.tail), gathered, st["updates"], n, rep))
+        q.put((rank, sorted(pre["loci"]), list(C.static), list(C.tail), gathered, st["updates"], n, rep, tail))
     finally:
         dist.destroy_process_group()
 
@@ -190,8 +195,13 @@ def test_gloo_world2_bench_cfg5_partition():
     ran = out[0][4]
     assert not set(ran[0]) & set(ran[1])
     assert sorted(ran[0] + ran[1]) == list(range(total))
-    for rank, generated, static, tail, _, upd, n, rep in out:
+    for rank, generated, static, tail, _, upd, n, rep, tl in out:
         assert set(ran[rank]) <= set(generated) and set(static) <= set(ran[rank])
         assert upd == n == len(ran[rank])
         assert rep["rank_loci"] == [len(ran[0]), len(ran[1])]
+        # the completion-time quantiles span both ranks' loci; the heaviest
+        # locus (largest cost) was found on the rank that ran it
+        assert 0 <= tl["t50_s"] <= tl["t95_s"] <= tl["t100_s"]
+        assert tl["heaviest_latency_under_load_s"] == 0.001 * (tl["heaviest_locus"] % 7)
+    assert out[0][8] == out[1][8]  # every rank reports the same gathered tail
     assert out[0][3] == out[1][3]  # both ranks see the same tail order

@@ -127,7 +127,7 @@ EXPORTED = (
     "wc_results_problem_stats", "wc_dwfa_batch", "wc_generate_test", "wc_gen_consensus",
     "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_wfa_ed_batch",
     "wc_service_create", "wc_service_destroy", "wc_service_consensus", "wc_service_dual_consensus",
-    "wc_service_get_stats", "wc_service_last_error",
+    "wc_service_priority_consensus", "wc_service_get_stats", "wc_service_last_error",
 )
 
 
@@ -208,6 +208,8 @@ def lib():
         L.wc_service_destroy.argtypes = [vp]
         for f in ("wc_service_consensus", "wc_service_dual_consensus"):
             getattr(L, f).argtypes = [vp, ctypes.POINTER(WcConfig), ctypes.POINTER(WcProblem), ctypes.POINTER(vp)]
+        L.wc_service_priority_consensus.argtypes = [vp, ctypes.POINTER(WcConfig), ctypes.POINTER(WcChainProblem),
+                                                    ctypes.POINTER(vp)]
         L.wc_service_get_stats.argtypes = [vp, ctypes.POINTER(WcServiceStats)]
         L.wc_service_last_error.argtypes = [vp]
         L.wc_service_last_error.restype = ctypes.c_char_p
@@ -288,17 +290,26 @@ def service_enabled():
     return os.environ.get("WAFFLE_CON_SERVICE", "1") != "0"
 
 
+_service_failed = set()
+
+
 def service(device=None):
     """The process-wide service of `device` (default: the default context's
-    device), created on first use and closed at exit."""
+    device), created on first use and closed at exit. None when it cannot be
+    created (e.g. its pinned arena): the callers then take the per-call batch
+    path, as with WAFFLE_CON_SERVICE=0."""
     if device is None:
         device = default_context().device
     svc = _services.get(device)
-    if svc is None:
+    if svc is None and device not in _service_failed:
         with _lock:
             svc = _services.get(device)
-            if svc is None:
-                svc = Service(device)
+            if svc is None and device not in _service_failed:
+                try:
+                    svc = Service(device)
+                except WaffleConError:
+                    _service_failed.add(device)
+                    return None
                 _services[device] = svc
                 if len(_services) == 1:
                     import atexit

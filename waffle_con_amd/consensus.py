@@ -194,8 +194,11 @@ def _problems(batch):
 def _service_call(fn, problem, config):
     """One locus through the submission service (wc_service_consensus /
     wc_service_dual_consensus): blocks this thread only (the GIL is released
-    while it waits). Returns the one-problem result set and its stats."""
+    while it waits). Returns the one-problem result set and its stats, or
+    None when the device has no service (the caller takes the batch path)."""
     svc = _lib.service()
+    if svc is None:
+        return None
     L = _lib.lib()
     arr, keep = _problems([problem])
     cfg = _lib.make_config(config)
@@ -269,10 +272,11 @@ class ConsensusDWFA:
         service (any number of threads share the device; WAFFLE_CON_SERVICE=0:
         one batch call per locus instead)."""
         offs = self._offsets if any(o is not None for o in self._offsets) else None
-        if _lib.service_enabled():
-            (res,), stats = _service_call("wc_service_consensus", (self._sequences, offs), self._config)
-        else:
-            (res,), stats = consensus_batch([(self._sequences, offs)], self._config)
+        out = _service_call("wc_service_consensus", (self._sequences, offs), self._config) \
+            if _lib.service_enabled() else None
+        if out is None:
+            out = consensus_batch([(self._sequences, offs)], self._config)
+        (res,), stats = out
         self.last_stats = stats
         return res
 

@@ -110,7 +110,7 @@ struct Ctl {
   int32_t store_idx;
   uint32_t cache_slot, cache_hit, cache_nend, cache_multi;
   uint32_t hot_slot;  // slot whose RStates are held in Lds::hot (authoritative), kNoSlot = none
-  uint32_t hot_prev, hot_load;
+  uint32_t hot_prev, hot_load, hot_prev_dual;
   // linear-chain run-ahead (run_chain)
   uint32_t chain_k, chain_slot, chain_stop, chain_novf, chain_nochain, chain_len, chain_nbak;
   uint32_t chain_kcur;  // dual engine: the next chain's length (doubles after a fully accepted chain)
@@ -175,7 +175,7 @@ struct Ctl {
 #endif
 
 struct Lds {
-  Sh<RState>* hot;       // [sides][nmax] RStates of the node being expanded (single engine)
+  Sh<RState>* hot;       // [hot_sides][nmax] RStates of the node being expanded (single engine; dual_hot)
   Sh<ChainStep>* cstep;  // chain area (single engine with A.chain > 0)
   Sh<ChainOvf>* covf;
   Sh<RState>* ctmp;      // [kEW]
@@ -193,11 +193,12 @@ struct Lds {
   Sh<uint16_t>* ce;    // dual: [kNCB * 2][nmax] edit distances of the children being built (prune + cost; kCeNone = None)
 };
 
-__device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t K) {
+__device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t K,
+                            uint32_t dual_hot) {
   Lds l;
   Sh<uint8_t>* p = smem;
   l.hot = (Sh<RState>*)p;
-  p += (uint64_t)hot_sides(sides, K) * nmax * sizeof(RState);
+  p += (uint64_t)hot_sides(sides, K, dual_hot) * nmax * sizeof(RState);
   l.cstep = (Sh<ChainStep>*)p;
   l.covf = nullptr;
   l.ctmp = nullptr;
@@ -494,7 +495,7 @@ __device__ inline Eng make_eng(const EngineArgs& A, Sh<uint8_t>* smem) {
   E.act_scr = A.act_scr ? (Gm<uint64_t>*)A.act_scr + (uint64_t)blockIdx.x * A.act_stride +
                               (uint64_t)wave_id() * 2 * A.act_m * 64
                         : nullptr;
-  E.L = carve(smem, A.sides, A.pcap, A.nmax, A.chain);
+  E.L = carve(smem, A.sides, A.pcap, A.nmax, A.chain, A.dual_hot);
   if (A.stream) {
     // the claimed problem's read table is copied here (stream_claim)
     Gm<uint8_t>* t = E.ws + ws_bytes(A.sides, A.pcap, A.nmax, A.wcap, A.lcap);
@@ -978,19 +979,21 @@ __device__ inline void hot_fetch(Eng& E, uint32_t slot, uint32_t side) {
 }
 
 // ---- clone a node: RState records, live wavefront rows, consensus bytes ----
-// kSrcHot: the source's RStates are the LDS copy; they are then not copied
-// (the clone's push writes the child's RStates straight into its slot).
-template <bool kSrcHot>
+// kSrcHot / kDstHot: the source's / destination's RStates are the LDS copy of
+// the node being expanded. kCopyRs: copy the RStates too (the single engine's
+// clones do not: their push writes the child's RStates straight into the slot).
+template <bool kSrcHot, bool kDstHot = false, bool kCopyRs = !kSrcHot>
 __device__ inline void copy_side(Eng& E, uint32_t src, uint32_t ssrc, uint32_t dst, uint32_t sdst, uint32_t len) {
   SideView a = E.sv(src, ssrc), b = E.sv(dst, sdst);
   const auto ars = node_rs<kSrcHot>(E, src, ssrc);
+  const auto brs = node_rs<kDstHot>(E, dst, sdst);
   copy_bytes(b.con, a.con, len);
   // thread per read: its RState, then its wavefront row in 16-byte moves with
   // eight loads in flight, so the reads' copies overlap instead of queueing
   // behind one wave per read (rows are 16-byte aligned: wcap % 64 == 0)
   for (uint32_t r = threadIdx.x; r < E.n; r += kEB) {
     const RRaw st = rstate_load(&ars[r]);
-    if (!kSrcHot) rstate_store(&b.rs[r], st);
+    if (kCopyRs) rstate_store(&brs[r], st);
     const uint32_t e = rraw_e(st);
     if (e == kInactive) continue;
     const uint32_t n4 = (2 * e + 1 + 3) >> 2;
@@ -1472,6 +1475,9 @@ __device__ inline void finish_problem(const EngineArgs& A, Lo<Ctl>& ctl, uint8_t
 // its own slot, and the clones copy the parent before the in-place child (the
 // last one) changes it. So each step runs over up to kNCB children in one
 // block-wide pass, and a group of children costs the latency of one.
+// kDH (dual_hot): the popped node's RStates are the LDS copy (Lds::hot); the
+// clones copy them into their slots, the in-place child is pushed there.
+template <bool kDH>
 __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, const SlotMeta& tm, bool tdual,
                                            uint32_t nc) {
   const int tid = threadIdx.x, lane = lane_id();
@@ -1526,10 +1532,13 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     for (uint32_t c = c0; c < c0 + cn; ++c) {
       const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       if (slot != top) {
-        copy_side<false>(E, top, 0, slot, 0, tm.len[0]);
-        if (tdual) copy_side<false>(E, top, 1, slot, 1, tm.len[1]);
+        copy_side<kDH, false, true>(E, top, 0, slot, 0, tm.len[0]);
+        if (tdual) copy_side<kDH, false, true>(E, top, 1, slot, 1, tm.len[1]);
       }
-      if (uni((uint32_t)ctl.ch_kind[c]) == 2) copy_side<false>(E, top, 0, slot, 1, tm.len[0]);
+      if (uni((uint32_t)ctl.ch_kind[c]) == 2) {
+        if (kDH && slot == top) copy_side<true, true, true>(E, top, 0, top, 1, tm.len[0]);
+        else copy_side<kDH, false, true>(E, top, 0, slot, 1, tm.len[0]);
+      }
     }
     __syncthreads();
     PH_MARK(4);
@@ -1554,11 +1563,13 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       const uint32_t olen = uni(E.L.meta[slot].len[sd]);
       SideView v = E.sv(slot, sd);
+      // the in-place child's RStates: the LDS copy (kDH), else its slot
+      auto push_pass = [&](auto rsb) {
       for (uint32_t base = 0; base < n; base += kEB) {
         const uint32_t r = base + tid;
         uint32_t kind = 0;  // 1: group list, 2: wave list
         if (r < n) {
-          const RRaw s = rstate_load(&v.rs[r]);
+          const RRaw s = rstate_load(&rsb[r]);
           if (rraw_e(s) == kInactive) ceq[r] = (uint16_t)kCeNone;
           if (rraw_e(s) != kInactive) {
             if (rraw_flags(s) & kWide) {  // frontier too wide for the register path
@@ -1570,7 +1581,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
               const bool heavy = thread_push(f, GlobalBytes{E.read(r)}, E.rlen(r), olen - 1, (uint8_t)sym,
                                              cfg.wildcard, early, v.wf + (uint64_t)r * E.wcap, cmp);
               tc.compares += cmp;
-              front_store(&v.rs[r], f);
+              front_store(&rsb[r], f);
               if (heavy) {
                 kind = 2 * f.e + 3 <= kRow16 ? 1u : 2u;
               } else {
@@ -1586,6 +1597,9 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         if (kind == 1) E.L.list[WC_IX(kg, list_entries(E.sides, E.nmax))] = q * n + r;
         if (kind == 2) E.L.list[WC_IX(lend - kw, list_entries(E.sides, E.nmax))] = q * n + r;
       }
+      };
+      if constexpr (kDH) push_pass(slot == top ? rs_generic(E.L.hot + sd * E.nmax) : rs_generic(v.rs));
+      else push_pass(v.rs);
     }
     flush_thread_counters(ctl, tc);
     __syncthreads();
@@ -1607,8 +1621,15 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t c = c0 + q / 2, sd = q & 1u;
       const uint32_t slot = ctl.ch_slot[c];
       SideView v = E.sv(slot, sd);
-      const GroupOut go = group_edinc(act, &v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
-                                      E.L.meta[slot].len[sd], cfg.wildcard, early, E.wcap);
+      GroupOut go;
+      if constexpr (kDH) {
+        const RSg rp = slot == top ? rs_generic(E.L.hot + sd * E.nmax + r) : rs_generic(&v.rs[r]);
+        go = group_edinc(act, rp, v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con, E.L.meta[slot].len[sd],
+                         cfg.wildcard, early, E.wcap);
+      } else {
+        go = group_edinc(act, &v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
+                         E.L.meta[slot].len[sd], cfg.wildcard, early, E.wcap);
+      }
       const uint32_t g = go.st, e = go.e;
       if (act && (lane & 15) == 0 && g == kG_DONE) E.L.ce[(uint64_t)q * E.nmax + r] = ce16(e);
       gc.edinc += go.edinc;
@@ -1630,8 +1651,16 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         const uint32_t slot2 = uni(ctl.ch_slot[c2]);
         SideView v2 = E.sv(slot2, sd2);
         uint32_t eo = 0;
-        if (!wave_edinc_mem(&v2.rs[r2], v2.wf + (uint64_t)r2 * E.wcap, e2, E.read(r2), E.rlen(r2), v2.con,
-                            uni(E.L.meta[slot2].len[sd2]), cfg.wildcard, early, E.wcap, cnt, eo)) {
+        bool okm;
+        if constexpr (kDH) {
+          const RSg rp = slot2 == top ? rs_generic(E.L.hot + sd2 * E.nmax + r2) : rs_generic(&v2.rs[r2]);
+          okm = wave_edinc_mem(rp, v2.wf + (uint64_t)r2 * E.wcap, e2, E.read(r2), E.rlen(r2), v2.con,
+                               uni(E.L.meta[slot2].len[sd2]), cfg.wildcard, early, E.wcap, cnt, eo);
+        } else {
+          okm = wave_edinc_mem(&v2.rs[r2], v2.wf + (uint64_t)r2 * E.wcap, e2, E.read(r2), E.rlen(r2), v2.con,
+                               uni(E.L.meta[slot2].len[sd2]), cfg.wildcard, early, E.wcap, cnt, eo);
+        }
+        if (!okm) {
           if (lane == 0) atomicOr(&ctl.ovf, 4u);
         } else if (lane == 0) {
           E.L.ce[(uint64_t)q2 * E.nmax + r2] = ce16(eo);
@@ -1654,9 +1683,17 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       SideView v = E.sv(slot, sd);
       uint32_t e = 0;
-      if (!wave_heavy(&v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
-                      uni(E.L.meta[slot].len[sd]), (uint8_t)uni((int32_t)ctl.ch_s[c][sd]), cfg.wildcard, early,
-                      E.wcap, cnt, e)) {
+      bool okh;
+      if constexpr (kDH) {
+        const RSg rp = slot == top ? rs_generic(E.L.hot + sd * E.nmax + r) : rs_generic(&v.rs[r]);
+        okh = wave_heavy(rp, v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con, uni(E.L.meta[slot].len[sd]),
+                         (uint8_t)uni((int32_t)ctl.ch_s[c][sd]), cfg.wildcard, early, E.wcap, cnt, e);
+      } else {
+        okh = wave_heavy(&v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
+                         uni(E.L.meta[slot].len[sd]), (uint8_t)uni((int32_t)ctl.ch_s[c][sd]), cfg.wildcard, early,
+                         E.wcap, cnt, e);
+      }
+      if (!okh) {
         if (lane == 0) atomicOr(&ctl.ovf, 4u);
       } else if (lane == 0) {
         E.L.ce[(uint64_t)q * E.nmax + r] = ce16(e);
@@ -1674,8 +1711,13 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t nl0 = uni(E.L.meta[slot].len[0]), nl1 = uni(E.L.meta[slot].len[1]);
       if (max(nl0, nl1) > E.P.max_act) continue;
       activated = true;
-      activate_side<false>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
-      if (uni(E.L.meta[slot].flags) & 1u) activate_side<false>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
+      if (kDH && slot == top) {
+        activate_side<true>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
+        if (uni(E.L.meta[slot].flags) & 1u) activate_side<true>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
+      } else {
+        activate_side<false>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
+        if (uni(E.L.meta[slot].flags) & 1u) activate_side<false>(E, ctl, slot, 1, nl1, max(nl0, nl1), false, nullptr);
+      }
     }
     PH_MARK(10);
     // prune + priority of every child of the group in one pass; every
@@ -1698,6 +1740,12 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
 #endif
     uint64_t ccost[kNCB] = {0, 0, 0, 0};
     uint32_t cn0[kNCB] = {0, 0, 0, 0}, cn1[kNCB] = {0, 0, 0, 0};
+    // child k's RState of read r on side sd (kDH: the in-place child's is the LDS copy)
+    auto crs_e = [&](uint32_t k, uint32_t sd, uint32_t r) -> auto& {
+      if constexpr (kDH)
+        return (cslot[k] == top ? rs_generic(&E.L.hot[sd * E.nmax + r]) : rs_generic(&E.sv(cslot[k], sd).rs[r]))->e;
+      else return E.sv(cslot[k], sd).rs[r].e;
+    };
     for (uint32_t r = tid; r < n; r += kEB) {
       uint32_t e1[kNCB], e2[kNCB];
 #pragma unroll
@@ -1706,9 +1754,9 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         if (k < cn) {
           // each child's edit distances as its pushes left them (LDS), or
           // from its slot when an activation changed them
-          e1[k] = slot_e ? E.sv(cslot[k], 0).rs[r].e : ce32(E.L.ce[(uint64_t)(2 * k) * E.nmax + r]);
+          e1[k] = slot_e ? crs_e(k, 0, r) : ce32(E.L.ce[(uint64_t)(2 * k) * E.nmax + r]);
           if (cdual & (1u << k))
-            e2[k] = slot_e ? E.sv(cslot[k], 1).rs[r].e : ce32(E.L.ce[(uint64_t)(2 * k + 1) * E.nmax + r]);
+            e2[k] = slot_e ? crs_e(k, 1, r) : ce32(E.L.ce[(uint64_t)(2 * k + 1) * E.nmax + r]);
         }
       }
 #pragma unroll
@@ -1716,10 +1764,10 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         if (k >= cn) continue;
         if ((cdual & (1u << k)) && e1[k] != kInactive && e2[k] != kInactive) {
           if ((uint64_t)e1[k] + cfg.dual_max_ed_delta < (uint64_t)e2[k]) {
-            E.sv(cslot[k], 1).rs[r].e = kInactive;
+            crs_e(k, 1, r) = kInactive;
             e2[k] = kInactive;
           } else if ((uint64_t)e2[k] + cfg.dual_max_ed_delta < (uint64_t)e1[k]) {
-            E.sv(cslot[k], 0).rs[r].e = kInactive;
+            crs_e(k, 0, r) = kInactive;
             e1[k] = kInactive;
           }
         }
@@ -2036,10 +2084,11 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
 // =====================================================================
 // DualConsensusDWFA engine (dual_consensus.rs:240-787)
 // =====================================================================
-__global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ Ctl ctl_lds;
-  Lo<Ctl>& ctl = *(Lo<Ctl>*)&ctl_lds;
+// kDH (EngineArgs::dual_hot): the popped node's RStates (both sides) move into
+// LDS (Lds::hot) and stay there while its in-place child is popped next; the
+// previous hot node is written back to its slot when another node is popped.
+template <bool kDH>
+__device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo<Ctl>& ctl) {
   const int tid = threadIdx.x;
   const int lane = lane_id();
   const DevConfig& cfg = A.cfg;
@@ -2097,6 +2146,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
           if (top.cost > ctl.max_err || top.len < ctl.trk_thr[dual] || at_cap || imbalanced) {
             ctl.cnt[S_IGNORED]++;
             E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top.slot;
+            if (kDH && top.slot == ctl.hot_slot) ctl.hot_slot = kNoSlot;  // its LDS state is dropped
             ctl.action = 1;
           } else {
             ctl.farthest[dual] = max(ctl.farthest[dual], (uint64_t)top.len);
@@ -2104,6 +2154,15 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
             t.process_unchecked(top.len);
             ctl.cnt[S_EXPLORED]++;
             ctl.action = 0;
+            if (kDH) {
+              // the popped node moves into LDS unless it is there already
+              // (the in-place child of the previous pop); the previous hot
+              // node (still queued) goes back to its slot first
+              ctl.hot_prev = ctl.hot_slot;
+              ctl.hot_load = top.slot != ctl.hot_slot;
+              ctl.hot_prev_dual = ctl.hot_slot != kNoSlot && (E.L.meta[ctl.hot_slot].flags & 1u) != 0;
+              ctl.hot_slot = top.slot;
+            }
           }
           trace_pop(A, prob, top, dual | (ctl.action << 1) | (m.nsome[0] << 8) | (m.nsome[1] << 20), (uint32_t)am);
         }
@@ -2124,8 +2183,20 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
       const bool tdual = uni(ctl.top_dual) != 0;
       const SlotMeta tm = meta_get(E.L.meta[top]);
       const uint32_t tlens[2] = {tm.len[0], tm.len[1]};
+      if (kDH && uni(ctl.hot_load)) {
+        // per read the same thread stores then fetches; the analysis below
+        // maps items to threads differently, hence the barrier
+        const uint32_t prev = uni(ctl.hot_prev);
+        if (prev != kNoSlot) {
+          hot_store(E, prev, 0);
+          if (uni(ctl.hot_prev_dual)) hot_store(E, prev, 1);
+        }
+        hot_fetch(E, top, 0);
+        if (tdual) hot_fetch(E, top, 1);
+        __syncthreads();
+      }
 
-      analyze_sides<false>(E, ctl, top, tdual ? 2 : 1, tlens[0], tlens[1], R0, R1);
+      analyze_sides<kDH>(E, ctl, top, tdual ? 2 : 1, tlens[0], tlens[1], R0, R1);
       // reached_all_end (dual_consensus.rs:1174-1195): per read, either side at its end
       {
         uint32_t ne = 0;
@@ -2148,8 +2219,8 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
       // ---- finalize a clone (dual_consensus.rs:438-492) ----
       if (uni(ctl.reached)) {
         WaveCounters cnt = {0, 0, 0, 0, 0, 0};
-        finalize_side<false>(E, ctl, top, 0, tlens[0], E.L.fe, cnt);
-        if (tdual) finalize_side<false>(E, ctl, top, 1, tlens[1], E.L.fe + E.nmax, cnt);
+        finalize_side<kDH>(E, ctl, top, 0, tlens[0], E.L.fe, cnt);
+        if (tdual) finalize_side<kDH>(E, ctl, top, 1, tlens[1], E.L.fe + E.nmax, cnt);
         flush_counters(ctl, cnt);
         __syncthreads();
         if (tid == 0) {
@@ -2319,7 +2390,10 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
       if (uni(ctl.status) != ST_OK) break;
       const uint32_t nc = uni(ctl.nchild);
       if (nc == 0) {
-        if (tid == 0) E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top;
+        if (tid == 0) {
+          E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top;
+          if (kDH) ctl.hot_slot = kNoSlot;
+        }
         __syncthreads();
         continue;
       }
@@ -2363,7 +2437,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
 
       // ---- build every child: clones first, the last child in place ----
       SUB_CNT(21, nc);
-      dual_build_children(E, ctl, top, tm, tdual, nc);
+      dual_build_children<kDH>(E, ctl, top, tm, tdual, nc);
       if (uni(ctl.status) != ST_OK) break;
       if (tid == 0) {
         for (uint32_t c = 0; c < nc; ++c) {
@@ -2379,6 +2453,21 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
   }
   stream_exit(A);
 }
+
+// two kernels, one per dual_hot: in one kernel the two paths' register
+// allocations merge (the 4-wave build spilled 236 VGPRs instead of 84)
+__global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Ctl ctl_lds;
+  dual_main<false>(A, smem, *(Lo<Ctl>*)&ctl_lds);
+}
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_DUAL_CHAIN_CALL)  // (the host plans dual_hot for neither build)
+__global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_hot_engine_kernel(EngineArgs A) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Ctl ctl_lds;
+  dual_main<true>(A, smem, *(Lo<Ctl>*)&ctl_lds);
+}
+#endif
 
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT)
 // =====================================================================
@@ -2441,12 +2530,22 @@ void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStr
   hipLaunchKernelGGL(single_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_DUAL_CHAIN_CALL)
+  if (a.dual_hot) {
+    hipLaunchKernelGGL(dual_hot_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
+    return;
+  }
+#endif
   hipLaunchKernelGGL(dual_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
-int engine_blocks_per_cu(uint32_t sides, size_t lds) {
+int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot) {
   int nb = 0;
-  hipError_t e = sides == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kEB, lds)
-                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kEB, lds);
+  hipError_t e = hipSuccess;
+  if (sides == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kEB, lds);
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_DUAL_CHAIN_CALL)
+  else if (dual_hot) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_hot_engine_kernel, kEB, lds);
+#endif
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kEB, lds);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT)

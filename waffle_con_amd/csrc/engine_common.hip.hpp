@@ -224,6 +224,27 @@ __device__ __forceinline__ void rstate_store(Sh<RState>* p, const RRaw& s) {
   q[3] = s.d;
 }
 #endif
+// A node's RStates through a generic (flat) pointer: the dual engine's
+// in-place child lives in the LDS copy of the popped node (dual_hot), its
+// clones in their HBM slots, and the same pass handles both
+using RSg = RState*;
+template <class P>
+__device__ __forceinline__ RSg rs_generic(P p) {
+  return (RSg)p;
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ RRaw rstate_load(const RState* p) {
+  const uint4* q = (const uint4*)p;
+  return RRaw{q[0], q[1], q[2], q[3]};
+}
+__device__ __forceinline__ void rstate_store(RState* p, const RRaw& s) {
+  uint4* q = (uint4*)p;
+  q[0] = s.a;
+  q[1] = s.b;
+  q[2] = s.c;
+  q[3] = s.d;
+}
+#endif
 __device__ __forceinline__ uint32_t rraw_e(const RRaw& s) { return s.a.x; }
 __device__ __forceinline__ uint32_t rraw_flags(const RRaw& s) { return s.a.w >> 24; }
 
@@ -980,7 +1001,10 @@ struct GroupCnt {
 struct GroupOut {
   uint32_t st, e, edinc, updates, w_out, cmp, rowb;
 };
-__device__ __noinline__ GroupOut group_edinc(bool act, Gm<RState>* rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd,
+// (P: the RState pointer, an HBM slot or, dual_hot, a generic pointer that
+// may point into the LDS copy of the popped node)
+template <class P>
+__device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd,
                                              uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc,
                                              bool early, uint32_t wcap) {
   GroupOut go_ = {kG_DONE, 0, 0, 0, 0, 0, 0};

@@ -137,11 +137,32 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   const char* lenv = getenv("WC_LOWLAT");
   c.lowlat = !gstate && !c.narrow && ids.size() <= 2ull * (uint64_t)ctx->n_cu && !(lenv && atoi(lenv) == 0);
   if (sides == 2 && chain > 0 && !gstate) c.narrow = c.lowlat = false;  // the chain build (wcd)
+  c.dual_hot = false;
   auto occupancy = [&](size_t l) {
     if (sides == 2 && chain > 0 && !gstate) return wcd::engine_blocks_per_cu(sides, l);
-    return c.narrow ? wcn::engine_blocks_per_cu(sides, l)
-                    : (c.lowlat ? wcl::engine_blocks_per_cu(sides, l) : engine_blocks_per_cu(sides, l));
+    return c.narrow ? wcn::engine_blocks_per_cu(sides, l, c.dual_hot)
+                    : (c.lowlat ? wcl::engine_blocks_per_cu(sides, l, c.dual_hot)
+                                : engine_blocks_per_cu(sides, l, c.dual_hot));
   };
+  // dual_hot: the dual engine keeps the popped node's RStates (2 x nmax x 64 B)
+  // in LDS, where its in-place child is pushed and, most of the time, popped
+  // next (no RState round trip to HBM). Measured not to pay (the
+  // heaviest cfg5 sub-problem alone, 37.9k vs 36.8k cycles per pop; the
+  // RState loads hit L2 and are not the per-pop critical path), so it is off
+  // by default: WC_DUAL_HOT=1 turns it on where it costs the launch no
+  // workgroups (same occupancy, or room for every problem anyway),
+  // WC_DUAL_HOT=2 wherever the LDS allows.
+  if (sides == 2 && chain == 0 && !gstate) {
+    const char* henv = getenv("WC_DUAL_HOT");
+    const int hmode = henv ? atoi(henv) : 0;
+    const uint64_t lhot = lds_bytes(sides, pcap, nmax, 0, 1);
+    if (hmode != 0 && lhot <= kLdsMax) {
+      const int occ0 = occupancy((size_t)lds_bytes(sides, pcap, nmax, 0, 0));
+      c.dual_hot = true;
+      const int occ1 = occupancy((size_t)lhot);
+      c.dual_hot = hmode == 2 || occ1 >= occ0 || ids.size() <= (uint64_t)occ1 * ctx->n_cu;
+    }
+  }
   // longer chains amortise the per-chain work (prediction, acceptance, the
   // literal pop between chains); take the longest one whose LDS still gives
   // the workgroups per CU of the default length (results do not depend on it)
@@ -180,7 +201,7 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   }
   c.conc = (uint32_t)conc;
   c.gstate = gstate;
-  c.gsb = align16(lds_bytes(sides, pcap, nmax, chain));
+  c.gsb = align16(lds_bytes(sides, pcap, nmax, chain, c.dual_hot));
   c.lds = gstate ? 0 : (size_t)c.gsb;
   c.per_cu = gstate ? wcg::engine_blocks_per_cu(sides, 0) : occupancy(c.lds);
   c.wsb = ws_bytes(sides, pcap, nmax, c.wcap, c.lcap);
@@ -378,6 +399,7 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   a.rmax = caps.rmax;
   a.chain = caps.chain;
   a.chain_kinds = env_chain_kinds();
+  a.dual_hot = caps.dual_hot ? 1u : 0u;
   a.out = dh + L.off_out;
   a.out_stride = caps.ob;
   a.status = (uint32_t*)(dh + L.off_status);
@@ -396,8 +418,8 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
-            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
+    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d dual_hot=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
+            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, (int)caps.dual_hot, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
   return WC_OK;
 }
 
@@ -652,6 +674,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.rmax = caps.rmax;
   a.chain = caps.chain;  // the device carves LDS from it: must match caps.lds
   a.chain_kinds = env_chain_kinds();
+  a.dual_hot = caps.dual_hot ? 1u : 0u;
   a.out = dh + L.off_out;
   a.out_stride = caps.ob;
   a.status = (uint32_t*)(dh + L.off_status);
@@ -671,9 +694,9 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u narrow=%d lowlat=%d\n",
+    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u narrow=%d lowlat=%d dual_hot=%d\n",
             L.grid, caps.per_cu, caps.lds, caps.pcap, caps.wcap, caps.lcap, caps.nmax, caps.rmax, (int)caps.narrow,
-            (int)caps.lowlat);
+            (int)caps.lowlat, (int)caps.dual_hot);
 
   // publication state: seq -> item, read-ring position; incomplete seqs in order
   std::vector<uint32_t> seq_item;
@@ -801,11 +824,6 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
 // PriorityConsensusDWFA (priority_consensus.rs:172-341), streamed
 // ---------------------------------------------------------------------------
 namespace {
-// FxHashSet<Option<usize>> iteration order of the seed groups (priority_consensus.rs:180).
-// The set is built by `.collect()`: hashbrown's extend first reserves the
-// iterator's exact size hint (one entry per chain), so the table starts with
-// capacity_to_buckets(n_chains) buckets and never grows while the (at most
-// n_chains) distinct keys are inserted.
 uint64_t fx_add(uint64_t h, uint64_t w) { return (((h << 5) | (h >> 59)) ^ w) * 0x517cc1b727220a95ULL; }
 uint64_t fx_hash_opt(int64_t v) { return v < 0 ? fx_add(0, 0) : fx_add(fx_add(0, 1), (uint64_t)v); }
 size_t fx_cap_h(size_t b) { return b == 0 ? 0 : (b < 8 ? b - 1 : b / 8 * 7); }
@@ -815,6 +833,12 @@ size_t fx_buckets_h(size_t cap) {
   while (p < adj) p <<= 1;
   return p;
 }
+}  // namespace
+// FxHashSet<Option<usize>> iteration order of the seed groups (priority_consensus.rs:180).
+// The set is built by `.collect()`: hashbrown's extend first reserves the
+// iterator's exact size hint (one entry per chain), so the table starts with
+// capacity_to_buckets(n_chains) buckets and never grows while the (at most
+// n_chains) distinct keys are inserted.
 std::vector<int64_t> seed_order(const std::vector<int64_t>& groups) {
   std::vector<int64_t> keys;
   std::vector<uint64_t> hashes;
@@ -859,6 +883,33 @@ std::vector<int64_t> seed_order(const std::vector<int64_t>& groups) {
   return out;
 }
 
+// priority_consensus.rs:309-335: the finished chains of one problem (and
+// which input chains each covers) into its result: chains stable-sorted by
+// their consensus sequences, sequence_indices per input chain
+void priority_assemble(uint32_t M, std::vector<std::vector<ConsRec>>& C, std::vector<std::vector<uint8_t>>& assigns,
+                       ProbRes& pr) {
+  if (C.size() > 1) {
+    std::vector<size_t> ord(C.size());
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+      size_t m = std::min(C[a].size(), C[b].size());
+      for (size_t l = 0; l < m; ++l)
+        if (C[a][l].seq != C[b][l].seq) return C[a][l].seq < C[b][l].seq;
+      return C[a].size() < C[b].size();
+    });
+    pr.indices.assign(M, UINT64_MAX);
+    for (size_t ci = 0; ci < ord.size(); ++ci) {
+      for (uint32_t c = 0; c < M; ++c)
+        if (assigns[ord[ci]][c]) pr.indices[c] = ci;
+      pr.chains.push_back(C[ord[ci]]);
+    }
+  } else {
+    pr.chains = C;
+    pr.indices.assign(M, 0);
+  }
+}
+
+namespace {
 // one stacked sub-problem: a read subset at a chain level
 struct PWork {
   uint32_t owner = 0;
@@ -871,6 +922,7 @@ struct PWork {
 }  // namespace
 
 int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chain_problem* problems, wc_results* R) {
+  const auto t_call = std::chrono::steady_clock::now();
   R->probs.resize(n);
   // 1. every read of every problem (all chain levels) resident in one arena:
   //    read (problem i, chain c, level l) = arena read base[i] + c * levels + l
@@ -993,6 +1045,11 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
       }
       w.res.reset();
     }
+    // the problem's result is final: record when (tail latency in the bench)
+    if (!alive[i] || stacks[i].empty())
+      if (R->probs[i].done_ms == 0)
+        R->probs[i].done_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
   };
 
   // 3. epochs of one persistent engine launch each (engine.hip stream mode):
@@ -1103,28 +1160,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
   for (uint32_t i = 0; i < n; ++i) {
     ProbRes& pr = R->probs[i];
     if (pr.status != WC_OK) continue;
-    const uint32_t M = problems[i].n_chains;
-    auto& C = cons[i];
-    if (C.size() > 1) {
-      // priority_consensus.rs:309-335: stable sort of the chains
-      std::vector<size_t> ord(C.size());
-      std::iota(ord.begin(), ord.end(), 0);
-      std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
-        size_t m = std::min(C[a].size(), C[b].size());
-        for (size_t l = 0; l < m; ++l)
-          if (C[a][l].seq != C[b][l].seq) return C[a][l].seq < C[b][l].seq;
-        return C[a].size() < C[b].size();
-      });
-      pr.indices.assign(M, UINT64_MAX);
-      for (size_t ci = 0; ci < ord.size(); ++ci) {
-        for (uint32_t c = 0; c < M; ++c)
-          if (assigns[i][ord[ci]][c]) pr.indices[c] = ci;
-        pr.chains.push_back(C[ord[ci]]);
-      }
-    } else {
-      pr.chains = C;
-      pr.indices.assign(M, 0);
-    }
+    priority_assemble(problems[i].n_chains, cons[i], assigns[i], pr);
   }
   R->stats.kernel_ms = kms;
   R->stats.launches = nl;

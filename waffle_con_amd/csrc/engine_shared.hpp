@@ -92,6 +92,7 @@ struct EngineArgs {
   uint32_t rmax;         // result records per problem
   uint32_t chain;        // max linear-chain run-ahead steps (0 = off); sizes the LDS chain area
   uint32_t chain_kinds;  // dual engine: bit 0 chains over single-consensus nodes, bit 1 over dual nodes
+  uint32_t dual_hot;     // dual engine (chain == 0): the popped node's RStates live in LDS (hot_sides)
   uint8_t* out;
   uint64_t out_stride;
   uint32_t* status;      // per problem
@@ -282,14 +283,18 @@ __host__ __device__ inline uint64_t list_entries(uint32_t sides, uint32_t nmax) 
 }
 // sides whose expanded node's RStates are held in LDS: the single engine's
 // popped node; in the dual engine side 1 of a single-consensus node for its
-// chain walk (chain > 0; the two-sided walk reads the slot)
-__host__ __device__ inline uint32_t hot_sides(uint32_t sides, uint32_t chain) {
-  return (sides == 1 || chain > 0) ? 1u : 0u;
+// chain walk (chain > 0; the two-sided walk reads the slot), or, with
+// `dual_hot` (EngineArgs::dual_hot, no chains), both sides of the popped node
+// (its in-place child is pushed there and usually popped next)
+__host__ __device__ inline uint32_t hot_sides(uint32_t sides, uint32_t chain, uint32_t dual_hot = 0) {
+  if (sides == 1 || chain > 0) return 1u;
+  return dual_hot ? 2u : 0u;
 }
 // LDS: hot RStates[hot_sides][nmax] | chain area | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
 //      heavy list[list_entries] u32 | (dual) child e[kDualChildBatch][2][nmax] u16
-__host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t chain) {
-  uint64_t t = (uint64_t)hot_sides(sides, chain) * nmax * sizeof(RState);
+__host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t chain,
+                                              uint32_t dual_hot = 0) {
+  uint64_t t = (uint64_t)hot_sides(sides, chain, dual_hot) * nmax * sizeof(RState);
   t += chain_lds_bytes(nmax, chain, sides);
   t += (uint64_t)pcap * sizeof(HeapEntry);
   t += align16((uint64_t)pcap * 4);

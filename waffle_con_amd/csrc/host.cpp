@@ -267,6 +267,7 @@ int batch_run(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, wc
     R->p_sc0.assign(n, ~0ull);
   }
   const std::function<void(uint32_t)> build = [&](uint32_t i) {
+    R->probs[i].done_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (sides == 1) {
       build_single(outs[i], cfg.consensus_cost, R->probs[i]);
       pack_single(R, i);
@@ -595,6 +596,7 @@ int wc_results_problem_stats(const wc_results* r, uint32_t p, wc_stats* o) {
   o->nodes_ignored = s[S_IGNORED];
   o->peak_queue_size = s[S_PEAKQ];
   o->row_bytes = s[S_ROWB];
+  o->wall_ms = r->probs[p].done_ms;
   return WC_OK;
 }
 

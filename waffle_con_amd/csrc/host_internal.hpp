@@ -16,7 +16,7 @@
 namespace wc {
 void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
-int engine_blocks_per_cu(uint32_t sides, size_t lds);
+int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s);
 void launch_wfa_ed_batch(const EdDevJob* jobs, uint32_t n, const uint8_t* seqs, uint64_t* scratch, int wc,
                          uint32_t both, uint64_t* out, hipStream_t s);
@@ -24,22 +24,22 @@ void launch_wfa_ed_batch(const EdDevJob* jobs, uint32_t n, const uint8_t* seqs, 
 namespace wcg {  // engine_gstate.hip: search state in HBM
 void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
-int engine_blocks_per_cu(uint32_t sides, size_t lds);
+int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 }  // namespace wcg
 namespace wcn {  // engine_narrow.hip: 128-thread workgroups (problems of <= 128 reads)
 void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
-int engine_blocks_per_cu(uint32_t sides, size_t lds);
+int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 }  // namespace wcn
 namespace wcl {  // engine_lowlat.hip: 256-thread workgroups at 2 waves/SIMD (launches with few problems)
 void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
-int engine_blocks_per_cu(uint32_t sides, size_t lds);
+int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 }  // namespace wcl
 namespace wcd {  // engine_dchain.hip: the dual engine with chains (launches with caps.chain > 0)
 void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
-int engine_blocks_per_cu(uint32_t sides, size_t lds);
+int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 }  // namespace wcd
 
 // device buffer, grown on demand (never shrinks)
@@ -145,6 +145,7 @@ struct ProbRes {
   std::vector<std::vector<ConsRec>> chains;
   std::vector<uint64_t> indices;
   uint64_t stats[wc::S_NSTAT] = {0};
+  double done_ms = 0;  // from the start of the call until this problem's result was final
 };
 struct wc_results {
   int kind = 0;  // 0 single, 1 dual, 2 priority
@@ -216,6 +217,11 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
                     wc_results* R);
 
 void destroy_launches(wc_ctx* ctx);
+// FxHashSet<Option<usize>> iteration order of seed groups (priority_consensus.rs:180)
+std::vector<int64_t> seed_order(const std::vector<int64_t>& groups);
+// priority_consensus.rs:309-335: finished chains -> sorted chains + sequence_indices
+void priority_assemble(uint32_t n_chains, std::vector<std::vector<ConsRec>>& chains,
+                       std::vector<std::vector<uint8_t>>& assigns, ProbRes& pr);
 bool dual_from_record(const RawRecord& rr, uint32_t n, int mode, DualRec& d);
 void build_single(const EngineOut& E, int mode, ProbRes& pr);
 // appends problem p's single results to the arenas (wc_results::a_seq/a_sc)

@@ -30,6 +30,7 @@ struct Caps {
   bool gstate = false;  // search state in HBM (engine_gstate.hip): it does not fit LDS
   bool narrow = false;  // 128-thread build (engine_narrow.hip)
   bool lowlat = false;  // 256-thread build at 2 waves/SIMD (engine_lowlat.hip)
+  bool dual_hot = false;  // dual engine: the popped node's RStates in LDS (EngineArgs::dual_hot)
   uint64_t gsb = 0;     // its bytes per workgroup
   uint32_t conc = 0;    // workgroups the HBM share was planned for
   bool pool_short = false;  // a retried item's node pool did not get its full growth

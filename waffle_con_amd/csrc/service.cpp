@@ -33,11 +33,20 @@
 // one lane's buffers while another runs deadlocks: hipFree waits for every
 // kernel on the device, and a lane's kernel only ends when the service thread
 // says so.) Offsets (add_sequence_offset), problems that still ask for more
-// capacity (ST_RETRY) and any service failure take the batch path on a
-// per-thread context (wc_consensus_batch with one problem), which plans and
-// retries capacities as usual: results never depend on the path. A lane that
-// cannot start (HBM) sends its requests there too, after one retry with the
-// lane's cached buffers released.
+// capacity (ST_RETRY) and any service failure take the batch path
+// (wc_consensus_batch with one problem, which plans and retries capacities as
+// usual: results never depend on the path). The service thread runs it, on
+// its own context, while no lane runs: a batch kernel next to a running lane
+// would find the CUs held by the lane's waiting workgroups, and a buffer
+// resize (hipFree) would wait for the lane itself. A lane that cannot start
+// (HBM) sends its requests there too, after one retry with the lane's cached
+// buffers released.
+//
+// PriorityConsensusDWFA::consensus (priority_consensus.rs:172-341) is served
+// the same way (wc_service_priority_consensus): the caller's thread keeps the
+// reference's LIFO work stack and submits every DualConsensusDWFA sub-problem
+// to the dual lane as soon as it exists (a split's two groups run at once),
+// unwinding the stack in the reference's order as the tops finish.
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -58,7 +67,7 @@ namespace {
 constexpr uint32_t kQcap = 1u << 14;      // published, unfinished problems per lane
 constexpr uint32_t kQslots = 1u << 21;    // their read-table entries
 constexpr double kIdleMs = 2.0;           // a lane with nothing to do stops after this
-constexpr uint64_t kArenaDefault = 1ull << 30;  // pinned host memory for in-flight callers' reads
+constexpr uint64_t kArenaDefault = 256ull << 20;  // pinned host memory for in-flight callers' reads
 
 using Clock = std::chrono::steady_clock;
 
@@ -69,10 +78,17 @@ struct Req {
   std::vector<uint64_t> roff;  // arena offsets of the reads
   std::vector<uint32_t> rlen;
   uint64_t aoff = 0;           // arena reservation
+  bool in_arena = false;       // holds it
   bool done = false;
   uint32_t st = 0;             // raw device status (ST_RETRY flags included; ~0u = service failure)
   EngineOut out;
   std::condition_variable cv;
+  // the batch path, run by the service thread: the caller's problem (valid
+  // until the request completes) and the outcome
+  const wc_problem* fb_p = nullptr;
+  bool fb = false;
+  wc_results* fb_res = nullptr;
+  int fb_rc = WC_OK;
 };
 
 bool same_cfg(const wc_config& a, const wc_config& b) { return memcmp(&a, &b, sizeof(wc_config)) == 0; }
@@ -108,6 +124,9 @@ struct wc_service {
   std::condition_variable cv_svc;    // requests arrived
   std::condition_variable cv_arena;  // arena space was released
   std::deque<Req*> ready;            // copied to the arena, not yet published (FIFO)
+  std::deque<Req*> fbq;              // batch-path requests (run by the service thread, no lane running)
+  uint32_t inflight = 0;             // calls inside the service (destroy waits for them)
+  std::condition_variable cv_idle;   // inflight reached 0
   HostBuf arena;                     // pinned, host-mapped: callers' reads (the lanes pull them)
   const uint8_t* arena_dev = nullptr;  // its device address
   std::map<uint64_t, uint64_t> live;  // arena reservations: offset -> bytes
@@ -156,8 +175,11 @@ bool arena_alloc(wc_service* S, uint64_t b, uint64_t& off) {
 void complete(wc_service* S, Req* q, uint32_t st) {
   q->st = st;
   q->done = true;
-  S->live.erase(q->aoff);
-  S->cv_arena.notify_all();
+  if (q->in_arena) {
+    S->live.erase(q->aoff);
+    q->in_arena = false;
+    S->cv_arena.notify_all();
+  }
   q->cv.notify_one();
 }
 
@@ -265,6 +287,7 @@ int lane_start(wc_service* S, const Req* q) {
   a.rmax = caps.rmax;
   a.chain = caps.chain;
   a.chain_kinds = env_chain_kinds();
+  a.dual_hot = caps.dual_hot ? 1u : 0u;
   a.out = dh + L->off_out;
   a.out_stride = caps.ob;
   a.status = (uint32_t*)(dh + L->off_status);
@@ -368,7 +391,27 @@ void service_loop(wc_service* S) {
   Clock::time_point last_beat = Clock::now();
   for (;;) {
     bool progress = false;
+    // 0. batch-path requests, one at a time, with no lane running
+    if (!S->fbq.empty() && !ln.running) {
+      Req* f = S->fbq.front();
+      S->fbq.pop_front();
+      S->stats.fallback++;
+      lk.unlock();
+      wc_results* r = nullptr;
+      const int rc = f->sides == 1 ? wc_consensus_batch(S->ctx, &f->cfg, 1, f->fb_p, &r)
+                                   : wc_dual_consensus_batch(S->ctx, &f->cfg, 1, f->fb_p, &r);
+      const std::string e = rc != WC_OK ? std::string(wc_last_error(S->ctx)) : std::string();
+      lk.lock();
+      if (rc != WC_OK) S->err = e;
+      f->fb_rc = rc;
+      f->fb_res = r;
+      f->done = true;
+      f->cv.notify_one();
+      continue;
+    }
     if (ln.running) {
+      // a batch-path request needs the device to itself: the lane drains
+      if (!S->fbq.empty()) ln.draining = true;
       // 1. publish in arrival order; the first request the lane cannot take
       //    (another kind or config, or larger capacities) makes it drain, and
       //    nothing behind that request is published before the restart
@@ -470,54 +513,51 @@ void service_loop(wc_service* S) {
         }
       }
     }
-    if (S->stop && S->ready.empty() && !ln.running) break;
+    if (S->stop && S->ready.empty() && S->fbq.empty() && !ln.running) break;
     if (!progress) {
-      if (!ln.running && S->ready.empty()) S->cv_svc.wait(lk, [&] { return S->stop || !S->ready.empty(); });
+      if (!ln.running && S->ready.empty() && S->fbq.empty())
+        S->cv_svc.wait(lk, [&] { return S->stop || !S->ready.empty() || !S->fbq.empty(); });
       else S->cv_svc.wait_for(lk, std::chrono::microseconds(20));
     }
   }
 }
 
-// the batch path on a per-thread context (offsets, capacity retries, service failures)
-struct ThreadCtx {
-  std::map<int, wc_ctx*> ctx;
-  ~ThreadCtx() {
-    for (auto& kv : ctx) wc_ctx_destroy(kv.second);
+// ---- requests (caller threads) ----
+// An RAII count of the calls inside the service: wc_service_destroy waits
+// until none is left. A call that finds the service stopping fails.
+struct InFlight {
+  wc_service* S;
+  bool ok;
+  explicit InFlight(wc_service* s) : S(s) {
+    std::lock_guard<std::mutex> g(S->mu);
+    ok = !S->stop;
+    if (ok) S->inflight++;
+  }
+  ~InFlight() {
+    if (!ok) return;
+    std::lock_guard<std::mutex> g(S->mu);
+    if (--S->inflight == 0) S->cv_idle.notify_all();
   }
 };
-int fallback(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p, wc_results** out) {
-  static thread_local ThreadCtx tl;
-  wc_ctx*& c = tl.ctx[S->device];
-  if (!c) {
-    const int rc = wc_ctx_create(S->device, &c);
-    if (rc != WC_OK) {
-      c = nullptr;
-      return rc;
-    }
-  }
-  {
-    std::lock_guard<std::mutex> g(S->mu);
-    S->stats.fallback++;
-  }
-  const int rc = sides == 1 ? wc_consensus_batch(c, cfg, 1, p, out) : wc_dual_consensus_batch(c, cfg, 1, p, out);
-  if (rc != WC_OK) {
-    std::lock_guard<std::mutex> g(S->mu);
-    S->err = wc_last_error(c);
-  }
-  return rc;
+
+// queues q for the batch path (the service thread runs it with no lane running)
+void queue_fallback(wc_service* S, Req* q, const wc_problem* p) {
+  std::lock_guard<std::mutex> g(S->mu);
+  q->fb = true;
+  q->fb_p = p;
+  q->done = false;
+  S->fbq.push_back(q);
+  S->cv_svc.notify_one();
 }
 
-int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p, wc_results** out) {
-  *out = nullptr;
-  if (!S || !cfg || !p) return WC_E_BAD_INPUT;
-  const auto t0 = Clock::now();
-  const uint32_t n = p->n_reads;
-  if (n && (!p->reads || !p->lens)) return WC_E_BAD_INPUT;
-  for (uint32_t r = 0; r < n; ++r)
-    if (p->lens[r] >= (1ull << 31) || (p->lens[r] && !p->reads[r])) return WC_E_BAD_INPUT;
+// Submits one problem (no waiting): into a lane through the arena, or to the
+// batch path (offsets, > 256 reads, reads too large for the arena). `p` must
+// stay valid until the request completes.
+std::unique_ptr<Req> submit(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p) {
   std::unique_ptr<Req> q(new Req());
   q->sides = sides;
   q->cfg = *cfg;
+  const uint32_t n = p->n_reads;
   std::vector<int64_t> offs(n, -1);
   if (p->offsets)
     for (uint32_t r = 0; r < n; ++r) offs[r] = p->offsets[r] < 0 ? -1 : p->offsets[r];
@@ -529,7 +569,10 @@ int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_p
   }
   // offsets (activation scratch) and deep problems (> 256 reads: the batch
   // path gives them a launch of their own) take the batch path
-  if (arc != WC_OK || q->sp.max_act > 0 || n > (uint32_t)kBlock) return fallback(S, sides, cfg, p, out);
+  if (arc != WC_OK || q->sp.max_act > 0 || n > (uint32_t)kBlock) {
+    queue_fallback(S, q.get(), p);
+    return q;
+  }
   // reads back to back (16-byte aligned) in a reservation of the pinned
   // arena, written straight from the caller's buffers: the lane's workgroups
   // pull them into HBM when they claim the locus, so a call makes no HIP
@@ -545,9 +588,16 @@ int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_p
     std::unique_lock<std::mutex> lk(S->mu);
     if (total > S->arena.cap / 4) {
       lk.unlock();
-      return fallback(S, sides, cfg, p, out);
+      queue_fallback(S, q.get(), p);
+      return q;
     }
-    S->cv_arena.wait(lk, [&] { return arena_alloc(S, total, q->aoff); });
+    S->cv_arena.wait(lk, [&] { return S->stop || arena_alloc(S, total, q->aoff); });
+    if (S->stop) {  // (the in-flight count keeps the service alive: the request still completes)
+      lk.unlock();
+      queue_fallback(S, q.get(), p);
+      return q;
+    }
+    q->in_arena = true;
   }
   uint8_t* h = (uint8_t*)S->arena.p + q->aoff;
   q->sp.gid.resize(n);
@@ -563,25 +613,180 @@ int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_p
     q->sp.max_len = std::max(q->sp.max_len, q->rlen[r]);
     q->sp.work += len;
   }
+  q->fb_p = p;
+  std::lock_guard<std::mutex> g(S->mu);
+  S->ready.push_back(q.get());
+  S->cv_svc.notify_one();
+  return q;
+}
+
+// Waits for q. A lane outcome that asks for more capacity (ST_RETRY) or a
+// failed lane sends the problem to the batch path and waits again. Returns
+// WC_OK with either q->out (lane) or q->fb_res (batch path) filled, or the
+// batch path's error code.
+int wait_req(wc_service* S, Req* q) {
   {
     std::unique_lock<std::mutex> lk(S->mu);
-    S->ready.push_back(q.get());
-    S->cv_svc.notify_one();
     q->cv.wait(lk, [&] { return q->done; });
-    if (q->st != ~0u && !(q->st & ST_RETRY)) S->stats.served++;
-  }
-  if (q->st == ~0u || (q->st & ST_RETRY)) {
-    {
-      std::lock_guard<std::mutex> g(S->mu);
-      if (q->st != ~0u) S->stats.retried++;
+    if (q->fb) return q->fb_rc;
+    if (q->st != ~0u && !(q->st & ST_RETRY)) {
+      S->stats.served++;
+      return WC_OK;
     }
-    return fallback(S, sides, cfg, p, out);
+    if (q->st != ~0u) S->stats.retried++;
+  }
+  queue_fallback(S, q, q->fb_p);
+  std::unique_lock<std::mutex> lk(S->mu);
+  q->cv.wait(lk, [&] { return q->done; });
+  return q->fb_rc;
+}
+
+int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p, wc_results** out) {
+  *out = nullptr;
+  if (!S || !cfg || !p) return WC_E_BAD_INPUT;
+  const auto t0 = Clock::now();
+  const uint32_t n = p->n_reads;
+  if (n && (!p->reads || !p->lens)) return WC_E_BAD_INPUT;
+  for (uint32_t r = 0; r < n; ++r)
+    if (p->lens[r] >= (1ull << 31) || (p->lens[r] && !p->reads[r])) return WC_E_BAD_INPUT;
+  InFlight in(S);
+  if (!in.ok) return WC_E_HIP;  // the service is shutting down
+  std::unique_ptr<Req> q = submit(S, sides, cfg, p);
+  const int rc = wait_req(S, q.get());
+  if (q->fb) {
+    *out = q->fb_res;
+    return rc;
   }
   std::unique_ptr<wc_results> R(new wc_results());
   R->kind = sides == 1 ? 0 : 1;
   R->probs.resize(1);
   if (sides == 1) build_single(q->out, cfg->consensus_cost, R->probs[0]);
   else build_dual(q->out, n, cfg->consensus_cost, R->probs[0]);
+  fill_stats(R.get(), 0.0, 0, std::chrono::duration<double, std::milli>(Clock::now() - t0).count());
+  *out = R.release();
+  return WC_OK;
+}
+
+// ---- PriorityConsensusDWFA::consensus (priority_consensus.rs:172-341) ----
+// one stacked sub-problem of a call: a read subset at a chain level
+struct PSub {
+  std::vector<uint8_t> inc;
+  uint32_t level = 0;
+  std::vector<ConsRec> chain;
+  std::vector<const uint8_t*> rp;
+  std::vector<uint64_t> rl;
+  std::vector<int64_t> ro;
+  wc_problem wp{};
+  std::unique_ptr<Req> rq;
+};
+
+int service_priority(wc_service* S, const wc_config* cfg, const wc_chain_problem* q, wc_results** out) {
+  *out = nullptr;
+  if (!S || !cfg || !q) return WC_E_BAD_INPUT;
+  const auto t0 = Clock::now();
+  const uint64_t nr = (uint64_t)q->n_chains * q->levels;
+  if (nr && (!q->reads || !q->lens)) return WC_E_BAD_INPUT;
+  for (uint64_t k = 0; k < nr; ++k)
+    if (q->lens[k] >= (1ull << 31) || (q->lens[k] && !q->reads[k])) return WC_E_BAD_INPUT;
+  InFlight in(S);
+  if (!in.ok) return WC_E_HIP;
+  std::unique_ptr<wc_results> R(new wc_results());
+  R->kind = 2;
+  R->probs.resize(1);
+  ProbRes& pr = R->probs[0];
+  if (q->n_chains == 0 || q->levels == 0) {
+    pr.status = WC_E_BAD_INPUT;
+    pr.error = "Must provide a non-empty sequences Vec";
+    fill_stats(R.get(), 0.0, 0, std::chrono::duration<double, std::milli>(Clock::now() - t0).count());
+    *out = R.release();
+    return WC_OK;
+  }
+  std::vector<std::unique_ptr<PSub>> stack;  // the reference's LIFO work stack
+  std::vector<std::vector<ConsRec>> cons;
+  std::vector<std::vector<uint8_t>> assigns;
+  // a new stack entry, submitted at once (it runs while the stack unwinds)
+  auto make = [&](std::vector<uint8_t> inc, uint32_t level, std::vector<ConsRec> chain) {
+    std::unique_ptr<PSub> w(new PSub());
+    w->inc = std::move(inc);
+    w->level = level;
+    w->chain = std::move(chain);
+    for (uint32_t c = 0; c < q->n_chains; ++c) {
+      if (!w->inc[c]) continue;
+      const uint64_t k = (uint64_t)c * q->levels + level;
+      w->rp.push_back(q->reads[k]);
+      w->rl.push_back(q->lens[k]);
+      w->ro.push_back(q->offsets && q->offsets[k] >= 0 ? q->offsets[k] : -1);
+    }
+    w->wp.n_reads = (uint32_t)w->rp.size();
+    w->wp.reads = w->rp.data();
+    w->wp.lens = w->rl.data();
+    w->wp.offsets = w->ro.data();
+    w->rq = submit(S, 2, cfg, &w->wp);
+    stack.push_back(std::move(w));
+  };
+  {
+    std::vector<int64_t> groups(q->n_chains, -1);
+    if (q->seed_groups)
+      for (uint32_t c = 0; c < q->n_chains; ++c) groups[c] = q->seed_groups[c] < 0 ? -1 : q->seed_groups[c];
+    for (int64_t g : seed_order(groups)) {
+      std::vector<uint8_t> inc(q->n_chains);
+      for (uint32_t c = 0; c < q->n_chains; ++c) inc[c] = groups[c] == g;
+      make(std::move(inc), 0, {});
+    }
+  }
+  int rc = WC_OK;
+  while (!stack.empty()) {
+    std::unique_ptr<PSub> w = std::move(stack.back());
+    stack.pop_back();
+    const int wrc = wait_req(S, w->rq.get());
+    ProbRes d;
+    if (wrc != WC_OK) {
+      rc = wrc;
+      break;
+    }
+    if (w->rq->fb) {
+      d = std::move(w->rq->fb_res->probs[0]);
+      wc_results_free(w->rq->fb_res);
+      w->rq->fb_res = nullptr;
+    } else {
+      build_dual(w->rq->out, w->wp.n_reads, cfg->consensus_cost, d);
+    }
+    for (int s = 0; s < S_NSTAT; ++s)
+      pr.stats[s] = s == S_PEAKQ ? std::max(pr.stats[s], d.stats[s]) : pr.stats[s] + d.stats[s];
+    if (d.status != WC_OK) {
+      pr.status = d.status;
+      pr.error = d.error;
+      break;
+    }
+    const DualRec& ch = d.dual[0];
+    if (ch.has_c2) {
+      std::vector<uint8_t> a1(q->n_chains, 0), a2(q->n_chains, 0);
+      size_t idx = 0;
+      for (uint32_t c = 0; c < q->n_chains; ++c) {
+        if (!w->inc[c]) continue;
+        (ch.is_c1[idx] ? a1 : a2)[c] = 1;
+        idx++;
+      }
+      make(std::move(a1), w->level, w->chain);
+      make(std::move(a2), w->level, std::move(w->chain));
+    } else {
+      w->chain.push_back(ch.c1);
+      if (w->level + 1 == q->levels) {
+        cons.push_back(std::move(w->chain));
+        assigns.push_back(w->inc);
+      } else {
+        make(w->inc, w->level + 1, std::move(w->chain));
+      }
+    }
+  }
+  // an error ends the search: the sub-problems still running finish first
+  // (they read the caller's buffers and this call's request records)
+  for (auto& w : stack) {
+    (void)wait_req(S, w->rq.get());
+    if (w->rq->fb_res) wc_results_free(w->rq->fb_res);
+  }
+  if (rc != WC_OK) return rc;
+  if (pr.status == WC_OK) priority_assemble(q->n_chains, cons, assigns, pr);
   fill_stats(R.get(), 0.0, 0, std::chrono::duration<double, std::milli>(Clock::now() - t0).count());
   *out = R.release();
   return WC_OK;
@@ -617,6 +822,14 @@ void wc_service_destroy(wc_service* S) {
     S->stop = true;
   }
   S->cv_svc.notify_all();
+  S->cv_arena.notify_all();
+  {
+    // calls already inside finish first (the service thread serves them);
+    // new ones are refused
+    std::unique_lock<std::mutex> lk(S->mu);
+    S->cv_idle.wait(lk, [&] { return S->inflight == 0; });
+  }
+  S->cv_svc.notify_all();
   S->th.join();
   (void)hipSetDevice(S->device);
   S->arena.release();
@@ -630,6 +843,11 @@ int wc_service_consensus(wc_service* s, const wc_config* cfg, const wc_problem* 
 
 int wc_service_dual_consensus(wc_service* s, const wc_config* cfg, const wc_problem* problem, wc_results** out) {
   return service_call(s, 2, cfg, problem, out);
+}
+
+int wc_service_priority_consensus(wc_service* s, const wc_config* cfg, const wc_chain_problem* problem,
+                                  wc_results** out) {
+  return service_priority(s, cfg, problem, out);
 }
 
 int wc_service_get_stats(wc_service* s, wc_service_stats* out) {

@@ -129,11 +129,13 @@ class DualConsensusDWFA:
     def consensus(self):
         """dual_consensus.rs:240-787 (on the GPU)."""
         offs = self._offsets if any(o is not None for o in self._offsets) else None
+        out = None
         if _lib.service_enabled():
             from .consensus import _service_call
-            (res,), stats = _service_call("wc_service_dual_consensus", (self._sequences, offs), self._config)
-        else:
-            (res,), stats = dual_consensus_batch([(self._sequences, offs)], self._config)
+            out = _service_call("wc_service_dual_consensus", (self._sequences, offs), self._config)
+        if out is None:
+            out = dual_consensus_batch([(self._sequences, offs)], self._config)
+        (res,), stats = out
         self.last_stats = stats
         return res
 

@@ -2,7 +2,9 @@
 
 The LIFO split/level orchestration runs in the library's host code
 (wc_priority_consensus_batch); every DualConsensusDWFA sub-problem runs on the
-device engine, batched across all problems of a call.
+device engine, batched across all problems of a call. One
+PriorityConsensusDWFA.consensus() goes through the device's submission
+service (wc_service_priority_consensus), shared by every calling thread.
 """
 import ctypes
 
@@ -32,11 +34,9 @@ class PriorityConsensus:
         return "PriorityConsensus(consensuses=%r, sequence_indices=%r)" % (self._consensuses, self._sequence_indices)
 
 
-def priority_consensus_batch(problems, config=None, context=None, return_errors=False):
-    """problems: list of (chains, offsets or None, seed_groups or None); chains[i][level] bytes."""
-    config = config or CdwfaConfig()
-    ctx = context or _lib.default_context()
-    L = _lib.lib()
+def _chain_problems(problems):
+    """WcChainProblem array (and the buffers it points into) for a list of
+    (chains, offsets or None, seed_groups or None); chains[i][level] bytes."""
     keep = []
     arr = (_lib.WcChainProblem * max(1, len(problems)))()
     for i, (chains, offsets, groups) in enumerate(problems):
@@ -56,36 +56,72 @@ def priority_consensus_batch(problems, config=None, context=None, return_errors=
         arr[i].lens = ctypes.cast(pr.lens, ctypes.POINTER(ctypes.c_uint64))
         arr[i].offsets = ctypes.cast(offs, ctypes.POINTER(ctypes.c_int64)) if offs is not None else None
         arr[i].seed_groups = ctypes.cast(grp, ctypes.POINTER(ctypes.c_int64)) if grp is not None else None
+    return arr, keep
+
+
+def _priority_results(res, n, config, L, return_errors):
+    out = []
+    for p in range(n):
+        try:
+            _raise_for(res, p, L)
+        except _lib.WaffleConError as e:
+            if not return_errors:
+                raise
+            out.append(e)
+            continue
+        chains = []
+        for k in range(L.wc_results_count(res, p)):
+            chain = []
+            for lvl in range(L.wc_results_chain_len(res, p, k)):
+                sp, sl = _lib._u8p(), ctypes.c_uint64()
+                cp, cl = ctypes.POINTER(ctypes.c_uint64)(), ctypes.c_uint64()
+                L.wc_results_chain(res, p, k, lvl, ctypes.byref(sp), ctypes.byref(sl), ctypes.byref(cp),
+                                   ctypes.byref(cl))
+                chain.append(Consensus(_lib.u8_bytes(sp, sl.value), config.consensus_cost,
+                                       _lib.u64_list(cp, cl.value)))
+            chains.append(chain)
+        ip, il = ctypes.POINTER(ctypes.c_uint64)(), ctypes.c_uint64()
+        L.wc_results_sequence_indices(res, p, ctypes.byref(ip), ctypes.byref(il))
+        out.append(PriorityConsensus(chains, _lib.u64_list(ip, il.value)))
+    return out
+
+
+def priority_consensus_batch(problems, config=None, context=None, return_errors=False, per_problem=False):
+    """problems: list of (chains, offsets or None, seed_groups or None); chains[i][level] bytes.
+    per_problem: the stats also carry "per_problem" (each problem's counters, and
+    wall_ms = time from the start of the call until its result was final)."""
+    config = config or CdwfaConfig()
+    ctx = context or _lib.default_context()
+    L = _lib.lib()
+    arr, keep = _chain_problems(problems)
     cfg = _lib.make_config(config)
     res = ctypes.c_void_p()
     rc = L.wc_priority_consensus_batch(ctx.handle, ctypes.byref(cfg), len(problems), arr, ctypes.byref(res))
     if rc != _lib.WC_OK:
         raise _lib.WaffleConError("wc_priority_consensus_batch failed: " + ctx.last_error(), rc)
     try:
-        out = []
-        for p in range(len(problems)):
-            try:
-                _raise_for(res, p, L)
-            except _lib.WaffleConError as e:
-                if not return_errors:
-                    raise
-                out.append(e)
-                continue
-            chains = []
-            for k in range(L.wc_results_count(res, p)):
-                chain = []
-                for lvl in range(L.wc_results_chain_len(res, p, k)):
-                    sp, sl = _lib._u8p(), ctypes.c_uint64()
-                    cp, cl = ctypes.POINTER(ctypes.c_uint64)(), ctypes.c_uint64()
-                    L.wc_results_chain(res, p, k, lvl, ctypes.byref(sp), ctypes.byref(sl), ctypes.byref(cp),
-                                       ctypes.byref(cl))
-                    chain.append(Consensus(_lib.u8_bytes(sp, sl.value), config.consensus_cost,
-                                           _lib.u64_list(cp, cl.value)))
-                chains.append(chain)
-            ip, il = ctypes.POINTER(ctypes.c_uint64)(), ctypes.c_uint64()
-            L.wc_results_sequence_indices(res, p, ctypes.byref(ip), ctypes.byref(il))
-            out.append(PriorityConsensus(chains, _lib.u64_list(ip, il.value)))
-        return out, _stats(res, L)
+        return _priority_results(res, len(problems), config, L, return_errors), _stats(res, L, per_problem)
+    finally:
+        L.wc_results_free(res)
+
+
+def priority_service_call(problem, config):
+    """One PriorityConsensusDWFA::consensus through the device's submission
+    service (wc_service_priority_consensus): this thread unwinds the LIFO
+    stack, the sub-problems share the service's persistent launches with every
+    other caller. None when the device has no service."""
+    svc = _lib.service()
+    if svc is None:
+        return None
+    L = _lib.lib()
+    arr, keep = _chain_problems([problem])
+    cfg = _lib.make_config(config)
+    res = ctypes.c_void_p()
+    rc = L.wc_service_priority_consensus(svc.handle, ctypes.byref(cfg), arr, ctypes.byref(res))
+    if rc != _lib.WC_OK:
+        raise _lib.WaffleConError("wc_service_priority_consensus failed: " + svc.last_error(), rc)
+    try:
+        return _priority_results(res, 1, config, L, False), _stats(res, L)
     finally:
         L.wc_results_free(res)
 
@@ -130,7 +166,11 @@ class PriorityConsensusDWFA:
 
     def consensus(self):
         """priority_consensus.rs:172-341."""
-        (res,), stats = priority_consensus_batch([(self._sequences, self._offsets, self._seed_groups)], self._config)
+        prob = (self._sequences, self._offsets, self._seed_groups)
+        out = priority_service_call(prob, self._config) if _lib.service_enabled() else None
+        if out is None:
+            out = priority_consensus_batch([prob], self._config)
+        (res,), stats = out
         self.last_stats = stats
         return res
 
