@@ -694,7 +694,7 @@ class Cfg5Api:
     @staticmethod
     def pregen(a, rank, world, total=None):
         from waffle_con_amd import synth
-        n = a.loci or 1024
+        n = a.loci or 512
         ids = list(range(rank * n, (rank + 1) * n))
         t0 = time.perf_counter()
         loci = pool_map(synth.cfg5_locus, ids)
@@ -768,10 +768,17 @@ class Cfg5Api:
         return tot, len(res)
 
     def extra(self):
+        """The batch path on the same loci, a thread sweep of the service path
+        (16 threads on the first 128 loci: a caller with T threads is bound by
+        T / latency) and per-call launches (first 64 loci)."""
         import waffle_con_amd as w
+
+        def note(msg):
+            print("[bench cfg5-api] %s" % msg, file=sys.stderr, flush=True)
         t0 = time.perf_counter()
         bres, _ = w.priority_consensus_batch([(ch, None, None) for ch in self.L], self.cfg, context=self.ctx)
         batch_s = time.perf_counter() - t0
+        note("batch path: %.1f s" % batch_s)
         out = {"api_threads": self.threads, "api_matches_batch_path": self.last == bres,
                "api_latency_ms_median": statistics.median(self.lat),
                "api_latency_ms_p90": sorted(self.lat)[int(0.9 * (len(self.lat) - 1))],
@@ -779,16 +786,19 @@ class Cfg5Api:
                "api_service_stats": self.svc, "batch_path_loci_per_s": self.n / batch_s}
         sweep = {}
         for t in sorted({16, 64, 256, self.threads}):
-            wt, _, r, _, _ = self.run(0, t)
-            sweep[str(t)] = self.n / wt
-            out["api_matches_batch_path"] &= r == bres
+            n = min(self.n, 128) if t <= 16 else self.n
+            wt, _, r, _, _ = self.run(0, t, n)
+            sweep[str(t)] = n / wt
+            out["api_matches_batch_path"] &= r == bres[:n]
+            note("service path, %d threads: %.1f loci/s" % (t, n / wt))
         out["api_service_loci_per_s_by_threads"] = sweep
         per_call = {}
         for t in (16, 64):
-            n = min(self.n, 128)
+            n = min(self.n, 64)
             wt, _, r, _, _ = self.run(1, t, n)
             per_call[str(t)] = n / wt
             out["api_matches_batch_path"] &= r == bres[:n]
+            note("per-call launches, %d threads: %.1f loci/s" % (t, n / wt))
         out["api_per_call_launch_loci_per_s_by_threads"] = per_call
         return out
 
@@ -850,6 +860,11 @@ def main():
     # reductions); the line says so and is not a scaling measurement
     share = world > 1 and os.environ.get("WC_BENCH_SHARE_GPU") == "1"
     device_index = local_rank % max(1, torch.cuda.device_count()) if share else local_rank
+    if share:
+        # co-tenants: every rank's launches are planned for its share of the
+        # device's CUs and HBM (the library reads this when its context is made)
+        per_dev = -(-world // max(1, torch.cuda.device_count()))
+        os.environ.setdefault("WC_DEVICE_SHARE", str(per_dev))
     torch.cuda.init()
     torch.cuda.set_device(device_index)
     dist = None

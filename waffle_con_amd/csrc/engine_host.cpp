@@ -36,12 +36,16 @@ namespace wch {
 
 constexpr uint32_t kLdsMax = 160 * 1024;  // one workgroup may take the whole CU's LDS
 
-// HBM the node pools of one launch may take: `share` of what is free plus the
-// launch's own cached workspace (reused by the launch)
-uint64_t hbm_share(uint64_t cached, double share) {
+// HBM the node pools of one launch may take: `frac` of what is free plus the
+// launch's own cached workspace (reused by the launch), and never more than
+// `frac` of this context's share of the device (WC_DEVICE_SHARE processes on
+// one GPU each plan for 1/share of its HBM, not for whatever is free when they
+// happen to look)
+uint64_t hbm_share(const wc_ctx* ctx, uint64_t cached, double frac) {
   size_t fr = 0, tot = 0;
-  if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 32ull << 30;
-  return (uint64_t)(((double)fr + (double)cached) * share);
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = tot = 32ull << 30;
+  const double avail = std::min((double)fr + (double)cached, (double)tot / std::max(1, ctx->share));
+  return (uint64_t)(avail * frac);
 }
 
 // Capacities of one launch over items[ids] (SURVEY §8(a) sizes): wavefront row
@@ -544,7 +548,7 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
     if (run.empty()) run.swap(later);
     Caps caps;
     std::string err;
-    int rc = plan_caps(ctx, cfg, sides, items, run, hbm_share(L->ws.cap, 0.5), caps, err);
+    int rc = plan_caps(ctx, cfg, sides, items, run, hbm_share(ctx, L->ws.cap, 0.5), caps, err);
     if (rc != WC_OK) {
       for (uint32_t id : run) {
         out[id].status = rc;
@@ -710,6 +714,9 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   uint32_t beat = 0, finished = 0;
   const bool log = getenv("WC_LAUNCH_LOG") != nullptr;
   auto t_log = std::chrono::steady_clock::now();
+  // a launch that stops finishing sub-problems says so (always, not only with
+  // WC_LAUNCH_LOG): how far it got and how many workgroups are still in
+  auto t_fin = t_log, t_warn = t_log;
   // what is ready but not yet published, in publication order: continuations
   // first, then the largest (reads x bases)
   auto later = [&](uint32_t x, uint32_t y) {
@@ -790,8 +797,21 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
       while (oldest < seq_item.size() && seq_done[oldest]) oldest++;
       on_done(id, st);
       progress = true;
+      t_fin = std::chrono::steady_clock::now();
     }
     if (outstanding == 0 && ready.empty() && waiting.empty()) break;
+    {
+      const auto now = std::chrono::steady_clock::now();
+      const double quiet = std::chrono::duration<double>(now - t_fin).count();
+      if (quiet > 20.0 && std::chrono::duration<double>(now - t_warn).count() > 20.0) {
+        t_warn = now;
+        fprintf(stderr,
+                "[wc] stream launch: no sub-problem finished for %.0f s (%u published, %u finished, %u outstanding, "
+                "%zu waiting; %u of %u workgroups exited; abort %u; grid planned for %d CUs)\n",
+                quiet, (uint32_t)seq_item.size(), finished, outstanding, ready.size() + waiting.size(), L.n_exited(),
+                L.grid, (uint32_t)sc->abort, ctx->n_cu);
+      }
+    }
     if (progress) {
       t_idle = std::chrono::steady_clock::now();
       continue;
@@ -1104,7 +1124,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     bool widened = false;
     for (;;) {
       std::vector<uint32_t> ids(conc, 0);
-      prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(L->ws.cap, 0.8), caps, err, 8);
+      prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(ctx, L->ws.cap, 0.8), caps, err, 8);
       // a first epoch whose workgroups fit more than 4 per CU plans for all of them
       if (prc == WC_OK && !widened && nretry == 0 && !caps.pool_short &&
           std::min<size_t>((size_t)caps.per_cu * ctx->n_cu, conc_cap) > conc) {

@@ -334,7 +334,12 @@ int wc_ctx_create(int device, wc_ctx** out) {
   wc_ctx* ctx = new wc_ctx();
   ctx->device = device;
   hipDeviceProp_t prop;
+  if (const char* e = getenv("WC_DEVICE_SHARE")) ctx->share = std::max(1, atoi(e));
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
+  // co-tenants of one device (WC_DEVICE_SHARE = k processes): every launch of
+  // this context is planned for 1/k of the CUs, so k persistent launches fit
+  // side by side instead of each asking for the whole chip
+  ctx->n_cu = std::max(1, ctx->n_cu / ctx->share);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
     delete ctx;

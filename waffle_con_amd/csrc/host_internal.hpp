@@ -94,7 +94,8 @@ struct Launch;
 
 struct wc_ctx {
   int device = 0;
-  int n_cu = 256;
+  int n_cu = 256;  // CUs this context plans its launches for: the device's / share
+  int share = 1;   // WC_DEVICE_SHARE: processes sharing the device (each plans for 1/share of CUs and HBM)
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string err;

@@ -80,6 +80,12 @@ struct Launch {
       if (!__atomic_load_n(&e[k], __ATOMIC_ACQUIRE)) return false;
     return true;
   }
+  uint32_t n_exited() const {
+    const uint32_t* e = (const uint32_t*)((const uint8_t*)host.p + off_exit);
+    uint32_t n = 0;
+    for (uint32_t k = 0; k < grid; ++k) n += __atomic_load_n(&e[k], __ATOMIC_ACQUIRE) != 0;
+    return n;
+  }
   ~Launch() {
     for (DevBuf* b : {&probs, &sroff, &srlen, &ract, &ws, &counter, &act, &phases, &gst}) b->release();
     host.release();
@@ -90,9 +96,8 @@ struct Launch {
   }
 };
 
-// HBM the node pools of one launch may take: `share` of what is free plus the
-// launch's own cached workspace (reused by the launch)
-uint64_t hbm_share(uint64_t cached, double share);
+// HBM the node pools of one launch may take (engine_host.cpp)
+uint64_t hbm_share(const wc_ctx* ctx, uint64_t cached, double frac);
 // Capacities of one launch over items[ids]; see engine_host.cpp
 int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vector<SubProb>& items,
               const std::vector<uint32_t>& ids, uint64_t hbm_budget, Caps& c, std::string& err,

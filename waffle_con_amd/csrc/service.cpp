@@ -112,7 +112,7 @@ struct Lane {
   uint32_t grid_full = 0;  // workgroups a full-chip launch of this lane would ask for
   bool can_grow = false;   // a restart with more requests waiting would get more workgroups
   uint64_t rw = 0;
-  Clock::time_point idle_since, started, last_result, last_query;
+  Clock::time_point idle_since, started, last_result, last_query, last_warn;
 };
 
 }  // namespace
@@ -225,7 +225,7 @@ int lane_start(wc_service* S, const Req* q) {
   std::vector<uint32_t> ids(want, 0);
   Caps caps;
   std::string err;
-  int rc = plan_caps(ctx, ln.cfg, ln.sides, env, ids, hbm_share(L->ws.cap, 0.25), caps, err);
+  int rc = plan_caps(ctx, ln.cfg, ln.sides, env, ids, hbm_share(ctx, L->ws.cap, 0.25), caps, err);
   if (rc != WC_OK) return set_err(ctx, rc, err);
   L->caps = caps;
   L->grid = std::min<uint32_t>((uint32_t)std::max(1, caps.per_cu) * (uint32_t)ctx->n_cu, std::max(1u, caps.conc));
@@ -490,7 +490,13 @@ void service_loop(wc_service* S) {
         const uint32_t ab = ln.sc->abort;
         bool ended = ab || ln.L->all_exited();
         const auto now = Clock::now();
-        if (!ended && std::chrono::duration<double>(now - ln.last_result).count() > 5.0 &&
+        const double quiet = std::chrono::duration<double>(now - ln.last_result).count();
+        if (quiet > 20.0 && std::chrono::duration<double>(now - ln.last_warn).count() > 20.0) {
+          ln.last_warn = now;  // a lane that stops finishing says so (always)
+          fprintf(stderr, "[wc] service lane: no locus finished for %.0f s (%u outstanding, %u of %u workgroups "
+                          "exited, abort %u)\n", quiet, ln.outstanding, ln.L->n_exited(), ln.L->grid, ab);
+        }
+        if (!ended && quiet > 5.0 &&
             std::chrono::duration<double>(now - ln.last_query).count() > 1.0) {
           ln.last_query = now;
           ended = hipStreamQuery(ln.L->stream) != hipErrorNotReady;
