@@ -1,5 +1,7 @@
 """Adapter: the product API (waffle_con_amd, HIP path) with the same call
 shape and result dicts as tests/oracle_ffi.py, so ref_cases drive both."""
+import os
+
 import waffle_con_amd as w
 from waffle_con_amd.cdwfa_config import CdwfaConfig, ConsensusCost
 
@@ -43,12 +45,20 @@ def dual_consensus(seqs, offsets=None, counters=False, **cfg):
 
 
 def priority_consensus(chains, offsets=None, seed_groups=None, counters=False, **cfg):
+    """PriorityConsensusDWFA.consensus() (the service path), or with
+    WC_TEST_PRIORITY_PATH=batch the same problem through
+    priority_consensus_batch (the streamed batch launch)."""
     d = w.PriorityConsensusDWFA.with_config(make_config(**cfg))
     for i, ch in enumerate(chains):
         offs = [None] * len(ch) if offsets is None else offsets[i]
         grp = None if seed_groups is None else seed_groups[i]
         d.add_seeded_sequence_chain(list(ch), offs, grp)
-    r = d.consensus()
+    if os.environ.get("WC_TEST_PRIORITY_PATH") == "batch":
+        from waffle_con_amd.priority_consensus import priority_consensus_batch
+        (r,), stats = priority_consensus_batch([(d._sequences, d._offsets, d._seed_groups)], d._config)
+    else:
+        r = d.consensus()
+        stats = d.last_stats
     res = {"consensuses": [[_cons(c) for c in chain] for chain in r.consensuses()],
            "sequence_indices": list(r.sequence_indices())}
-    return (res, d.last_stats) if counters else res
+    return (res, stats) if counters else res

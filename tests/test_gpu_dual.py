@@ -14,7 +14,7 @@ def test_reference_dual(name):
 
 
 @pytest.mark.parametrize("name", sorted(rc.PRIORITY_CASES))
-def test_reference_priority(name):
+def test_reference_priority(priority_path, name):
     rc.check_priority(rc.PRIORITY_CASES[name], hip)
 
 
@@ -81,7 +81,7 @@ def test_dual_weighted_l2_vs_oracle(seed):
 
 
 @pytest.mark.parametrize("seed", range(3))
-def test_priority_synthetic_vs_oracle(seed):
+def test_priority_synthetic_vs_oracle(priority_path, seed):
     reads = _two_haplotypes(100, 5, 0.01, 200 + seed)
     chains = [[r, r[: len(r) // 2]] for r in reads]
     cfg = dict(min_count=3, wildcard=ord("*"))

@@ -64,7 +64,7 @@ def test_cfg3_full_locus_vs_oracle():
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_cfg5_full_locus_vs_oracle(seed):
+def test_cfg5_full_locus_vs_oracle(priority_path, seed):
     """cfg5: PGx locus at real size (1-6 kb, 15-40 reads per haplotype, [HPC, full] chains)."""
     from waffle_con_amd import synth
     chains = synth.cfg5_locus(seed)
@@ -78,7 +78,7 @@ def _digest(b):
     return hashlib.sha256(bytes(b)).hexdigest()
 
 
-def test_cfg4_full_locus_vs_oracle_fixture():
+def test_cfg4_full_locus_vs_oracle_fixture(priority_path):
     """cfg4: 4 haplotypes x 50 reads x 8 kb with inserted segments {0, 25, 60,
     150} bp, chain length 1, wildcard '*' (priority tests' config)."""
     path = os.path.join(HERE, "golden", "cfg4_seed4.json")

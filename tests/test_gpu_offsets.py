@@ -98,7 +98,7 @@ def test_dual_offsets_vs_oracle(seed):
 
 
 @pytest.mark.parametrize("seed", range(3))
-def test_priority_seeded_offsets_vs_oracle(seed):
+def test_priority_seeded_offsets_vs_oracle(priority_path, seed):
     from test_gpu_dual import _two_haplotypes
     reads = _two_haplotypes(120, 5, 0.01, 400 + seed)
     rng = random.Random(seed)

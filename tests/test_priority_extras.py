@@ -110,14 +110,14 @@ def _cmp_priority(hip, chains, offsets=None, seed_groups=None, **cfg):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(3))
-def test_gpu_priority_counters_vs_oracle(seed):
+def test_gpu_priority_counters_vs_oracle(priority_path, seed):
     hip = pytest.importorskip("hip_runner")
     _cmp_priority(hip, _chains(500 + seed), min_count=2, wildcard=ord("*"))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(2))
-def test_gpu_priority_seed_groups_vs_oracle(seed):
+def test_gpu_priority_seed_groups_vs_oracle(priority_path, seed):
     """Several seed groups over 20 chains; groups 1 and 3 hold identical reads,
     so their (identical) chains keep the seed-group processing order."""
     hip = pytest.importorskip("hip_runner")
@@ -128,7 +128,7 @@ def test_gpu_priority_seed_groups_vs_oracle(seed):
 
 
 @pytest.mark.gpu
-def test_gpu_priority_per_level_offsets_vs_oracle():
+def test_gpu_priority_per_level_offsets_vs_oracle(priority_path):
     """Offsets on the second chain level only (activation at a consensus length)."""
     hip = pytest.importorskip("hip_runner")
     chains = _chains(700, n_hap=2, per=5, L=200)
@@ -137,7 +137,7 @@ def test_gpu_priority_per_level_offsets_vs_oracle():
 
 
 @pytest.mark.gpu
-def test_gpu_priority_error_mid_stack_vs_oracle():
+def test_gpu_priority_error_mid_stack_vs_oracle(priority_path):
     """A level-1 sub-problem whose reads all carry offsets fails (no start) after
     the level-0 split succeeded: the error and its precedence match."""
     hip = pytest.importorskip("hip_runner")

@@ -14,6 +14,8 @@
 // its path), so the harness never brings in a second copy.
 #include <dlfcn.h>
 
+#include <cstdio>
+
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -107,10 +109,13 @@ extern "C" int api_bench_priority_run(const char* libpath, int device, int mode,
   decltype(&wc_ctx_create) ctx_create;
   decltype(&wc_ctx_destroy) ctx_destroy;
   decltype(&wc_priority_consensus_batch) batch_prio;
+  decltype(&wc_last_error) last_error;
+  decltype(&wc_service_last_error) svc_last_error;
   if (!sym(h, "wc_service_create", svc_create) || !sym(h, "wc_service_destroy", svc_destroy) ||
       !sym(h, "wc_service_priority_consensus", svc_prio) || !sym(h, "wc_service_get_stats", svc_stats_fn) ||
       !sym(h, "wc_ctx_create", ctx_create) || !sym(h, "wc_ctx_destroy", ctx_destroy) ||
-      !sym(h, "wc_priority_consensus_batch", batch_prio))
+      !sym(h, "wc_priority_consensus_batch", batch_prio) || !sym(h, "wc_last_error", last_error) ||
+      !sym(h, "wc_service_last_error", svc_last_error))
     return -1;
   wc_service* svc = nullptr;
   if (mode == 0) {
@@ -133,7 +138,8 @@ extern "C" int api_bench_priority_run(const char* libpath, int device, int mode,
       lat_ms[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       if (rc) {
         int z = 0;
-        first_rc.compare_exchange_strong(z, rc);
+        if (first_rc.compare_exchange_strong(z, rc))
+          fprintf(stderr, "[api_bench] locus %u failed (rc %d): %s\n", i, rc, mode == 0 ? svc_last_error(svc) : last_error(ctx));
       }
     }
     if (ctx) ctx_destroy(ctx);

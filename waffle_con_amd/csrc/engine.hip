@@ -191,6 +191,7 @@ struct Lds {
   Sh<uint32_t>* fe;    // [sides][nmax]
   Sh<uint32_t>* list;  // [list_entries] work list (heavy reads / wide analyses)
   Sh<uint16_t>* ce;    // dual: [kNCB * 2][nmax] edit distances of the children being built (prune + cost; kCeNone = None)
+  Sh<uint2>* rt;       // [nmax] the claimed problem's reads: byte offset / 16 from rbytes, length (init_problem)
 };
 
 __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t K,
@@ -240,6 +241,8 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
   l.list = (Sh<uint32_t>*)p;
   p += align16((uint64_t)list_entries(sides, nmax) * 4);
   l.ce = sides == 2 ? (Sh<uint16_t>*)p : nullptr;
+  if (sides == 2) p += align16((uint64_t)kDualChildBatch * 2 * nmax * 2);
+  l.rt = (Sh<uint2>*)p;
   return l;
 }
 
@@ -445,8 +448,11 @@ struct Eng {
   __device__ SideView sv(uint32_t slot, uint32_t side) const {
     return side_view(ws + (uint64_t)WC_IX(slot, pcap) * sbytes, WC_IX(side, sides), nmax, wcap, lcap);
   }
-  __device__ const Gm<uint8_t>* read(uint32_t r) const { return rbytes + roff[P.read_begin + WC_IX(r, nmax)]; }
-  __device__ uint32_t rlen(uint32_t r) const { return rlenp[P.read_begin + WC_IX(r, nmax)]; }
+  // a read's bytes and length from the LDS read table (init_problem fills it
+  // from the HBM tables: one dependent HBM round trip less wherever a phase
+  // loads read bytes)
+  __device__ const Gm<uint8_t>* read(uint32_t r) const { return rbytes + (uint64_t)L.rt[WC_IX(r, nmax)].x * 16; }
+  __device__ uint32_t rlen(uint32_t r) const { return L.rt[WC_IX(r, nmax)].y; }
   __device__ __forceinline__ TrackerRef tracker(Lo<Ctl>& ctl, int k) const {
     const uint64_t L2 = lcap + 2;
     return TrackerRef{trk + 2 * k * L2, trk + (2 * k + 1) * L2, &ctl.trk_total[k], &ctl.trk_thr[k],
@@ -718,6 +724,10 @@ __device__ inline void init_problem(Eng& E, Lo<Ctl>& ctl) {
   }
   for (uint32_t i = tid; i < E.pcap; i += kEB) E.L.freestack[i] = E.pcap - 1 - i;
   for (uint32_t i = tid; i < 4 * (E.lcap + 2); i += kEB) E.trk[i] = 0;
+  // the read table in LDS (reads start 16-byte aligned in every arena)
+  for (uint32_t r = tid; r < E.n; r += kEB)
+    E.L.rt[r] = make_uint2((uint32_t)(E.roff[E.P.read_begin + r] >> 4), E.rlenp[E.P.read_begin + r]);
+  __syncthreads();
   SideView v = E.sv(0, 0);
   for (uint32_t r = tid; r < E.n; r += kEB) {
     // e = 0 (or None), off = 0, maxb = 0, nscmp = 0, nf = 1: the single
@@ -2290,9 +2300,9 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
       }
       SUB_T1(31, tam);
 
-      // ---- votes on both sides (waves 0 and 1 in parallel) ----
-      if (wave_id() < (tdual ? 2 : 1)) {
-        const uint32_t side = wave_id();
+      // ---- votes on both sides (waves 0 and 1 in parallel; one after the
+      // other in a one-wave workgroup) ----
+      for (uint32_t side = wave_id(); side < (tdual ? 2u : 1u); side += (uint32_t)kEW) {
         const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, E.n, weighted, tdual,
                                    ctl.multi[side] != 0, cfg.wildcard);
         if (!ok && lane == 0) atomicOr(&ctl.ovf, (uint32_t)LIM_VOTES);

@@ -32,6 +32,32 @@
 
 using namespace wc;
 
+namespace {
+std::mutex g_persist_mu;
+int g_persist_running = 0;
+std::vector<std::pair<void*, bool>> g_parked;  // buffers freed while a persistent launch ran
+}  // namespace
+
+void persistent_begin() {
+  std::lock_guard<std::mutex> g(g_persist_mu);
+  g_persist_running++;
+}
+void persistent_end() {
+  std::vector<std::pair<void*, bool>> go;
+  {
+    std::lock_guard<std::mutex> g(g_persist_mu);
+    if (--g_persist_running > 0) return;
+    go.swap(g_parked);
+  }
+  for (auto& b : go) (void)(b.second ? hipHostFree(b.first) : hipFree(b.first));
+}
+bool free_deferred(void* p, bool host) {
+  std::lock_guard<std::mutex> g(g_persist_mu);
+  if (g_persist_running == 0) return false;
+  g_parked.emplace_back(p, host);
+  return true;
+}
+
 namespace wch {
 
 constexpr uint32_t kLdsMax = 160 * 1024;  // one workgroup may take the whole CU's LDS
@@ -620,10 +646,20 @@ template <class OnDone, class Live>
 static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg, const Caps& caps,
                         std::vector<SubProb>& items, std::deque<uint32_t>& ready, OnDone on_done, Live live,
                         std::vector<EngineOut>& outs) {
-  constexpr uint32_t kQcap = 1u << 16;   // published, unfinished problems
-  constexpr uint32_t kQslots = 1u << 23; // their read-table entries
   L.caps = caps;
   L.grid = std::min<uint32_t>((uint32_t)std::max(1, caps.per_cu) * (uint32_t)ctx->n_cu, std::max(1u, caps.conc));
+  // the ring (pinned host memory) holds the published, unfinished problems:
+  // at most a grid and a quarter of them (the backlog below) and their read
+  // tables. Sized for that, not for the largest batch: a call per locus from
+  // many threads (per-thread contexts) would otherwise pin 160 MB each.
+  auto pow2 = [](uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+  };
+  const uint32_t kQcap = (uint32_t)std::min<uint64_t>(1u << 16, std::max<uint64_t>(1024, pow2(2ull * L.grid + 64)));
+  const uint32_t kQslots =
+      (uint32_t)std::min<uint64_t>(1u << 23, std::max<uint64_t>(1u << 16, pow2((uint64_t)kQcap * caps.nmax)));
   L.P = 2 * L.grid;  // two output slots per workgroup
   L.kernel_ms = 0;
   const uint32_t P = L.P;
@@ -694,8 +730,12 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.qhead = (uint32_t*)L.counter.p;
   a.idle_ticks = (uint64_t)clk * 1000ull * 30ull;  // 30 s without a host heartbeat: the host is gone
   a.exited = (uint32_t*)(dh + L.off_exit);
+  persistent_begin();
   const int krc = launch_kernel(ctx, L, a, caps);
-  if (krc != WC_OK) return krc;
+  if (krc != WC_OK) {
+    persistent_end();
+    return krc;
+  }
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
     fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u narrow=%d lowlat=%d dual_hot=%d\n",
@@ -837,6 +877,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   }
   __atomic_store_n(&sc->stop, 1u, __ATOMIC_RELEASE);
   const int frc = launch_finish(ctx, L);
+  persistent_end();
   return rc != WC_OK ? rc : frc;
 }
 
@@ -936,14 +977,28 @@ struct PWork {
   std::vector<uint8_t> inc;
   uint32_t level = 0;
   std::vector<ConsRec> chain;
-  int state = 0;  // 0 waiting to launch, 1 launched, 2 done
+  int state = 0;  // 0 waiting to launch, 1 launched, 2 done (result known, successors made)
   std::unique_ptr<ProbRes> res;
+  double t_make = 0;  // ms from the call's start (WC_SUBPROB_LOG)
+  // the sub-problems this one's result makes (a split's two groups, or the
+  // next level), made as soon as the result is known; they go on the stack
+  // when this one is popped (the reference's LIFO order)
+  std::vector<uint32_t> kids;
+  bool final_chain = false;  // no successor: `chain` is finished (the last level)
 };
 }  // namespace
 
 int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chain_problem* problems, wc_results* R) {
   const auto t_call = std::chrono::steady_clock::now();
   R->probs.resize(n);
+  // WC_SUBPROB_LOG=<file> (diagnostics): owner level reads made_ms done_ms pops updates split status
+  FILE* sublog = getenv("WC_SUBPROB_LOG") ? fopen(getenv("WC_SUBPROB_LOG"), "a") : nullptr;
+  struct CloseLog {
+    FILE* f;
+    ~CloseLog() {
+      if (f) fclose(f);
+    }
+  } close_log{sublog};
   // 1. every read of every problem (all chain levels) resident in one arena:
   //    read (problem i, chain c, level l) = arena read base[i] + c * levels + l
   std::vector<wc_problem> flat(n);
@@ -974,6 +1029,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     pool.emplace_back(new PWork());
     PWork& w = *pool.back();
     w.owner = i;
+    w.t_make = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
     w.inc = std::move(inc);
     w.level = level;
     w.chain = std::move(chain);
@@ -1001,7 +1057,44 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     } else {
       ready.push_back(id);
     }
-    stacks[i].push_back(id);
+    return id;
+  };
+  // A finished sub-problem's successors (priority_consensus.rs:254-305): a
+  // split makes one sub-problem per consensus group at the same level, no
+  // split extends the chain to the next level (or finishes it). They depend
+  // on this result alone, so they are made and published at once, even when
+  // this sub-problem is still deep in the stack: a group whose sibling is
+  // still splitting does not wait for the sibling's whole subtree to start
+  // its next level. What enters the stack, the counters and the result order
+  // still follow the reference's LIFO unwinding (unwind below).
+  auto expand = [&](uint32_t id) {
+    PWork& w = *pool[id];
+    const uint32_t i = w.owner;
+    const wc_chain_problem& q = problems[i];
+    const ProbRes& d = *w.res;
+    if (!alive[i] || d.status != WC_OK) return;
+    const DualRec& ch = d.dual[0];
+    if (ch.has_c2) {
+      std::vector<uint8_t> a1(q.n_chains, 0), a2(q.n_chains, 0);
+      size_t idx = 0;
+      for (uint32_t c = 0; c < q.n_chains; ++c) {
+        if (!w.inc[c]) continue;
+        if (ch.is_c1[idx]) a1[c] = 1;
+        else a2[c] = 1;
+        idx++;
+      }
+      const uint32_t k1 = make(i, std::move(a1), w.level, w.chain);
+      const uint32_t k2 = make(i, std::move(a2), w.level, w.chain);
+      pool[id]->kids = {k1, k2};
+    } else {
+      w.chain.push_back(ch.c1);
+      if (w.level + 1 == q.levels) {
+        w.final_chain = true;
+      } else {
+        const uint32_t k = make(i, w.inc, w.level + 1, w.chain);
+        pool[id]->kids = {k};
+      }
+    }
   };
 
   for (uint32_t i = 0; i < n; ++i) {
@@ -1018,15 +1111,15 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     for (int64_t g : seed_order(groups)) {
       std::vector<uint8_t> inc(q.n_chains);
       for (uint32_t c = 0; c < q.n_chains; ++c) inc[c] = groups[c] == g;
-      make(i, std::move(inc), 0, {});
+      stacks[i].push_back(make(i, std::move(inc), 0, {}));
     }
   }
   roots_made = true;
 
   // pop finished tops in LIFO order (priority_consensus.rs:195-307); the
-  // counters of a sub-problem are added when it is popped
+  // counters of a sub-problem are added when it is popped, its successors
+  // (made when its result came, expand) go on the stack then
   auto unwind = [&](uint32_t i) {
-    const wc_chain_problem& q = problems[i];
     ProbRes& pr = R->probs[i];
     while (alive[i] && !stacks[i].empty() && pool[stacks[i].back()]->state == 2) {
       const uint32_t id = stacks[i].back();
@@ -1041,27 +1134,11 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
         alive[i] = false;
         break;
       }
-      const DualRec& ch = d.dual[0];
-      if (ch.has_c2) {
-        std::vector<uint8_t> a1(q.n_chains, 0), a2(q.n_chains, 0);
-        size_t idx = 0;
-        for (uint32_t c = 0; c < q.n_chains; ++c) {
-          if (!w.inc[c]) continue;
-          if (ch.is_c1[idx]) a1[c] = 1;
-          else a2[c] = 1;
-          idx++;
-        }
-        std::vector<ConsRec> chain = w.chain;
-        make(i, std::move(a1), w.level, std::move(chain));
-        make(i, std::move(a2), w.level, std::move(w.chain));
+      if (w.final_chain) {
+        cons[i].push_back(std::move(w.chain));
+        assigns[i].push_back(w.inc);
       } else {
-        w.chain.push_back(ch.c1);
-        if (w.level + 1 == q.levels) {
-          cons[i].push_back(std::move(w.chain));
-          assigns[i].push_back(w.inc);
-        } else {
-          make(i, w.inc, w.level + 1, std::move(w.chain));
-        }
+        for (uint32_t k : w.kids) stacks[i].push_back(k);
       }
       w.res.reset();
     }
@@ -1167,6 +1244,14 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
       build_dual(o, (uint32_t)subs[id].gid.size(), cfg.consensus_cost, *w.res);
       w.state = 2;
       o.recs.clear();
+      expand(id);
+      if (sublog) {
+        // diagnostics: one line per finished sub-problem (the critical path of a locus)
+        const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
+        fprintf(sublog, "%u %u %zu %.3f %.3f %llu %llu %d %d\n", w.owner, w.level, subs[id].gid.size(), w.t_make, t,
+                (unsigned long long)w.res->stats[S_POPS], (unsigned long long)w.res->stats[S_UPDATES],
+                w.res->status == WC_OK && !w.res->dual.empty() && w.res->dual[0].has_c2 ? 1 : 0, w.res->status);
+      }
       unwind(w.owner);
     }, [&](uint32_t id) { return (bool)alive[pool[id]->owner]; }, outs);
     if (rc2 != WC_OK) return rc2;

@@ -9,7 +9,10 @@
 // (no spills). Same source as engine.hip; LDS/HBM layouts are unchanged
 // (sized for the 256-thread build).
 #define WC_NARROW 1
-#define WC_BLOCK 128
+#ifndef WC_NARROW_BLOCK
+#define WC_NARROW_BLOCK 128
+#endif
+#define WC_BLOCK WC_NARROW_BLOCK  // (64: one-wave workgroups, an experiment build)
 #define WC_ENGINE_NS wcn
 #ifndef WC_NARROW_WAVES_PER_EU
 #define WC_NARROW_WAVES_PER_EU 2

@@ -291,7 +291,7 @@ __host__ __device__ inline uint32_t hot_sides(uint32_t sides, uint32_t chain, ui
   return dual_hot ? 2u : 0u;
 }
 // LDS: hot RStates[hot_sides][nmax] | chain area | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
-//      heavy list[list_entries] u32 | (dual) child e[kDualChildBatch][2][nmax] u16
+//      heavy list[list_entries] u32 | (dual) child e[kDualChildBatch][2][nmax] u16 | read table [nmax] u32x2
 __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t chain,
                                               uint32_t dual_hot = 0) {
   uint64_t t = (uint64_t)hot_sides(sides, chain, dual_hot) * nmax * sizeof(RState);
@@ -304,6 +304,8 @@ __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uin
   t += align16((uint64_t)list_entries(sides, nmax) * 4);
   // dual engine: the children's edit distances per (child, side, read) of one build pass (prune + cost), u16
   if (sides == 2) t += align16((uint64_t)kDualChildBatch * 2 * nmax * 2);
+  // the claimed problem's read table (offset / 16, length) per read
+  t += align16((uint64_t)nmax * 8);
   return align16(t);
 }
 

@@ -42,6 +42,19 @@ void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipS
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 }  // namespace wcd
 
+// Persistent (stream-mode) launches of this process and deferred frees.
+// hipFree / hipHostFree wait for every kernel on the device, a persistent
+// launch included, and that one only ends when its host thread says so. If
+// that thread is meanwhile blocked on the runtime inside another HIP call,
+// neither moves (its workgroups give up after 30 s without a heartbeat:
+// "stream launch ended with problems outstanding (abort=1)", seen with 16
+// threads each running wc_priority_consensus_batch on its own context). So
+// while any persistent launch of the process runs, buffers are not freed but
+// parked, and released by the thread that ends the last persistent launch.
+void persistent_begin();
+void persistent_end();
+bool free_deferred(void* p, bool host);  // true: parked (a persistent launch is running)
+
 // device buffer, grown on demand (never shrinks)
 struct DevBuf {
   void* p = nullptr;
@@ -58,7 +71,7 @@ struct DevBuf {
     return true;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p && !free_deferred(p, false)) (void)hipFree(p);
     p = nullptr;
     cap = 0;
   }
@@ -82,7 +95,7 @@ struct HostBuf {
     return true;
   }
   void release() {
-    if (p) (void)hipHostFree(p);
+    if (p && !free_deferred(p, true)) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
   }

@@ -89,6 +89,8 @@ struct Req {
   bool fb = false;
   wc_results* fb_res = nullptr;
   int fb_rc = WC_OK;
+  std::condition_variable* notify = nullptr;  // also woken on completion (a priority call's requests)
+  bool counted = false;                       // counted as served (poll_req)
 };
 
 bool same_cfg(const wc_config& a, const wc_config& b) { return memcmp(&a, &b, sizeof(wc_config)) == 0; }
@@ -181,6 +183,7 @@ void complete(wc_service* S, Req* q, uint32_t st) {
     S->cv_arena.notify_all();
   }
   q->cv.notify_one();
+  if (q->notify) q->notify->notify_all();
 }
 
 // ---- lanes (service thread, under mu) ----
@@ -300,8 +303,12 @@ int lane_start(wc_service* S, const Req* q) {
   a.qhead = (uint32_t*)L->counter.p;
   a.idle_ticks = (uint64_t)clk * 1000ull * 30ull;  // 30 s without a heartbeat: the host is gone
   a.exited = (uint32_t*)(dh + L->off_exit);
+  persistent_begin();
   rc = launch_kernel(ctx, *L, a, caps);
-  if (rc != WC_OK) return rc;
+  if (rc != WC_OK) {
+    persistent_end();
+    return rc;
+  }
   L->busy = true;
   ln.running = true;
   ln.idle_since = ln.started = ln.last_result = Clock::now();
@@ -373,6 +380,7 @@ void lane_stop(wc_service* S, Lane& ln, bool failed) {
     std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
   (void)launch_finish(S->ctx, *ln.L);
+  persistent_end();
   if (failed)
     for (uint32_t s = ln.oldest; s < ln.seq_req.size(); ++s)
       if (!ln.seq_done[s]) complete(S, ln.seq_req[s], ~0u);
@@ -407,6 +415,7 @@ void service_loop(wc_service* S) {
       f->fb_res = r;
       f->done = true;
       f->cv.notify_one();
+      if (f->notify) f->notify->notify_all();
       continue;
     }
     if (ln.running) {
@@ -559,8 +568,10 @@ void queue_fallback(wc_service* S, Req* q, const wc_problem* p) {
 // Submits one problem (no waiting): into a lane through the arena, or to the
 // batch path (offsets, > 256 reads, reads too large for the arena). `p` must
 // stay valid until the request completes.
-std::unique_ptr<Req> submit(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p) {
+std::unique_ptr<Req> submit(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_problem* p,
+                            std::condition_variable* notify = nullptr) {
   std::unique_ptr<Req> q(new Req());
+  q->notify = notify;
   q->sides = sides;
   q->cfg = *cfg;
   const uint32_t n = p->n_reads;
@@ -674,7 +685,7 @@ int service_call(wc_service* S, uint32_t sides, const wc_config* cfg, const wc_p
 }
 
 // ---- PriorityConsensusDWFA::consensus (priority_consensus.rs:172-341) ----
-// one stacked sub-problem of a call: a read subset at a chain level
+// one sub-problem of a call: a read subset at a chain level
 struct PSub {
   std::vector<uint8_t> inc;
   uint32_t level = 0;
@@ -684,7 +695,32 @@ struct PSub {
   std::vector<int64_t> ro;
   wc_problem wp{};
   std::unique_ptr<Req> rq;
+  bool done = false;         // result known (and successors made)
+  ProbRes res;
+  std::vector<size_t> kids;  // successors, made when the result came; stacked when this one is popped
+  bool final_chain = false;
 };
+
+// The outcome of a finished request: 0 = pending (still running, or just
+// sent to the batch path), 1 = done (lane or batch result in q), -1 = the
+// batch path failed (q->fb_rc). Caller holds S->mu.
+int poll_req(wc_service* S, Req* q) {
+  if (!q->done) return 0;
+  if (q->fb) return q->fb_rc == WC_OK ? 1 : -1;
+  if (q->st != ~0u && !(q->st & ST_RETRY)) {
+    if (!q->counted) {
+      q->counted = true;
+      S->stats.served++;
+    }
+    return 1;
+  }
+  if (q->st != ~0u) S->stats.retried++;
+  q->fb = true;  // capacity retry or a failed lane: the batch path (queue_fallback without re-locking)
+  q->done = false;
+  S->fbq.push_back(q);
+  S->cv_svc.notify_one();
+  return 0;
+}
 
 int service_priority(wc_service* S, const wc_config* cfg, const wc_chain_problem* q, wc_results** out) {
   *out = nullptr;
@@ -707,11 +743,13 @@ int service_priority(wc_service* S, const wc_config* cfg, const wc_chain_problem
     *out = R.release();
     return WC_OK;
   }
-  std::vector<std::unique_ptr<PSub>> stack;  // the reference's LIFO work stack
+  std::condition_variable call_cv;  // any of this call's requests completed
+  std::vector<std::unique_ptr<PSub>> subs;
+  std::vector<size_t> stack;  // the reference's LIFO work stack (indices into subs)
   std::vector<std::vector<ConsRec>> cons;
   std::vector<std::vector<uint8_t>> assigns;
-  // a new stack entry, submitted at once (it runs while the stack unwinds)
-  auto make = [&](std::vector<uint8_t> inc, uint32_t level, std::vector<ConsRec> chain) {
+  // a new sub-problem, submitted at once
+  auto make = [&](std::vector<uint8_t> inc, uint32_t level, std::vector<ConsRec> chain) -> size_t {
     std::unique_ptr<PSub> w(new PSub());
     w->inc = std::move(inc);
     w->level = level;
@@ -725,10 +763,48 @@ int service_priority(wc_service* S, const wc_config* cfg, const wc_chain_problem
     }
     w->wp.n_reads = (uint32_t)w->rp.size();
     w->wp.reads = w->rp.data();
-    w->wp.lens = w->rl.data();
+    w->wp.lens = w->rp.empty() ? nullptr : w->rl.data();
     w->wp.offsets = w->ro.data();
-    w->rq = submit(S, 2, cfg, &w->wp);
-    stack.push_back(std::move(w));
+    w->rq = submit(S, 2, cfg, &w->wp, &call_cv);
+    subs.push_back(std::move(w));
+    return subs.size() - 1;
+  };
+  // a finished sub-problem: its result and its successors (made at once, as
+  // in priority_stream's expand: they depend on this result alone)
+  auto finish = [&](size_t id) {
+    PSub& w = *subs[id];
+    if (w.rq->fb) {
+      w.res = std::move(w.rq->fb_res->probs[0]);
+      wc_results_free(w.rq->fb_res);
+      w.rq->fb_res = nullptr;
+    } else {
+      build_dual(w.rq->out, w.wp.n_reads, cfg->consensus_cost, w.res);
+    }
+    w.done = true;
+    if (w.res.status != WC_OK) return;
+    const DualRec& ch = w.res.dual[0];
+    if (ch.has_c2) {
+      std::vector<uint8_t> a1(q->n_chains, 0), a2(q->n_chains, 0);
+      size_t idx = 0;
+      for (uint32_t c = 0; c < q->n_chains; ++c) {
+        if (!w.inc[c]) continue;
+        (ch.is_c1[idx] ? a1 : a2)[c] = 1;
+        idx++;
+      }
+      const std::vector<ConsRec> chain = w.chain;
+      const uint32_t level = w.level;
+      const size_t k1 = make(std::move(a1), level, chain);
+      const size_t k2 = make(std::move(a2), level, chain);
+      subs[id]->kids = {k1, k2};
+    } else {
+      subs[id]->chain.push_back(ch.c1);
+      if (subs[id]->level + 1 == q->levels) {
+        subs[id]->final_chain = true;
+      } else {
+        const size_t k = make(subs[id]->inc, subs[id]->level + 1, subs[id]->chain);
+        subs[id]->kids = {k};
+      }
+    }
   };
   {
     std::vector<int64_t> groups(q->n_chains, -1);
@@ -737,60 +813,68 @@ int service_priority(wc_service* S, const wc_config* cfg, const wc_chain_problem
     for (int64_t g : seed_order(groups)) {
       std::vector<uint8_t> inc(q->n_chains);
       for (uint32_t c = 0; c < q->n_chains; ++c) inc[c] = groups[c] == g;
-      make(std::move(inc), 0, {});
+      stack.push_back(make(std::move(inc), 0, {}));
     }
   }
   int rc = WC_OK;
-  while (!stack.empty()) {
-    std::unique_ptr<PSub> w = std::move(stack.back());
-    stack.pop_back();
-    const int wrc = wait_req(S, w->rq.get());
-    ProbRes d;
-    if (wrc != WC_OK) {
-      rc = wrc;
-      break;
-    }
-    if (w->rq->fb) {
-      d = std::move(w->rq->fb_res->probs[0]);
-      wc_results_free(w->rq->fb_res);
-      w->rq->fb_res = nullptr;
-    } else {
-      build_dual(w->rq->out, w->wp.n_reads, cfg->consensus_cost, d);
-    }
-    for (int s = 0; s < S_NSTAT; ++s)
-      pr.stats[s] = s == S_PEAKQ ? std::max(pr.stats[s], d.stats[s]) : pr.stats[s] + d.stats[s];
-    if (d.status != WC_OK) {
-      pr.status = d.status;
-      pr.error = d.error;
-      break;
-    }
-    const DualRec& ch = d.dual[0];
-    if (ch.has_c2) {
-      std::vector<uint8_t> a1(q->n_chains, 0), a2(q->n_chains, 0);
-      size_t idx = 0;
-      for (uint32_t c = 0; c < q->n_chains; ++c) {
-        if (!w->inc[c]) continue;
-        (ch.is_c1[idx] ? a1 : a2)[c] = 1;
-        idx++;
+  bool stop = false;
+  while (!stack.empty() && !stop) {
+    // results that came in (any sub-problem, not only the stack's top)
+    std::vector<size_t> fin;
+    {
+      std::unique_lock<std::mutex> lk(S->mu);
+      for (;;) {
+        for (size_t id = 0; id < subs.size(); ++id) {
+          if (subs[id]->done) continue;
+          const int pst = poll_req(S, subs[id]->rq.get());
+          if (pst < 0) {
+            rc = subs[id]->rq->fb_rc;
+            stop = true;
+          } else if (pst > 0) {
+            fin.push_back(id);
+          }
+        }
+        if (stop || !fin.empty()) break;
+        call_cv.wait(lk);
       }
-      make(std::move(a1), w->level, w->chain);
-      make(std::move(a2), w->level, std::move(w->chain));
-    } else {
-      w->chain.push_back(ch.c1);
-      if (w->level + 1 == q->levels) {
-        cons.push_back(std::move(w->chain));
-        assigns.push_back(w->inc);
+    }
+    if (stop) break;
+    for (size_t id : fin) finish(id);
+    // pop finished tops in the reference's order; counters are added then
+    while (!stack.empty() && subs[stack.back()]->done) {
+      const size_t id = stack.back();
+      stack.pop_back();
+      PSub& w = *subs[id];
+      for (int s = 0; s < S_NSTAT; ++s)
+        pr.stats[s] = s == S_PEAKQ ? std::max(pr.stats[s], w.res.stats[s]) : pr.stats[s] + w.res.stats[s];
+      if (w.res.status != WC_OK) {
+        pr.status = w.res.status;
+        pr.error = w.res.error;
+        stop = true;
+        break;
+      }
+      if (w.final_chain) {
+        cons.push_back(std::move(w.chain));
+        assigns.push_back(w.inc);
       } else {
-        make(w->inc, w->level + 1, std::move(w->chain));
+        for (size_t k : w.kids) stack.push_back(k);
       }
     }
   }
-  // an error ends the search: the sub-problems still running finish first
-  // (they read the caller's buffers and this call's request records)
-  for (auto& w : stack) {
-    (void)wait_req(S, w->rq.get());
-    if (w->rq->fb_res) wc_results_free(w->rq->fb_res);
+  // the search is over (or failed): every request still out finishes first
+  // (they read this call's request records and the caller's buffers)
+  {
+    std::unique_lock<std::mutex> lk(S->mu);
+    for (;;) {
+      bool pending = false;
+      for (auto& w : subs)
+        if (!w->done && poll_req(S, w->rq.get()) == 0) pending = true;
+      if (!pending) break;
+      call_cv.wait(lk);
+    }
   }
+  for (auto& w : subs)
+    if (w->rq->fb_res) wc_results_free(w->rq->fb_res);
   if (rc != WC_OK) return rc;
   if (pr.status == WC_OK) priority_assemble(q->n_chains, cons, assigns, pr);
   fill_stats(R.get(), 0.0, 0, std::chrono::duration<double, std::milli>(Clock::now() - t0).count());
