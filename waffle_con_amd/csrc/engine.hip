@@ -1641,7 +1641,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
                          E.L.meta[slot].len[sd], cfg.wildcard, early, E.wcap);
       }
       const uint32_t g = go.st, e = go.e;
-      if (act && (lane & 15) == 0 && g == kG_DONE) E.L.ce[(uint64_t)q * E.nmax + r] = ce16(e);
+      if (act && (lane & 15) == 0 && g == kG_DONE) E.L.ce[WC_IX((uint64_t)q * E.nmax + r, (uint64_t)2 * kNCB * E.nmax)] = ce16(e);
       gc.edinc += go.edinc;
       gc.updates += go.updates;
       gc.w_out += go.w_out;
@@ -1673,7 +1673,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         if (!okm) {
           if (lane == 0) atomicOr(&ctl.ovf, 4u);
         } else if (lane == 0) {
-          E.L.ce[(uint64_t)q2 * E.nmax + r2] = ce16(eo);
+          E.L.ce[WC_IX((uint64_t)q2 * E.nmax + r2, (uint64_t)2 * kNCB * E.nmax)] = ce16(eo);
         }
       }
     }
@@ -1706,7 +1706,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       if (!okh) {
         if (lane == 0) atomicOr(&ctl.ovf, 4u);
       } else if (lane == 0) {
-        E.L.ce[(uint64_t)q * E.nmax + r] = ce16(e);
+        E.L.ce[WC_IX((uint64_t)q * E.nmax + r, (uint64_t)2 * kNCB * E.nmax)] = ce16(e);
       }
     }
     SUB_T1(20, tw);
@@ -1764,9 +1764,9 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
         if (k < cn) {
           // each child's edit distances as its pushes left them (LDS), or
           // from its slot when an activation changed them
-          e1[k] = slot_e ? crs_e(k, 0, r) : ce32(E.L.ce[(uint64_t)(2 * k) * E.nmax + r]);
+          e1[k] = slot_e ? crs_e(k, 0, r) : ce32(E.L.ce[WC_IX((uint64_t)(2 * k) * E.nmax + r, (uint64_t)2 * kNCB * E.nmax)]);
           if (cdual & (1u << k))
-            e2[k] = slot_e ? crs_e(k, 1, r) : ce32(E.L.ce[(uint64_t)(2 * k + 1) * E.nmax + r]);
+            e2[k] = slot_e ? crs_e(k, 1, r) : ce32(E.L.ce[WC_IX((uint64_t)(2 * k + 1) * E.nmax + r, (uint64_t)2 * kNCB * E.nmax)]);
         }
       }
 #pragma unroll
