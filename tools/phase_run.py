@@ -115,9 +115,13 @@ def main():
     c15 = cyc[15]
     rep["chains"] = {"count": c15 & 0xFFFFF, "full": (c15 >> 20) & 0xFFFFF, "accepted_steps": c15 >> 40}
     # wave-0 sub-phases (cycles per chain, summed over workgroups / chains)
-    SUB = {16: "walk-push", 17: "walk-heavy", 18: "walk-nominate", 19: "walk-heavy-count(w0)", 20: "votes-fast",
+    # (the run-length walk: 16 = the lanes' own loops, 17 = the wave's edit-distance
+    # increases and the steps they end, 18 = the whole walk of wave 0, 26 = rounds of
+    # lane loops, 27 = lane-loop iterations, the wave's maximum per round)
+    SUB = {16: "walk-lanes", 17: "walk-heavy", 18: "walk-total(w0)", 19: "walk-heavy-count(w0)", 20: "votes-fast",
            21: "votes-exact", 23: "prepare-windows", 24: "prepare-predict", 25: "votes-exact-count(w0)",
-           26: "nominate-tips", 27: "nominate-code"}
+           26: "walk-rounds(w0)", 27: "walk-lane-iterations(w0)", 40: "accept-tracker-steps(w0)",
+           41: "accept-tracker-loop(w0)", 42: "walk-lane0-iterations"}
     nch = max(1, rep["chains"]["count"])
     rep["sub_cycles_per_chain"] = {SUB[k]: round(cyc[k] / nch, 1) for k in SUB if k < len(cyc)}
     rep["block_cycles_per_chain"] = {PHASES[k]: round(cyc[k] / nch, 1) for k in (8, 9, 10, 11, 14)}

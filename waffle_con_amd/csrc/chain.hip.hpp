@@ -35,26 +35,26 @@ constexpr uint32_t kNomOne = 1u << 8;     // exactly one distinct symbol
 constexpr uint32_t kNomEnd = 1u << 12;    // reached_baseline_end
 constexpr uint32_t kNomActive = 1u << 13; // Some(dwfa)
 constexpr uint32_t kNomOvf = 1u << 14;    // >= 2 symbols: ChainOvf[code & kNomSymMask]
+constexpr uint32_t kNomQuiet = 1u << 15;  // a quiet step: one symbol, the step's next prediction
+constexpr uint16_t kNomQuietCode = (uint16_t)(kNomActive | kNomOne | kNomQuiet);
 
-__device__ __forceinline__ RInfoReg nom_load(const Sh<uint16_t>* nom, const Sh<ChainOvf>* ovf, uint32_t r) {
+__device__ __forceinline__ RInfoReg nom_load(const Sh<uint16_t>* nom, const Sh<ChainOvf>* ovf, uint32_t r,
+                                             uint32_t qsym = 0) {
   const uint32_t c = nom[r];
   RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
   if (!(c & kNomActive)) return x;
   x.e = 0;
   if (c & kNomOvf) {
     const ChainOvf o = ovf[c & kNomSymMask];
-    x.n = o.n;
-    x.split = o.split;
+    x.n = o.n();
+    x.split = o.split();
     x.sym = o.sym;
-    const uint64_t q = o.occ;
-    x.occ = make_uint4((uint32_t)(q & 0xFF) | (uint32_t)((q >> 8) & 0xFF) << 16,
-                       (uint32_t)((q >> 16) & 0xFF) | (uint32_t)((q >> 24) & 0xFF) << 16,
-                       (uint32_t)((q >> 32) & 0xFF) | (uint32_t)((q >> 40) & 0xFF) << 16,
-                       (uint32_t)((q >> 48) & 0xFF) | (uint32_t)((q >> 56) & 0xFF) << 16);
+    x.occ = make_uint4(o.occ_at(0) | o.occ_at(1) << 16, o.occ_at(2) | o.occ_at(3) << 16,
+                       o.occ_at(4) | o.occ_at(5) << 16, o.occ_at(6) | o.occ_at(7) << 16);
   } else if (c & kNomOne) {
     x.n = 1;
     x.split = 1;  // occ / split = 1.0 exactly for a single symbol
-    x.sym = c & kNomSymMask;
+    x.sym = (c & kNomQuiet) ? qsym : (c & kNomSymMask);
     x.occ = make_uint4(1, 0, 0, 0);
   }
   return x;
@@ -87,6 +87,7 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
   SUB_T0(ta);
   // windows: 64 bytes from the lowest tip, 16-byte aligned (reads are
   // 16-byte aligned and the read buffer has 64 bytes of tail padding)
+  uint64_t c0 = 0;
   for (uint32_t r = tid; r < E.n; r += kEB) {
     const RRaw h = rstate_load(&E.L.hot[r]);
     if (rraw_e(h) != kInactive && (rraw_flags(h) & kWide)) atomicOr(&ctl.chain_nochain, 1u);
@@ -109,10 +110,21 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     w[8] = a2.x, w[9] = a2.y, w[10] = a2.z, w[11] = a2.w;
     w[12] = a3.x, w[13] = a3.y, w[14] = a3.z, w[15] = a3.w;
     E.L.cwb[r] = wb;
+    // Every step of an active read starts as a quiet step (it nominates the
+    // step's next prediction with weight 1); the walk stores the code of every
+    // other step. An inactive read nominates nothing. The node's cost is the
+    // base of the steps' costs (chain_votes adds the walk's changes).
+    const bool act = rraw_e(h) != kInactive;
+    const uint16_t qc = act ? kNomQuietCode : (uint16_t)0;
+    Sh<uint16_t>* nm = E.L.cnom + r;
+    for (uint32_t j = 1; j <= K; ++j) nm[j * E.nmax] = qc;
+    if (act) c0 += cost_of(rraw_e(h), E.cfg.cost_mode);
   }
+  c0 = wave_sum_u64(c0);
   const Gm<uint32_t>* pc = E.trk + (E.lcap + 2);  // PQueueTracker processed counts
   for (uint32_t j = tid; j <= K; j += kEB) E.L.cpc[j] = (j >= 1) ? trk_load(&pc[L0 + j]) : 0u;
   __syncthreads();
+  if (lane == 0 && c0) atomicAdd((unsigned long long*)&E.L.cstep[0].cost, (unsigned long long)c0);
   SUB_T1(23, ta);
   SUB_T0(tb);
   {
@@ -342,13 +354,166 @@ __device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, 
   return ok ? e_out : kInactive;
 }
 
+// 8 bytes of an LDS byte array from byte q (the array is dword aligned; bytes
+// the three dword loads touch past its end are never counted)
+__device__ __forceinline__ uint64_t lds_bytes8(const Sh<uint8_t>* a, uint32_t q) {
+  const Sh<uint32_t>* w32 = (const Sh<uint32_t>*)a + (q >> 2);
+  const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2], sh = q & 3u;
+  return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
+}
+
+// The quiet run of one read from step j: the number m (<= lim) of consecutive
+// pushes N_j, N_j+1, ... under which every live tip extends (its read bytes
+// equal the predictions; 8-byte XOR + ctz of the LDS window against the LDS
+// predictions, chunk after chunk). 0 when a live tip is not at the end of the
+// consensus (olen = |N_j-1|), lies at the read's end, or outside the window.
+__device__ __forceinline__ uint32_t lane_run(const Front& f, const Win& W, const Sh<uint8_t>* pred, uint32_t blen,
+                                             uint32_t olen, uint32_t j, uint32_t lim, uint32_t kb, uint32_t& nlive) {
+  uint32_t m = lim;
+  nlive = 0;
+#pragma unroll
+  for (int k = 0; k < kF; ++k) {
+    if ((uint32_t)k >= kb) break;
+    if (!(f.mask & (1u << k))) continue;
+    const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+    const uint32_t q = bo - W.wb;
+    if (f.fd[k] + f.off != olen || bo >= blen || q >= 64u) return 0;
+    const uint32_t mk = min(m, min(blen - bo, 64u - q));
+    uint32_t c = 0;
+    while (c < mk) {
+      const uint64_t mm = nz_bytes(lds_bytes8(W.w, q + c) ^ lds_bytes8(pred, j + c));
+      if (mm) {
+        c += (uint32_t)__builtin_ctzll(mm) >> 3;
+        break;
+      }
+      c += 8;
+    }
+    m = min(mk, c);
+    nlive++;
+  }
+  return m;
+}
+
+// The walk's edit-distance increases for up to four reads of one wave at
+// once, one per 16-lane group (group_edinc, the dual engine's path: the same
+// arithmetic as wave_heavy's register path; a row that outgrows a group's
+// registers goes on in wave_edinc_mem). ls[q] (q < ng) are the lanes whose
+// frontiers wait in gtmp[q]; their reads are ls[q] * kEW + wave, their steps
+// j of those lanes. kFirst: the first rewrite of a row in the chain leaves a
+// copy in slot S (the rows are otherwise only touched at frontier diagonals,
+// which a rollback restores from the node's LDS RStates), and each step's
+// cost change goes to its ChainStep. Returns the backed-up-lanes mask and the
+// groups whose wavefront outgrew its capacity (the chain stops before them).
+struct GHOut {
+  uint64_t bak;
+  uint32_t fail;
+};
+template <bool kFirst>
+__device__ __noinline__ GHOut chain_group_heavy(Sh<RState>* gtmp0, Gm<uint32_t>* nwf, Gm<uint32_t>* swf,
+                                                const Gm<uint8_t>* rbytes, const Sh<uint2>* rt, const Gm<uint8_t>* con,
+                                                uint32_t L0, uint32_t j, uint32_t ls0, uint32_t ls1, uint32_t ls2,
+                                                uint32_t ls3, uint32_t ng, uint32_t wave, uint32_t wcap, int wc,
+                                                bool early, int cost_mode, Lo<Ctl>& ctl, Sh<ChainStep>* cstep,
+                                                Sh<uint32_t>* list, uint32_t list_n, uint64_t bak) {
+  const int lane = lane_id();
+  const uint32_t g = (uint32_t)lane >> 4, gl = (uint32_t)lane & 15u;
+  const uint32_t ls[4] = {uni(ls0), uni(ls1), uni(ls2), uni(ls3)};
+  ng = uni(ng);
+  wave = uni(wave);
+  const uint32_t lsel = g == 0 ? ls[0] : g == 1 ? ls[1] : g == 2 ? ls[2] : ls[3];
+  const bool gact = g < ng;
+  Sh<RState>* gtmp = gtmp0 + g;
+  const uint32_t rl = lsel * kEW + wave;
+  const uint32_t jl = (uint32_t)__shfl((int)j, (int)lsel, 64);
+  const uint32_t e_in = gact ? gtmp->e : 0u;
+  Gm<uint32_t>* gwf = nwf + (uint64_t)rl * wcap;
+  const Gm<uint8_t>* rd = rbytes + (uint64_t)rt[rl].x * 16;
+  const uint32_t blen = rt[rl].y;
+  if (kFirst) {
+    const bool first = gact && !((bak >> lsel) & 1ull);
+    if (first) {
+      Gm<uint32_t>* bdst = swf + (uint64_t)rl * wcap;
+      for (uint32_t i = gl; i < 2 * e_in + 1; i += 16) bdst[i] = gwf[i];
+      if (gl == 0) {
+        const uint32_t k = atomicAdd(&ctl.chain_nbak, 1u);
+        list[WC_IX(2 * k, list_n)] = rl;
+        list[WC_IX(2 * k + 1, list_n)] = 2 * e_in + 1;
+      }
+    }
+    const uint64_t fm = ballot(first && gl == 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if ((fm >> (16 * q)) & 1ull) bak |= 1ull << ls[q];
+    __builtin_amdgcn_wave_barrier();
+  }
+  const GroupOut go = group_edinc(gact, gtmp, gwf, rd, blen, con, L0 + jl, wc, early, wcap);
+  uint32_t st = go.st, e_out = go.e;
+  uint32_t t_ed = go.edinc, t_up = go.updates, t_wo = go.w_out, t_rb = go.rowb, t_cm = go.cmp;
+  // rows that outgrew the group's registers (rare): the wave goes on with each
+  uint64_t mem = ballot(gact && gl == 0 && st == kG_MEM);
+  while (mem) {
+    const uint32_t q = (uint32_t)__builtin_ctzll(mem) >> 4;
+    mem &= mem - 1;
+    const uint32_t rq = ls[q] * kEW + wave;
+    const uint32_t jq = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)ls[q]);
+    const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)e_out, (int)(16 * q));
+    WaveCounters cnt = {0, 0, 0, 0, 0, 0};
+    uint32_t eo = 0;
+    const bool okq = wave_edinc_mem(gtmp0 + q, nwf + (uint64_t)rq * wcap, eq, rbytes + (uint64_t)rt[rq].x * 16,
+                                    rt[rq].y, con, L0 + jq, wc, early, wcap, cnt, eo);
+    if (lane == 0) {
+      t_ed += (uint32_t)cnt.edinc;
+      t_up += (uint32_t)cnt.updates;
+      t_wo += (uint32_t)cnt.w_out;
+      t_rb += (uint32_t)cnt.rowb;
+      t_cm += (uint32_t)cnt.compares;
+    }
+    if (g == q) {
+      st = okq ? kG_DONE : kG_WCAP;
+      e_out = eo;
+    }
+  }
+  const uint32_t s_up = wave_sum_u32(t_up), s_wo = wave_sum_u32(t_wo), s_cm = wave_sum_u32(t_cm),
+                 s_ed = wave_sum_u32(t_ed), s_rb = wave_sum_u32(t_rb);
+  if (lane == 0) {
+    atomicAdd((unsigned long long*)&ctl.chain_tot[0], (unsigned long long)s_up);
+    atomicAdd((unsigned long long*)&ctl.chain_tot[1], (unsigned long long)s_wo);
+    atomicAdd((unsigned long long*)&ctl.chain_tot[2], (unsigned long long)s_cm);
+    atomicAdd((unsigned long long*)&ctl.chain_tot[3], (unsigned long long)s_ed);
+    atomicAdd((unsigned long long*)&ctl.chain_tot[4], (unsigned long long)s_rb);
+  }
+  if (gact && gl == 0) {
+    if (st == kG_WCAP) atomicMin(&ctl.chain_stop, jl - 1);
+    else if (kFirst && e_out != e_in)  // the node cost from step jl on (chain_votes sums the changes)
+      atomicAdd((unsigned long long*)&cstep[jl].cost,
+                (unsigned long long)(cost_of(e_out, cost_mode) - cost_of(e_in, cost_mode)));
+  }
+  const uint64_t fb = ballot(gact && gl == 0 && st == kG_WCAP);
+  GHOut o;
+  o.bak = bak;
+  o.fail = (uint32_t)((fb & 1ull) | ((fb >> 15) & 2ull) | ((fb >> 30) & 4ull) | ((fb >> 45) & 8ull));
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  return o;
+}
+
 // (C) push the K predicted symbols through every read, thread per read.
-// kFirst: speculative pass; stores each step's nominations and aggregates,
-// leaves the final RStates in slot S. Replay pass: writes the final RStates to
-// the LDS copy and the last step's nominations to rinfo (the analysis cache).
-// Both passes add their work counters to ctl.chain_tot. Wavefront rows are
-// written lazily (thread_push<kLazy>): only when a diagonal leaves the
-// frontier, plus one flush of the final frontier.
+// Each lane walks its own read through the steps (a run-length walk): from
+// step j, a read whose live tips all match the next m predictions takes the
+// first m - 1 of those steps at once (their pushes extend every tip, and each
+// of them nominates exactly the next prediction with weight 1: the code
+// chain_prepare stored for every (step, read)); the step after the run, and
+// any step where a tip mismatches or the read ends, takes the step path (push,
+// tip bytes, nominations). A lane stops when its push needs an edit-distance
+// increase; the wave then runs those, one read at a time (wave_heavy), and the
+// lanes go on. The step aggregates are computed from the nominations after
+// the walk (chain_votes); the walk only adds each step's cost change.
+// kFirst: speculative pass; stores each step's nominations, leaves the final
+// RStates in slot S. Replay pass: writes the final RStates to the LDS copy and
+// the last step's nominations to rinfo (the analysis cache). Both passes add
+// their work counters to ctl.chain_tot. Wavefront rows are written lazily
+// (thread_push<kLazy>): only when a diagonal leaves the frontier, plus one
+// flush of the final frontier.
 template <bool kFirst>
 __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, uint32_t K, uint32_t S) {
   const int lane = lane_id(), wave = wave_id();
@@ -356,6 +521,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   // every wave walks a quarter of the reads, so the edit-distance increases,
   // which a wave handles one read at a time, are spread over all four
   if ((uint32_t)wave >= E.n) return;  // no reads in this wave (no barriers below)
+  SUB_T0(tw);
   const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
   const int wc = cfg.wildcard;
@@ -376,12 +542,9 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   }
   const bool active = has && f.e != kInactive;
   Gm<uint32_t>* wf_row = v.wf + (uint64_t)r * E.wcap;
-  Sh<RState>* tmp = &E.L.ctmp[wave];
   uint32_t t_upd = 0, t_wout = 0, t_cmp = 0;
   uint64_t bak = 0;  // lanes whose row was backed up (wave-uniform)
-  // this wave's share of the node cost; changes only when an edit distance grows
-  uint64_t wcost = kFirst ? wave_sum_u64(active ? cost_of(f.e, cfg.cost_mode) : 0ull) : 0ull;
-  TipBytes x;  // bytes at the current tips
+  TipBytes x;        // bytes at the current tips
   // frontier entries sit at mask bits below 32 - clz(mask) (entries only
   // leave between rebuilds): kb, the wave's largest such bound, is a scalar
   // loop bound for the per-entry work (typically 1-3 of the kF = 8 slots)
@@ -393,18 +556,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     const bool oob = win_tip_bytes(W, f, blen, kb, x) && active;
     if (kFirst && ballot(oob) && lane == 0) atomicMin(&ctl.chain_stop, 0u);
   }
-  // predicted symbols in a register: lane t holds N_t's symbol (t <= K + 1 < 64)
-  const uint32_t predv = (uint32_t)E.L.cpred[min((uint32_t)lane, K + 1)];
-  auto pred_at = [&](uint32_t t) { return (uint32_t)__builtin_amdgcn_readlane((int)predv, (int)t); };
-  // lane t: the predictions N_t .. N_t+7 packed (bytes past N_K+1 are never compared)
-  uint32_t plo = 0, phi = 0;
-#pragma unroll
-  for (uint32_t u = 0; u < 4; ++u) {
-    plo |= (uint32_t)E.L.cpred[min((uint32_t)lane + u, 127u)] << (8 * u);
-    phi |= (uint32_t)E.L.cpred[min((uint32_t)lane + 4 + u, 127u)] << (8 * u);
-  }
-  uint64_t a_cost = 0, a_po = 0, a_ef = 0;  // kFirst: step (lane) aggregates of this wave
-  uint32_t jlast = 0;                       // last step this wave walked
+  const Sh<uint8_t>* pred = E.L.cpred;  // pred[t] = N_t's symbol
 #ifdef WC_NO_FF
   const bool ffon = false;
 #else
@@ -413,54 +565,56 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   // the step path takes it)
   const bool ffon = true;
 #endif
-  for (uint32_t j = 1; j <= K; ++j) {
-    const uint32_t stopv =
-        kFirst ? uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) : K;
-    if (kFirst && j > stopv) break;
-    // ---- quiet steps in bulk ----
-    // From step j, read r's pushes match for m steps when every live tip
-    // slot's read bytes equal the predictions N_j, N_j+1, ... (8-byte XOR +
-    // ctz against the LDS window); the first m - 1 of those steps then
-    // nominate exactly the next prediction with weight 1. Steps every read of
-    // the wave is quiet in are applied at once: tips advance, the counters
-    // grow by the per-step amounts, each step votes 840/840 per active read
-    // for its prediction and nothing else. Step K and every other step take
-    // the step path below.
-    if (ffon && j < K) {
-      uint32_t qn = 8;  // inactive lanes never limit the run
-      uint32_t nlive = 0;
-      if (active) {
-        qn = 0;
-        if (f.mask != 0 && f.maxb != blen) {
-          const uint64_t p8 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)plo, (int)j) |
-                              (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)phi, (int)j) << 32;
-          uint32_t m = min(8u, K - j + 1);
-          bool ok = true;
-#pragma unroll
-          for (int k = 0; k < kF; ++k) {
-            if ((uint32_t)k >= kb) break;
-            if (!(f.mask & (1u << k))) continue;
-            const uint32_t bo = f.fd[k] + f.e - f.fi[k];
-            ok &= f.fd[k] + f.off == L0 + j - 1 && bo < blen;
-            const uint32_t q = bo - W.wb;
-            // 8 window bytes from q: three aligned dwords, funnel-shifted
-            // (the window slot is dword aligned; bytes past 64 are not used)
-            const Sh<uint32_t>* w32 = (const Sh<uint32_t>*)W.w + (min(q, 63u) >> 2);
-            const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2], sh = q & 3u;
-            const uint64_t r8 = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
-                                (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
-            const uint64_t mm = nz_bytes(r8 ^ p8);
-            const uint32_t t0 = mm ? (uint32_t)__builtin_ctzll(mm) >> 3 : 8u;
-            m = min(m, min(t0, min(blen - bo, q < 64u ? 64u - q : 0u)));
-            nlive++;
-          }
-          qn = ok && m >= 1 ? m - 1 : 0u;
+  Sh<uint16_t>* nom_r = E.L.cnom + r;  // cnom[j * nmax + r]
+  uint32_t j = 1;                      // this lane's next step
+  uint32_t jend = active ? K : 0u;     // its last step (lowered when it stops the chain)
+  bool pend = false;                   // step j's push needs an edit-distance increase
+  // the rest of step j after its push: the bytes at the new tips and the
+  // node's nominations (kFirst: into cnom; replay: the analysis cache at K)
+  auto step_tail = [&]() {
+    const bool oob = win_tip_bytes(W, f, blen, kb, x);
+    const Nom o = chain_nominate(f, x, blen, L0 + j, kb);
+    if (kFirst) {
+      bool stop = oob;
+      uint32_t code = kNomActive | (o.end ? kNomEnd : 0u) | (uint32_t)(o.sym & 0xFF) | (o.n == 1 ? kNomOne : 0u);
+      if (o.n > 1) {
+        const uint32_t idx = atomicAdd(&ctl.chain_novf, 1u);
+        if (idx < kChainOvf) {
+          E.L.covf[idx].set(o.sym, o.occ, o.split, o.n);
+          code = (code & ~kNomSymMask) | kNomOvf | idx;
+        } else {
+          stop = true;
         }
       }
-      uint32_t Q = 8u - wave_max_u32(8u - qn);
-      Q = min(Q, min(K - j, stopv - j));  // the step after the run is walked normally, and none past the stop
-      if (Q > 0) {
-        if (active) {
+      nom_r[j * E.nmax] = (uint16_t)code;
+      if (stop) {
+        atomicMin(&ctl.chain_stop, j - 1);
+        jend = j - 1;
+      }
+    } else if (j == K) {
+      rinfo_store(&E.L.rinfo[r], o, f.e);
+    }
+    ++j;
+  };
+  for (;;) {
+    const uint32_t stopv =
+        kFirst ? uni(__hip_atomic_load(&ctl.chain_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) : K;
+    uint32_t lim = min(jend, stopv);
+    SUB_T0(ta);
+#ifdef WC_PHASE_PROF
+    uint32_t it = 0;
+#endif
+    while (j <= lim) {
+#ifdef WC_PHASE_PROF
+      ++it;
+#endif
+      // ---- this read's quiet run from step j ----
+      if (ffon && j < K && f.mask != 0 && f.maxb != blen) {
+        uint32_t nlive;
+        const uint32_t m = lane_run(f, W, pred, blen, L0 + j - 1, j, K - j + 1, kb, nlive);
+        // the run's last push nominates the byte after the run: the step path takes it
+        const uint32_t Q = m >= 1 ? min(m - 1, lim - j) : 0u;
+        if (Q > 0) {
 #pragma unroll
           for (int k = 0; k < kF; ++k) {
             if ((uint32_t)k >= kb) break;
@@ -469,46 +623,47 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
           t_upd += Q;
           t_wout += Q * (2 * f.e + 1);
           t_cmp += Q * (f.nscmp + nlive);
+          j += Q;
+          win_tip_bytes(W, f, blen, kb, x);  // the tips moved (all inside the window)
         }
-        if (kFirst) {
-          const uint64_t nact = (uint64_t)__popcll((unsigned long long)ballot(active));
-          if ((uint32_t)lane >= j && (uint32_t)lane < j + Q) {
-            a_cost = wcost;
-            a_po = (uint64_t)kVoteDen * nact;
-            a_ef = 0;
-          }
-          if (has)
-            for (uint32_t t = j; t < j + Q; ++t)
-              E.L.cnom[t * E.nmax + r] = (uint16_t)(active ? (kNomActive | kNomOne | pred_at(t + 1)) : 0u);
-          jlast = j + Q - 1;
-        }
-        j += Q;
-        win_tip_bytes(W, f, blen, kb, x);  // the tips moved (all inside the window)
       }
-    }
-    const uint32_t sym = pred_at(j);
-    const uint32_t nsym = j < K ? pred_at(j + 1) : 0x100u;  // the next prediction (`pred` below)
-    const uint32_t olen = L0 + j;
-    uint32_t cmp = 0;
-    bool heavy = false;
-    SUB_T0(ta);
-    if (active) heavy = chain_push(f, x, blen, olen - 1, sym, wc, early, wf_row, kb, cmp);
-    t_cmp += cmp;
-    if (active && !heavy) {
+      // ---- step j ----
+      uint32_t cmp = 0;
+      const bool heavy = chain_push(f, x, blen, L0 + j - 1, (uint32_t)pred[j], wc, early, wf_row, kb, cmp);
+      t_cmp += cmp;
+      if (heavy) {
+        pend = true;
+        break;
+      }
       t_upd++;
       t_wout += 2 * f.e + 1;
+      step_tail();
+      lim = min(lim, jend);
     }
-    uint64_t hm = ballot(heavy);
+#ifdef WC_PHASE_PROF
+    SUB_CNT(27, wave_max_u32(it));
+    SUB_CNT(42, it);
+    SUB_CNT(26, 1);
+#endif
     SUB_T1(16, ta);
+    uint64_t hm = ballot(pend);
+    if (!hm) break;
     SUB_CNT(19, __popcll(hm));
     SUB_T0(tb);
-    while (hm) {  // edit-distance increase: the wave works on one read at a time
+// The 2-waves-per-SIMD build (WC_LOWLAT, 256 VGPRs) runs the edit-distance
+// increases of up to four reads at once (chain_group_heavy); in the 4-wave build the call's
+// register needs make the walk spill, which cost more than the overlap saves
+// under load (cfg2 batch 32.7 vs 27.6 ms; one locus alone 19.1 vs 19.9 ms in
+// the 2-wave build): one read at a time there.
+#if !defined(WC_LOWLAT) || defined(WC_SEQ_HEAVY)
+    while (hm) {  // edit-distance increases: the wave works on one read at a time
       const int l = __builtin_ctzll(hm);
       hm &= hm - 1;
-      if (lane == l) front_store(tmp, f);
+      const uint32_t jl = (uint32_t)__builtin_amdgcn_readlane((int)j, l);
+      if (lane == l) front_store(&E.L.ctmp[4 * wave], f);
       wave_lds_sync();
       const uint32_t rl = (uint32_t)l * kEW + (uint32_t)wave;
-      const uint32_t e_in = uni(tmp->e);
+      const uint32_t e_in = uni(E.L.ctmp[4 * wave].e);
       Gm<uint32_t>* bdst = nullptr;
       if (kFirst && !((bak >> l) & 1ull)) {
         // first rewrite of this row in the chain: chain_heavy keeps a copy in
@@ -522,109 +677,77 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
         }
         bak |= 1ull << l;
       }
-      const uint32_t e_out = chain_heavy(tmp, v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, olen,
-                                         sym, wc, early, E.wcap, ctl.chain_tot, bdst);
+      const uint32_t e_out = uni(chain_heavy(&E.L.ctmp[4 * wave], v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, L0 + jl,
+                                             (uint32_t)pred[jl], wc, early, E.wcap, ctl.chain_tot, bdst));
       const bool ok = e_out != kInactive;
       wave_lds_sync();
-      if (!ok && lane == 0) atomicMin(&ctl.chain_stop, j - 1);
-      if (ok) wcost += cost_of(uni(e_out), cfg.cost_mode) - cost_of(e_in, cfg.cost_mode);
+      if (lane == 0) {
+        if (!ok) atomicMin(&ctl.chain_stop, jl - 1);
+        else if (kFirst && e_out != e_in)  // the node cost from step jl on (chain_votes sums the changes)
+          atomicAdd((unsigned long long*)&E.L.cstep[jl].cost,
+                    (unsigned long long)(cost_of(e_out, cfg.cost_mode) - cost_of(e_in, cfg.cost_mode)));
+      }
       if (lane == l) {
-        const RRaw t = rstate_load(tmp);
-        if (kFirst && (rraw_flags(t) & kWide)) atomicMin(&ctl.chain_stop, j - 1);  // not a thread-path state
+        const RRaw t = rstate_load(&E.L.ctmp[4 * wave]);
+        bool stop = !ok;
+        if (kFirst && (rraw_flags(t) & kWide)) {  // not a thread-path state
+          atomicMin(&ctl.chain_stop, jl - 1);
+          stop = true;
+        }
+        if (stop) jend = jl - 1;
         front_load(t, f);
       }
       wave_lds_sync();
     }
+#else
+    // edit-distance increases: up to four reads at once, one per 16-lane
+    // group (chain_group_heavy); the selected lanes hand their frontiers over
+    // in LDS, so the call keeps the walk's register allocation
+    while (hm) {
+      uint32_t ls[4], ng = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ls[q] = hm ? (uint32_t)__builtin_ctzll(hm) : 0u;
+        if (hm) {
+          hm &= hm - 1;
+          ng++;
+        }
+      }
+      const bool mine = (uint32_t)lane == ls[0] || (ng > 1 && (uint32_t)lane == ls[1]) ||
+                        (ng > 2 && (uint32_t)lane == ls[2]) || (ng > 3 && (uint32_t)lane == ls[3]);
+      const uint32_t myg = (uint32_t)lane == ls[0] ? 0u : (uint32_t)lane == ls[1] ? 1u : (uint32_t)lane == ls[2] ? 2u : 3u;
+      if (mine) front_store(&E.L.ctmp[4 * wave + myg], f);
+      wave_lds_sync();
+      const GHOut gh = chain_group_heavy<kFirst>(E.L.ctmp + 4 * wave, v.wf, E.sv(S, 0).wf, E.rbytes, E.L.rt, v.con, L0, j,
+                                                 ls[0], ls[1], ls[2], ls[3], ng, (uint32_t)wave, E.wcap, wc, early,
+                                                 cfg.cost_mode, ctl, E.L.cstep, E.L.list,
+                                                 (uint32_t)list_entries(E.sides, E.nmax), bak);
+      bak = gh.bak;
+      if (mine) {
+        const RRaw t = rstate_load(&E.L.ctmp[4 * wave + myg]);
+        bool stop = ((gh.fail >> myg) & 1u) != 0;
+        if (kFirst && (rraw_flags(t) & kWide)) {  // not a thread-path state
+          atomicMin(&ctl.chain_stop, j - 1);
+          stop = true;
+        }
+        if (stop) jend = j - 1;
+        front_load(t, f);
+      }
+      wave_lds_sync();
+    }
+#endif
+    kb = front_bound();  // rebuilt frontiers
+    if (pend) {
+      pend = false;
+      if (j <= jend) step_tail();
+    }
     SUB_T1(17, tb);
-    SUB_T0(tc);
-    if (ballot(heavy)) kb = front_bound();  // rebuilt frontiers
-    // bytes at the new tips: this node's nominations and the next push
-    const bool oob = win_tip_bytes(W, f, blen, kb, x) && active;
+  }
+  if (!kFirst && has && !active) {
     Nom o;
     o.sym = o.occ = 0;
     o.n = o.split = o.end = 0;
-    if (active) o = chain_nominate(f, x, blen, olen, kb);
-    SUB_T1(26, tc);
-    SUB_T0(td);
-    if (kFirst) {
-      bool stop = oob;
-      if (has) {
-        uint32_t code = 0;
-        if (active) {
-          code = kNomActive | (o.end ? kNomEnd : 0u) | (uint32_t)(o.sym & 0xFF) | (o.n == 1 ? kNomOne : 0u);
-          if (o.n > 1) {
-            const uint32_t idx = atomicAdd(&ctl.chain_novf, 1u);
-            if (idx < kChainOvf) {
-              auto& q = E.L.covf[idx];
-              q.sym = o.sym;
-              q.occ = o.occ;
-              q.split = o.split;
-              q.n = o.n;
-              code = (code & ~kNomSymMask) | kNomOvf | idx;
-            } else {
-              stop = true;
-            }
-          }
-        }
-        E.L.cnom[j * E.nmax + r] = (uint16_t)code;
-      }
-      SUB_T1(27, td);
-      // step aggregates: cost; reads at their end; votes for the predicted
-      // next symbol (P) and for all other symbols (O) in 1/840ths; counts of
-      // multi-symbol reads and of fractional votes for the prediction
-      const uint32_t pred = nsym;
-      uint32_t vp = 0, vo = 0;
-      bool frac = false;
-      // (votes for the wildcard symbol count in neither: chain_votes)
-      const uint32_t wsym = wc >= 0 ? (uint32_t)(uint8_t)wc : 0x100u;
-      if (active && o.n > 0) {
-        if (o.n == 1) {
-          const uint32_t s0 = (uint32_t)(o.sym & 0xFF);
-          if (s0 == pred) vp = kVoteDen;
-          else if (s0 != wsym) vo = kVoteDen;
-        } else {
-          const uint32_t unit = vote_unit(o.split);
-          for (uint32_t k = 0; k < o.n; ++k) {
-            const uint32_t c = unit * (uint32_t)((o.occ >> (8 * k)) & 0xFF);
-            const uint32_t sk = (uint32_t)((o.sym >> (8 * k)) & 0xFF);
-            if (sk == pred) {
-              vp += c;
-              frac = true;
-            } else if (sk != wsym) {
-              vo += c;
-            }
-          }
-        }
-      }
-      const uint64_t nend = (uint64_t)__popcll((unsigned long long)ballot(active && o.end));
-      const uint64_t mm = ballot(active && o.n > 1);
-      const uint64_t nmul = (uint64_t)__popcll((unsigned long long)mm);
-      const uint64_t nfrac = (uint64_t)__popcll((unsigned long long)ballot(frac));
-      uint64_t po;
-      if (mm == 0)  // every vote is 0 or one whole read: count with ballots
-        po = (uint64_t)kVoteDen * (uint64_t)__popcll((unsigned long long)ballot(vp != 0)) |
-             ((uint64_t)kVoteDen * (uint64_t)__popcll((unsigned long long)ballot(vo != 0)) << 32);
-      else
-        po = (uint64_t)wave_sum_u32(vp) | ((uint64_t)wave_sum_u32(vo) << 32);
-      if (ballot(stop) && lane == 0) atomicMin(&ctl.chain_stop, j - 1);
-      // lane j keeps step j's aggregates (j <= K < 64); they go to LDS once,
-      // after the walk, one atomic per aggregate for all steps at once
-      if ((uint32_t)lane == j) {
-        a_cost = wcost;
-        a_po = po;
-        a_ef = nend | nmul << 16 | nfrac << 32;
-      }
-      jlast = j;
-    } else if (j == K && has) {
-      rinfo_store(&E.L.rinfo[r], o, f.e);
-    }
-    SUB_T1(18, tc);
-  }
-  if (kFirst && lane >= 1 && (uint32_t)lane <= jlast) {
-    auto& st = E.L.cstep[lane];
-    atomicAdd((unsigned long long*)&st.cost, (unsigned long long)a_cost);
-    atomicAdd((unsigned long long*)&st.po, (unsigned long long)a_po);
-    atomicAdd((unsigned long long*)&st.ef, (unsigned long long)a_ef);
+    rinfo_store(&E.L.rinfo[r], o, f.e);
   }
   if (active) front_flush(f, wf_row);  // lazy rows: write the final frontier
   if (has) {
@@ -639,21 +762,90 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     atomicAdd((unsigned long long*)&ctl.chain_tot[1], (unsigned long long)s_wout);
     atomicAdd((unsigned long long*)&ctl.chain_tot[2], (unsigned long long)s_cmp);
   }
+  SUB_T1(18, tw);
 }
 
-// (D) per chain node N_j, j < K: ok[j] = exactly one passing candidate and it
-// is the predicted symbol j+1 (consensus.rs:283-321). Unless the wildcard is
-// predicted, the walk's exact rational vote totals (prediction vs every other
-// non-wildcard symbol) decide almost every step; the rest take the exact path
-// (per-key f64 sums in read order, hashbrown key order).
-__device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t K) {
+// (D) Step aggregates, then per chain node N_j, j < Keff: ok[j] = exactly one
+// passing candidate and it is the predicted symbol j+1 (consensus.rs:283-321).
+// Aggregates of step j (1 <= j <= Keff) from the walk's nomination codes: the
+// node cost (N_0's plus the walk's changes up to j), reads at their end, and
+// the votes for the predicted next symbol (P) and for all other non-wildcard
+// symbols (O) in exact 1/840ths, with the counts of multi-symbol reads and of
+// fractional votes for the prediction. Unless the wildcard is predicted, P and
+// O decide almost every step; the rest take the exact path (per-key f64 sums
+// in read order, hashbrown key order).
+__device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t Keff, uint32_t K) {
   const int lane = lane_id();
   const DevConfig& cfg = E.cfg;
-  for (uint32_t j = 1 + wave_id(); j < K; j += kEW) {
+  if (wave_id() == 0) {
+    // step costs: the running sum of the per-step changes (Keff <= K < 64)
+    uint64_t d = ((uint32_t)lane >= 1 && (uint32_t)lane <= Keff) ? E.L.cstep[lane].cost : 0ull;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t t = __shfl_up(d, (unsigned)o, 64);
+      if (lane >= o) d += t;
+    }
+    if ((uint32_t)lane >= 1 && (uint32_t)lane <= Keff) E.L.cstep[lane].cost = E.L.cstep[0].cost + d;
+  }
+  const uint32_t wsym = cfg.wildcard >= 0 ? (uint32_t)(uint8_t)cfg.wildcard : 0x100u;
+  for (uint32_t j = 1 + wave_id(); j <= Keff; j += kEW) {
     SUB_T0(ta);
     auto& st = E.L.cstep[j];
-    const uint64_t po = st.po, ef = st.ef;
-    const uint64_t P = po & 0xFFFFFFFFull, O = po >> 32;
+    const uint32_t pred = j < K ? (uint32_t)E.L.cpred[j + 1] : 0x100u;
+    const Sh<uint16_t>* nom = E.L.cnom + j * E.nmax;
+    // one code per lane and 64-read block (n <= 256 with chains), all loaded
+    // under one wait; single-symbol votes are counted with ballots, the
+    // multi-symbol reads (rare) add their fractions lane-parallel
+    uint32_t cc[4];
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) {
+      const uint32_t r = 64u * b + (uint32_t)lane;
+      cc[b] = r < E.n ? (uint32_t)nom[r] : 0u;
+    }
+    uint32_t np = 0, no = 0, nend = 0, nmul = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) {
+      const uint32_t c = cc[b];
+      const uint32_t s0 = (c & kNomQuiet) ? pred : (c & kNomSymMask);
+      const bool one = (c & kNomOne) != 0;  // (codes with kNomOne or kNomOvf are active)
+      np += (uint32_t)__popcll((unsigned long long)ballot(one && s0 == pred));
+      no += (uint32_t)__popcll((unsigned long long)ballot(one && s0 != pred && s0 != wsym));
+      nend += (uint32_t)__popcll((unsigned long long)ballot((c & (kNomActive | kNomEnd)) == (kNomActive | kNomEnd)));
+      nmul += (uint32_t)__popcll((unsigned long long)ballot((c & kNomOvf) != 0));
+    }
+    uint64_t P = (uint64_t)kVoteDen * np, O = (uint64_t)kVoteDen * no;
+    uint32_t nfrac = 0;
+    if (nmul) {
+      uint32_t vp = 0, vo = 0, fr = 0;
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t c = cc[b];
+        if (!(c & kNomOvf)) continue;
+        const ChainOvf q = E.L.covf[c & kNomSymMask];
+        const uint32_t unit = vote_unit(q.split());
+        bool frac = false;
+        for (uint32_t k = 0; k < q.n(); ++k) {
+          const uint32_t w = unit * q.occ_at(k);
+          const uint32_t sk = (uint32_t)((q.sym >> (8 * k)) & 0xFF);
+          if (sk == pred) {
+            vp += w;
+            frac = true;
+          } else if (sk != wsym) {
+            vo += w;
+          }
+        }
+        if (frac) fr++;
+      }
+      P += wave_sum_u32(vp);
+      O += wave_sum_u32(vo);
+      nfrac = wave_sum_u32(fr);
+    }
+    const uint64_t ef = (uint64_t)nend | (uint64_t)nmul << 16 | (uint64_t)nfrac << 32;
+    if (lane == 0) {
+      st.po = P | O << 32;
+      st.ef = ef;
+    }
+    if (j >= Keff) break;  // N_Keff: aggregates only (the commit's cost and end counts)
     const uint32_t multi = step_nmulti(ef) ? 1u : 0u;
     const uint64_t M = (uint64_t)kVoteDen * cfg.min_count;
     // Exact rational votes (P, O in 1/840ths); the f64 sums of the reference
@@ -675,10 +867,9 @@ __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t K) {
     SUB_T0(tb);
     bool ok = dec == 1;
     if (dec < 0) {
-      const Sh<uint16_t>* nom = E.L.cnom + j * E.nmax;
       uint32_t m = 0, key = 0;
       double val = 0.0;
-      ok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r); }, [&](uint32_t) { return 1.0; },
+      ok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r, pred); }, [&](uint32_t) { return 1.0; },
                            E.n, false, multi != 0, cfg.wildcard, m, key, val);
       if (ok) {
         const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
@@ -725,11 +916,13 @@ __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint3
   uint32_t jstar = Keff >= 1 ? 1u : 0u;
   uint64_t thr = ctl.trk_thr[0], farthest = ctl.farthest[0], lcnst = ctl.last_constraint[0];
   uint64_t others = ctl.trk_total[0];
+  SUB_T0(ta);
   for (uint32_t j = 1; j < Keff && j < jbad; ++j) {
     const uint64_t L = L0 + j;
     uint64_t t_thr = thr, t_l = lcnst, t_oth = others;
     while ((t_oth + (L >= t_thr ? 1u : 0u) > cfg.max_queue_size || t_l >= cfg.max_nodes_wo_constraint) &&
            t_thr < farthest) {
+      SUB_CNT(40, 1);
       if (t_oth) t_oth -= trk_load(&lc[t_thr]);
       t_thr++;
       t_l = 0;
@@ -741,6 +934,7 @@ __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint3
     farthest = max(farthest, L);
     jstar = j + 1;
   }
+  SUB_T1(41, ta);
   if (jl < jstar) pc[L0 + jl] = E.L.cpc[jl] + 1;
   if (lane == 0) {
     ctl.trk_thr[0] = thr;
@@ -802,7 +996,7 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
   __syncthreads();
   PH_MARK(9);
   const uint32_t Keff = uni(ctl.chain_stop);
-  chain_votes(E, ctl, Keff);
+  chain_votes(E, ctl, Keff, K);
   __syncthreads();
   PH_MARK(10);
   if (wave_id() == 0) {

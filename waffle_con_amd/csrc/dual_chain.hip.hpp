@@ -285,11 +285,7 @@ __device__ inline void dual_chain_walk(Eng& E, Lo<Ctl>& ctl, const DualChainArea
             if (o[s].n > 1) {
               const uint32_t idx = atomicAdd(&ctl.chain_novf, 1u);
               if (idx < kChainOvf) {
-                auto& q = E.L.covf[idx];
-                q.sym = o[s].sym;
-                q.occ = o[s].occ;
-                q.split = o[s].split;
-                q.n = o[s].n;
+                E.L.covf[idx].set(o[s].sym, o[s].occ, o[s].split, o[s].n);
                 code = (code & ~kNomSymMask) | kNomOvf | idx;
               } else {
                 stop = true;

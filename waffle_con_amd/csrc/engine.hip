@@ -216,7 +216,7 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
     l.covf = (Sh<ChainOvf>*)p;
     p += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
     l.ctmp = (Sh<RState>*)p;
-    p += (uint64_t)kWaves * 64;
+    p += (uint64_t)kWaves * 4 * 64;
     l.cnom = (Sh<uint16_t>*)p;
     p += align16(S * (K + 1) * nmax * 2);
     l.cwin = p;

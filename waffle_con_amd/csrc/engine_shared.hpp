@@ -143,7 +143,7 @@ __host__ __device__ inline uint64_t rtab_bytes(uint32_t nmax) {
 // staging stride of one read pulled from host memory (EngineArgs::hreads): its
 // bytes rounded up to 16, then 64 zero bytes (the engine's over-read margin)
 __host__ __device__ inline uint64_t rstage_stride(uint32_t maxlen) { return ((uint64_t)maxlen + 15) / 16 * 16 + 64; }
-constexpr int kPhases = 40;  // 32..39: chain statistics of the dual engine (engine.hip, dual chain call site)
+constexpr int kPhases = 48;  // 32..39: chain statistics of the dual engine (engine.hip, dual chain call site); 40..: single-engine chain counters
 // offset-activation scratch per workgroup (u64): per wave two lane-interleaved pair arrays of m entries
 __host__ __device__ inline uint64_t act_scr_u64(uint32_t m) { return (uint64_t)kWaves * 2 * m * 64; }  // 0..15 block phases, 16..31 wave-0 sub-phases
 
@@ -231,9 +231,21 @@ __host__ __device__ inline uint32_t step_nend(uint64_t ef) { return (uint32_t)(e
 __host__ __device__ inline uint32_t step_nmulti(uint64_t ef) { return (uint32_t)((ef >> 16) & 0xFFFFu); }
 __host__ __device__ inline uint32_t step_nfrac(uint64_t ef) { return (uint32_t)((ef >> 32) & 0xFFFFu); }
 struct ChainOvf {  // nominations of a read with >= 2 distinct tip symbols
-  uint64_t sym, occ;  // bytes in iteration order
-  uint32_t split, n;
+  uint64_t sym;  // bytes in iteration order
+  uint32_t occ;  // nibble k: occurrences of symbol k (<= kF = 8 tips)
+  uint32_t sn;   // split | n << 8
+  __host__ __device__ void set(uint64_t s, uint64_t occ_bytes, uint32_t split, uint32_t n) {
+    sym = s;
+    uint32_t o = 0;
+    for (uint32_t k = 0; k < 8; ++k) o |= (uint32_t)((occ_bytes >> (8 * k)) & 15u) << (4 * k);
+    occ = o;
+    sn = split | n << 8;
+  }
+  __host__ __device__ uint32_t occ_at(uint32_t k) const { return (occ >> (4 * k)) & 15u; }
+  __host__ __device__ uint32_t split() const { return sn & 0xFFu; }
+  __host__ __device__ uint32_t n() const { return sn >> 8; }
 };
+static_assert(sizeof(ChainOvf) == 16, "ChainOvf layout");
 // Read windows of the chain walk: 64 bytes of each read in LDS. The walk reads
 // them per step, one read per lane (read r = 4 * lane + wave), so they are laid
 // out for the LDS banks: read r's window is slot (r & 3) * m4 + (r >> 2)
@@ -258,14 +270,14 @@ inline uint32_t env_chain_kinds() {
   return e ? (uint32_t)atoi(e) & 3u : 3u;
 }
 // chain LDS (per side S = chain_sides: the dual engine's chains walk both):
-//   steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves] | nom[S][K+1][nmax] u16 |
+//   steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves][4] | nom[S][K+1][nmax] u16 |
 //   win[S][4*m4][68 B] (read windows) | wb[S][nmax] u32 | pc[K+1] u32 | pred[S][K+2] u8
 __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K, uint32_t sides = 1) {
   if (K == 0) return 0;
   const uint64_t S = chain_sides(sides);
   uint64_t t = align16((uint64_t)(K + 1) * (S == 2 ? sizeof(DualStep) : sizeof(ChainStep)));
   t += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
-  t += (uint64_t)kWaves * 64;
+  t += (uint64_t)kWaves * 4 * 64;  // per wave, one RState per 16-lane group
   t += align16(S * (K + 1) * nmax * 2);
   t += align16(S * 4 * win_m4(nmax) * kWinStride);
   t += align16(S * nmax * 4);
