@@ -38,9 +38,7 @@ constexpr uint32_t kNomOvf = 1u << 14;    // >= 2 symbols: ChainOvf[code & kNomS
 constexpr uint32_t kNomQuiet = 1u << 15;  // a quiet step: one symbol, the step's next prediction
 constexpr uint16_t kNomQuietCode = (uint16_t)(kNomActive | kNomOne | kNomQuiet);
 
-__device__ __forceinline__ RInfoReg nom_load(const Sh<uint16_t>* nom, const Sh<ChainOvf>* ovf, uint32_t r,
-                                             uint32_t qsym = 0) {
-  const uint32_t c = nom[r];
+__device__ __forceinline__ RInfoReg nom_decode(uint32_t c, const Sh<ChainOvf>* ovf, uint32_t qsym) {
   RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
   if (!(c & kNomActive)) return x;
   x.e = 0;
@@ -58,6 +56,10 @@ __device__ __forceinline__ RInfoReg nom_load(const Sh<uint16_t>* nom, const Sh<C
     x.occ = make_uint4(1, 0, 0, 0);
   }
   return x;
+}
+__device__ __forceinline__ RInfoReg nom_load(const Sh<uint16_t>* nom, const Sh<ChainOvf>* ovf, uint32_t r,
+                                             uint32_t qsym = 0) {
+  return nom_decode(nom[r], ovf, qsym);
 }
 
 // LDS window slot of read r (the walk deals read r to wave r % kEW, lane
@@ -116,8 +118,8 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     // base of the steps' costs (chain_votes adds the walk's changes).
     const bool act = rraw_e(h) != kInactive;
     const uint16_t qc = act ? kNomQuietCode : (uint16_t)0;
-    Sh<uint16_t>* nm = E.L.cnom + r;
-    for (uint32_t j = 1; j <= K; ++j) nm[j * E.nmax] = qc;
+    Sh<uint16_t>* nm = E.L.cnom + r * (K + 1);  // read r's row: step j at nm[j]
+    for (uint32_t j = 1; j <= K; ++j) nm[j] = qc;
     if (act) c0 += cost_of(rraw_e(h), E.cfg.cost_mode);
   }
   c0 = wave_sum_u64(c0);
@@ -565,7 +567,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   // the step path takes it)
   const bool ffon = true;
 #endif
-  Sh<uint16_t>* nom_r = E.L.cnom + r;  // cnom[j * nmax + r]
+  Sh<uint16_t>* nom_r = E.L.cnom + r * (K + 1);  // read r's row: cnom[r * (K + 1) + j]
   uint32_t j = 1;                      // this lane's next step
   uint32_t jend = active ? K : 0u;     // its last step (lowered when it stops the chain)
   bool pend = false;                   // step j's push needs an edit-distance increase
@@ -586,7 +588,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
           stop = true;
         }
       }
-      nom_r[j * E.nmax] = (uint16_t)code;
+      nom_r[j] = (uint16_t)code;
       if (stop) {
         atomicMin(&ctl.chain_stop, j - 1);
         jend = j - 1;
@@ -771,56 +773,31 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
 // node cost (N_0's plus the walk's changes up to j), reads at their end, and
 // the votes for the predicted next symbol (P) and for all other non-wildcard
 // symbols (O) in exact 1/840ths, with the counts of multi-symbol reads and of
-// fractional votes for the prediction. Unless the wildcard is predicted, P and
-// O decide almost every step; the rest take the exact path (per-key f64 sums
-// in read order, hashbrown key order).
+// fractional votes for the prediction. Lane j of every wave sums step j over
+// the wave's share of the reads (a read's codes are one row: the lanes read
+// consecutive entries) and adds it to the step with two LDS atomics. Then
+// wave 0 decides the steps lane-parallel: unless the wildcard is predicted, P
+// and O decide almost every step; the rest take the exact path, the wave per
+// step (per-key f64 sums in read order, hashbrown key order).
 __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t Keff, uint32_t K) {
   const int lane = lane_id();
   const DevConfig& cfg = E.cfg;
-  if (wave_id() == 0) {
-    // step costs: the running sum of the per-step changes (Keff <= K < 64)
-    uint64_t d = ((uint32_t)lane >= 1 && (uint32_t)lane <= Keff) ? E.L.cstep[lane].cost : 0ull;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t t = __shfl_up(d, (unsigned)o, 64);
-      if (lane >= o) d += t;
-    }
-    if ((uint32_t)lane >= 1 && (uint32_t)lane <= Keff) E.L.cstep[lane].cost = E.L.cstep[0].cost + d;
-  }
   const uint32_t wsym = cfg.wildcard >= 0 ? (uint32_t)(uint8_t)cfg.wildcard : 0x100u;
-  for (uint32_t j = 1 + wave_id(); j <= Keff; j += kEW) {
-    SUB_T0(ta);
-    auto& st = E.L.cstep[j];
-    const uint32_t pred = j < K ? (uint32_t)E.L.cpred[j + 1] : 0x100u;
-    const Sh<uint16_t>* nom = E.L.cnom + j * E.nmax;
-    // one code per lane and 64-read block (n <= 256 with chains), all loaded
-    // under one wait; single-symbol votes are counted with ballots, the
-    // multi-symbol reads (rare) add their fractions lane-parallel
-    uint32_t cc[4];
-#pragma unroll
-    for (uint32_t b = 0; b < 4; ++b) {
-      const uint32_t r = 64u * b + (uint32_t)lane;
-      cc[b] = r < E.n ? (uint32_t)nom[r] : 0u;
-    }
-    uint32_t np = 0, no = 0, nend = 0, nmul = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; ++b) {
-      const uint32_t c = cc[b];
-      const uint32_t s0 = (c & kNomQuiet) ? pred : (c & kNomSymMask);
-      const bool one = (c & kNomOne) != 0;  // (codes with kNomOne or kNomOvf are active)
-      np += (uint32_t)__popcll((unsigned long long)ballot(one && s0 == pred));
-      no += (uint32_t)__popcll((unsigned long long)ballot(one && s0 != pred && s0 != wsym));
-      nend += (uint32_t)__popcll((unsigned long long)ballot((c & (kNomActive | kNomEnd)) == (kNomActive | kNomEnd)));
-      nmul += (uint32_t)__popcll((unsigned long long)ballot((c & kNomOvf) != 0));
-    }
-    uint64_t P = (uint64_t)kVoteDen * np, O = (uint64_t)kVoteDen * no;
-    uint32_t nfrac = 0;
-    if (nmul) {
-      uint32_t vp = 0, vo = 0, fr = 0;
-#pragma unroll
-      for (uint32_t b = 0; b < 4; ++b) {
-        const uint32_t c = cc[b];
-        if (!(c & kNomOvf)) continue;
+  const uint32_t jl = (uint32_t)lane;  // Keff <= K < 64: one step per lane
+  const bool lact = jl >= 1 && jl <= Keff;
+  const uint32_t pred = lact && jl < K ? (uint32_t)E.L.cpred[jl + 1] : 0x100u;
+  SUB_T0(ta);
+  if (Keff > 0 && (uint32_t)wave_id() < E.n) {
+    uint32_t np = 0, no = 0, nend = 0, nmul = 0, nfrac = 0, vpx = 0, vox = 0;
+    const Sh<uint16_t>* col = E.L.cnom + (lact ? jl : 0u);
+    for (uint32_t r = (uint32_t)wave_id(); r < E.n; r += kEW) {
+      const uint32_t c = lact ? (uint32_t)col[r * (K + 1)] : 0u;
+      if (c & kNomEnd) nend++;  // (kNomEnd only with kNomActive)
+      if (c & kNomOne) {
+        const uint32_t s0 = (c & kNomQuiet) ? pred : (c & kNomSymMask);
+        if (s0 == pred) np++;
+        else if (s0 != wsym) no++;
+      } else if (c & kNomOvf) {
         const ChainOvf q = E.L.covf[c & kNomSymMask];
         const uint32_t unit = vote_unit(q.split());
         bool frac = false;
@@ -828,61 +805,80 @@ __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t Keff, uint32_t
           const uint32_t w = unit * q.occ_at(k);
           const uint32_t sk = (uint32_t)((q.sym >> (8 * k)) & 0xFF);
           if (sk == pred) {
-            vp += w;
+            vpx += w;
             frac = true;
           } else if (sk != wsym) {
-            vo += w;
+            vox += w;
           }
         }
-        if (frac) fr++;
+        nmul++;
+        if (frac) nfrac++;
       }
-      P += wave_sum_u32(vp);
-      O += wave_sum_u32(vo);
-      nfrac = wave_sum_u32(fr);
     }
-    const uint64_t ef = (uint64_t)nend | (uint64_t)nmul << 16 | (uint64_t)nfrac << 32;
-    if (lane == 0) {
-      st.po = P | O << 32;
-      st.ef = ef;
+    if (lact) {
+      const uint64_t P = (uint64_t)kVoteDen * np + vpx, O = (uint64_t)kVoteDen * no + vox;
+      atomicAdd((unsigned long long*)&E.L.cstep[jl].po, (unsigned long long)(P | O << 32));
+      atomicAdd((unsigned long long*)&E.L.cstep[jl].ef,
+                (unsigned long long)((uint64_t)nend | (uint64_t)nmul << 16 | (uint64_t)nfrac << 32));
     }
-    if (j >= Keff) break;  // N_Keff: aggregates only (the commit's cost and end counts)
-    const uint32_t multi = step_nmulti(ef) ? 1u : 0u;
+  }
+  __syncthreads();
+  SUB_T1(20, ta);
+  if (wave_id() != 0) return;
+  SUB_T0(tb);
+  // step costs: the running sum of the per-step changes
+  {
+    uint64_t d = lact ? E.L.cstep[jl].cost : 0ull;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t t = __shfl_up(d, (unsigned)o, 64);
+      if (lane >= o) d += t;
+    }
+    if (lact) E.L.cstep[jl].cost = E.L.cstep[0].cost + d;
+  }
+  // Exact rational votes (P, O in 1/840ths); the f64 sums of the reference
+  // differ from them by far less than 1/840, so strict inequalities carry
+  // over. Only exact ties with fractional terms need the f64 path. With a
+  // wildcard (not predicted here), its votes are left out of O: any other key
+  // present drops it from the candidates (consensus.rs:556-561), and P > 0 is
+  // one.
+  int dec = 0;  // 1 ok, 0 not ok, -1 undecided
+  if (jl >= 1 && jl < Keff) {
+    const auto& st = E.L.cstep[jl];
+    const uint64_t P = st.po & 0xFFFFFFFFull, O = st.po >> 32;
     const uint64_t M = (uint64_t)kVoteDen * cfg.min_count;
-    // Exact rational votes (P, O in 1/840ths); the f64 sums of the reference
-    // differ from them by far less than 1/840, so strict inequalities carry
-    // over. Only exact ties with fractional terms need the f64 path.
-    int dec = -1;  // 1 ok, 0 not ok, -1 undecided
-    // With a wildcard (not predicted here), its votes are left out of O: any
-    // other key present drops it from the candidates (consensus.rs:556-561),
-    // and P > 0 is one.
-    if (cfg.wildcard < 0 || (uint32_t)E.L.cpred[j + 1] != (uint32_t)(uint8_t)cfg.wildcard) {
+    dec = -1;
+    if (cfg.wildcard < 0 || pred != (uint32_t)(uint8_t)cfg.wildcard) {
       if (P == 0) dec = 0;  // the prediction is not a candidate
       else if (O < P && O < M) {
         // thr = min(min_count, max) and max = P when P < M: the prediction
         // passes, every other key stays below the threshold
-        if (P != M || step_nfrac(ef) == 0) dec = 1;
+        if (P != M || step_nfrac(st.ef) == 0) dec = 1;
       }
     }
-    SUB_T1(20, ta);
-    SUB_T0(tb);
-    bool ok = dec == 1;
-    if (dec < 0) {
-      uint32_t m = 0, key = 0;
-      double val = 0.0;
-      ok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r, pred); }, [&](uint32_t) { return 1.0; },
-                           E.n, false, multi != 0, cfg.wildcard, m, key, val);
-      if (ok) {
-        const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
-        const double thr = fmin((double)cfg.min_count, max_obs);
-        const uint64_t pass = ballot((uint32_t)lane < m && val >= thr);
-        ok = __popcll((unsigned long long)pass) == 1 &&
-             (uint32_t)__builtin_amdgcn_readlane((int)key, __builtin_ctzll(pass)) == (uint32_t)E.L.cpred[j + 1];
-      }
-      SUB_CNT(25, 1);
-    }
-    SUB_T1(21, tb);
-    if (lane == 0) st.ok = ok ? 1u : 0u;
+    E.L.cstep[jl].ok = dec == 1 ? 1u : 0u;
   }
+  uint64_t und = ballot(dec < 0);
+  while (und) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(und);
+    und &= und - 1;
+    const uint32_t pj = (uint32_t)E.L.cpred[j + 1];
+    const uint32_t multi = step_nmulti(E.L.cstep[j].ef) ? 1u : 0u;
+    uint32_t m = 0, key = 0;
+    double val = 0.0;
+    bool ok = wave_votes_core([&](uint32_t r) { return nom_decode(E.L.cnom[r * (K + 1) + j], E.L.covf, pj); },
+                              [&](uint32_t) { return 1.0; }, E.n, false, multi != 0, cfg.wildcard, m, key, val);
+    if (ok) {
+      const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
+      const double thr = fmin((double)cfg.min_count, max_obs);
+      const uint64_t pass = ballot((uint32_t)lane < m && val >= thr);
+      ok = __popcll((unsigned long long)pass) == 1 &&
+           (uint32_t)__builtin_amdgcn_readlane((int)key, __builtin_ctzll(pass)) == pj;
+    }
+    SUB_CNT(25, 1);
+    if (lane == 0) E.L.cstep[j].ok = ok ? 1u : 0u;
+  }
+  SUB_T1(21, tb);
 }
 
 // (E) wave 0: replay the pops of N_1.. on the scalar search state
@@ -917,7 +913,22 @@ __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint3
   uint64_t thr = ctl.trk_thr[0], farthest = ctl.farthest[0], lcnst = ctl.last_constraint[0];
   uint64_t others = ctl.trk_total[0];
   SUB_T0(ta);
-  for (uint32_t j = 1; j < Keff && j < jbad; ++j) {
+  // Fast path, exact: with others + 1 <= max_queue_size the queue-size clause
+  // of the threshold loop is false at every step (others does not change
+  // while no threshold moves), and the constraint clause stays false while
+  // last_constraint + (j - 1) < max_nodes_wo_constraint; L0 + 1 >= thr keeps
+  // every L above the threshold. Then every step up to the first bad one
+  // passes with the tracker untouched but for the constraint count and
+  // farthest.
+  const uint32_t jlim = min(Keff, jbad);
+  const bool fast = jlim >= 2 && others + 1 <= cfg.max_queue_size &&
+                    lcnst + (uint64_t)(jlim - 2) < cfg.max_nodes_wo_constraint && (uint64_t)L0 + 1 >= thr;
+  if (fast) {
+    lcnst += jlim - 1;
+    farthest = max(farthest, (uint64_t)(L0 + jlim - 1));
+    jstar = jlim;
+  }
+  for (uint32_t j = 1; !fast && j < Keff && j < jbad; ++j) {
     const uint64_t L = L0 + j;
     uint64_t t_thr = thr, t_l = lcnst, t_oth = others;
     while ((t_oth + (L >= t_thr ? 1u : 0u) > cfg.max_queue_size || t_l >= cfg.max_nodes_wo_constraint) &&
@@ -1022,12 +1033,12 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
     for (uint32_t r = tid; r < E.n; r += kEB) {
       const RRaw t = rstate_load(&b.rs[r]);
       rstate_store(&E.L.hot[r], t);
-      RInfoReg x = nom_load(E.L.cnom + K * E.nmax, E.L.covf, r);
+      RInfoReg x = nom_decode(E.L.cnom[r * (K + 1) + K], E.L.covf, 0u);
       Nom o;
       o.n = x.n;
       o.split = x.split;
       o.sym = x.sym;
-      o.end = (E.L.cnom[K * E.nmax + r] & kNomEnd) ? 1u : 0u;
+      o.end = (E.L.cnom[r * (K + 1) + K] & kNomEnd) ? 1u : 0u;
       o.occ = (uint64_t)(x.occ.x & 0xFF) | (uint64_t)((x.occ.x >> 16) & 0xFF) << 8 |
               (uint64_t)(x.occ.y & 0xFF) << 16 | (uint64_t)((x.occ.y >> 16) & 0xFF) << 24 |
               (uint64_t)(x.occ.z & 0xFF) << 32 | (uint64_t)((x.occ.z >> 16) & 0xFF) << 40 |
