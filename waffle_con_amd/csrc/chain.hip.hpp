@@ -62,6 +62,14 @@ __device__ __forceinline__ RInfoReg nom_load(const Sh<uint16_t>* nom, const Sh<C
   return nom_decode(nom[r], ovf, qsym);
 }
 
+// 8 bytes of an LDS byte array from byte q (the array is dword aligned; bytes
+// the three dword loads touch past its end are never counted)
+__device__ __forceinline__ uint64_t lds_bytes8(const Sh<uint8_t>* a, uint32_t q) {
+  const Sh<uint32_t>* w32 = (const Sh<uint32_t>*)a + (q >> 2);
+  const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2], sh = q & 3u;
+  return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
+}
+
 // LDS window slot of read r (the walk deals read r to wave r % kEW, lane
 // r / kEW): the lanes of one wave read consecutive slots (engine_shared.hpp
 // kWinStride). kEW * ceil(n / kEW) <= 4 * win_m4(n) slots, so the carve of
@@ -200,6 +208,57 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
   // the predicted symbols extend the node's own consensus buffer in place
   // (positions >= L0 are not part of the node)
   if (tid >= 1 && (uint32_t)tid <= K) v.con[L0 + tid - 1] = E.L.cpred[tid];
+  // Deal the reads to the walk's positions (position p: wave p % kEW, lane
+  // p / kEW). A wave runs its reads' edit-distance increases one at a time
+  // and the walk ends with its slowest wave, so the reads whose every tip
+  // disagrees with the predictions within the chain (each costs its wave an
+  // increase) go first, spread evenly over the waves; the others follow. Any
+  // order gives the same results (reads are walked independently).
+  {
+    const uint32_t r = (uint32_t)tid;  // (n <= kEB with chains: one read per thread)
+    bool hv = false;
+    if (r < E.n) {
+      Front f;
+      front_load(rstate_load(&E.L.hot[r]), f);
+      if (f.e != kInactive) {
+        const uint32_t wb = E.L.cwb[r], blen = E.rlen(r);
+        const Sh<uint8_t>* win = E.L.cwin + (uint64_t)cwin_slot(r, E.n) * kWinStride;
+        bool any = false, lives = false;
+#pragma unroll
+        for (int k = 0; k < kF; ++k) {
+          if (!((f.mask >> k) & 1u)) continue;
+          const uint32_t bo = f.fd[k] + f.e - f.fi[k], q = bo - wb;
+          if (f.fd[k] + f.off != L0 || bo >= blen || q >= 64u) continue;
+          any = true;
+          const uint32_t lim = min(K, min(blen - bo, 64u - q));
+          uint32_t c = 0;
+          while (c < lim) {
+            const uint64_t mm = nz_bytes(lds_bytes8(win, q + c) ^ lds_bytes8(E.L.cpred, 1 + c));
+            if (mm) {
+              c += (uint32_t)__builtin_ctzll(mm) >> 3;
+              break;
+            }
+            c += 8;
+          }
+          lives |= c >= lim;
+        }
+        hv = any && !lives;
+      }
+    }
+    const uint64_t hm = ballot(hv);
+    if (lane == 0) ctl.deal_cnt[wave_id()] = (uint32_t)__popcll((unsigned long long)hm);
+    __syncthreads();
+    uint32_t hb = 0, H = 0;
+    for (uint32_t w = 0; w < (uint32_t)kEW; ++w) {
+      const uint32_t c = ctl.deal_cnt[w];
+      if (w < (uint32_t)wave_id()) hb += c;
+      H += c;
+    }
+    if (r < E.n) {
+      const uint32_t hr = hb + (uint32_t)__popcll((unsigned long long)(hm & ((1ull << lane) - 1ull)));
+      E.L.cperm[hv ? hr : H + r - hr] = (uint8_t)r;
+    }
+  }
   SUB_T1(24, tb);
 }
 
@@ -356,13 +415,6 @@ __device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, 
   return ok ? e_out : kInactive;
 }
 
-// 8 bytes of an LDS byte array from byte q (the array is dword aligned; bytes
-// the three dword loads touch past its end are never counted)
-__device__ __forceinline__ uint64_t lds_bytes8(const Sh<uint8_t>* a, uint32_t q) {
-  const Sh<uint32_t>* w32 = (const Sh<uint32_t>*)a + (q >> 2);
-  const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2], sh = q & 3u;
-  return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
-}
 
 // The quiet run of one read from step j: the number m (<= lim) of consecutive
 // pushes N_j, N_j+1, ... under which every live tip extends (its read bytes
@@ -400,7 +452,7 @@ __device__ __forceinline__ uint32_t lane_run(const Front& f, const Win& W, const
 // once, one per 16-lane group (group_edinc, the dual engine's path: the same
 // arithmetic as wave_heavy's register path; a row that outgrows a group's
 // registers goes on in wave_edinc_mem). ls[q] (q < ng) are the lanes whose
-// frontiers wait in gtmp[q]; their reads are ls[q] * kEW + wave, their steps
+// frontiers wait in gtmp[q]; their reads are perm[ls[q] * kEW + wave], their steps
 // j of those lanes. kFirst: the first rewrite of a row in the chain leaves a
 // copy in slot S (the rows are otherwise only touched at frontier diagonals,
 // which a rollback restores from the node's LDS RStates), and each step's
@@ -411,21 +463,32 @@ struct GHOut {
   uint32_t fail;
 };
 template <bool kFirst>
-__device__ __noinline__ GHOut chain_group_heavy(Sh<RState>* gtmp0, Gm<uint32_t>* nwf, Gm<uint32_t>* swf,
-                                                const Gm<uint8_t>* rbytes, const Sh<uint2>* rt, const Gm<uint8_t>* con,
-                                                uint32_t L0, uint32_t j, uint32_t ls0, uint32_t ls1, uint32_t ls2,
-                                                uint32_t ls3, uint32_t ng, uint32_t wave, uint32_t wcap, int wc,
-                                                bool early, int cost_mode, Lo<Ctl>& ctl, Sh<ChainStep>* cstep,
-                                                Sh<uint32_t>* list, uint32_t list_n, uint64_t bak) {
+__device__ __noinline__ GHOut chain_group_heavy(Lo<Ctl>& ctl, uint32_t j, uint32_t ls0, uint32_t ls1, uint32_t ls2,
+                                                uint32_t ls3, uint32_t ng, uint64_t bak) {
   const int lane = lane_id();
+  const uint32_t wave = (uint32_t)wave_id();
+  // the chain's uniform arguments (run_chain_impl stores them)
+  Sh<RState>* gtmp0 = ctl.gh_tmp + 4 * wave;
+  Gm<uint32_t>* nwf = ctl.gh_nwf;
+  Gm<uint32_t>* swf = ctl.gh_swf;
+  const Gm<uint8_t>* rbytes = ctl.gh_rbytes;
+  const Sh<uint2>* rt = ctl.gh_rt;
+  const Gm<uint8_t>* con = ctl.gh_con;
+  const uint32_t L0 = uni(ctl.gh_L0), wcap = uni(ctl.gh_wcap), list_n = uni(ctl.gh_list_n);
+  (void)list_n;  // (bounds of the checked build's WC_IX)
+  const uint32_t flags = uni(ctl.gh_flags);
+  const bool early = (flags & 1u) != 0;
+  const int cost_mode = (int)(flags >> 1);
+  const int wc = uni(ctl.gh_wc);
+  Sh<ChainStep>* cstep = ctl.gh_cstep;
+  Sh<uint32_t>* list = ctl.gh_list;
   const uint32_t g = (uint32_t)lane >> 4, gl = (uint32_t)lane & 15u;
   const uint32_t ls[4] = {uni(ls0), uni(ls1), uni(ls2), uni(ls3)};
   ng = uni(ng);
-  wave = uni(wave);
   const uint32_t lsel = g == 0 ? ls[0] : g == 1 ? ls[1] : g == 2 ? ls[2] : ls[3];
   const bool gact = g < ng;
   Sh<RState>* gtmp = gtmp0 + g;
-  const uint32_t rl = lsel * kEW + wave;
+  const uint32_t rl = ctl.gh_perm[lsel * kEW + wave];
   const uint32_t jl = (uint32_t)__shfl((int)j, (int)lsel, 64);
   const uint32_t e_in = gact ? gtmp->e : 0u;
   Gm<uint32_t>* gwf = nwf + (uint64_t)rl * wcap;
@@ -456,7 +519,7 @@ __device__ __noinline__ GHOut chain_group_heavy(Sh<RState>* gtmp0, Gm<uint32_t>*
   while (mem) {
     const uint32_t q = (uint32_t)__builtin_ctzll(mem) >> 4;
     mem &= mem - 1;
-    const uint32_t rq = ls[q] * kEW + wave;
+    const uint32_t rq = ctl.gh_perm[ls[q] * kEW + wave];
     const uint32_t jq = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)ls[q]);
     const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)e_out, (int)(16 * q));
     WaveCounters cnt = {0, 0, 0, 0, 0, 0};
@@ -528,8 +591,9 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
   const bool early = cfg.early != 0;
   const int wc = cfg.wildcard;
   SideView v = E.sv(top, 0);
-  const uint32_t r = (uint32_t)lane * kEW + (uint32_t)wave;
-  const bool has = r < E.n;
+  const uint32_t pos = (uint32_t)lane * kEW + (uint32_t)wave;
+  const bool has = pos < E.n;
+  const uint32_t r = has ? (uint32_t)E.L.cperm[pos] : pos;  // (chain_prepare's deal)
   Front f;
   f.e = kInactive;
   f.off = f.maxb = f.nscmp = f.mask = 0;
@@ -657,14 +721,14 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
 // register needs make the walk spill, which cost more than the overlap saves
 // under load (cfg2 batch 32.7 vs 27.6 ms; one locus alone 19.1 vs 19.9 ms in
 // the 2-wave build): one read at a time there.
-#if !defined(WC_LOWLAT) || defined(WC_SEQ_HEAVY)
+#if (!defined(WC_LOWLAT) && !defined(WC_GROUP_HEAVY)) || defined(WC_SEQ_HEAVY)
     while (hm) {  // edit-distance increases: the wave works on one read at a time
       const int l = __builtin_ctzll(hm);
       hm &= hm - 1;
       const uint32_t jl = (uint32_t)__builtin_amdgcn_readlane((int)j, l);
       if (lane == l) front_store(&E.L.ctmp[4 * wave], f);
       wave_lds_sync();
-      const uint32_t rl = (uint32_t)l * kEW + (uint32_t)wave;
+      const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, l);
       const uint32_t e_in = uni(E.L.ctmp[4 * wave].e);
       Gm<uint32_t>* bdst = nullptr;
       if (kFirst && !((bak >> l) & 1ull)) {
@@ -720,10 +784,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
       const uint32_t myg = (uint32_t)lane == ls[0] ? 0u : (uint32_t)lane == ls[1] ? 1u : (uint32_t)lane == ls[2] ? 2u : 3u;
       if (mine) front_store(&E.L.ctmp[4 * wave + myg], f);
       wave_lds_sync();
-      const GHOut gh = chain_group_heavy<kFirst>(E.L.ctmp + 4 * wave, v.wf, E.sv(S, 0).wf, E.rbytes, E.L.rt, v.con, L0, j,
-                                                 ls[0], ls[1], ls[2], ls[3], ng, (uint32_t)wave, E.wcap, wc, early,
-                                                 cfg.cost_mode, ctl, E.L.cstep, E.L.list,
-                                                 (uint32_t)list_entries(E.sides, E.nmax), bak);
+      const GHOut gh = chain_group_heavy<kFirst>(ctl, j, ls[0], ls[1], ls[2], ls[3], ng, bak);
       bak = gh.bak;
       if (mine) {
         const RRaw t = rstate_load(&E.L.ctmp[4 * wave + myg]);
@@ -978,7 +1039,7 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
     // length adapts, so a chain that ends early wastes few speculative steps)
     const uint32_t K = min(kDual ? min(E.chain, ctl.chain_kcur) : E.chain, E.lcap - L0);
     ctl.chain_k = 0;
-    if (K >= 2 && ctl.nfree > 0) {
+    if (K >= 2 && ctl.nfree > 0 && E.n <= (uint32_t)kEB) {  // (the walk deals one read per thread)
       ctl.chain_k = K;
       ctl.chain_slot = E.L.freestack[WC_IX(--ctl.nfree, E.pcap)];
       ctl.chain_stop = K;
@@ -993,6 +1054,22 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
   const uint32_t K = uni(ctl.chain_k);
   if (K == 0) return 0;
   const uint32_t S = uni(ctl.chain_slot);
+  if (tid == 0) {  // chain_group_heavy's arguments (read after chain_prepare's barriers)
+    ctl.gh_nwf = E.sv(top, 0).wf;
+    ctl.gh_swf = E.sv(S, 0).wf;
+    ctl.gh_rbytes = E.rbytes;
+    ctl.gh_con = E.sv(top, 0).con;
+    ctl.gh_rt = E.L.rt;
+    ctl.gh_tmp = E.L.ctmp;
+    ctl.gh_cstep = E.L.cstep;
+    ctl.gh_list = E.L.list;
+    ctl.gh_perm = E.L.cperm;
+    ctl.gh_L0 = L0;
+    ctl.gh_wcap = E.wcap;
+    ctl.gh_list_n = (uint32_t)list_entries(E.sides, E.nmax);
+    ctl.gh_flags = (E.cfg.early ? 1u : 0u) | (uint32_t)E.cfg.cost_mode << 1;
+    ctl.gh_wc = E.cfg.wildcard;
+  }
   for (uint32_t i = tid; i < (K + 1) * (uint32_t)(sizeof(ChainStep) / 4); i += kEB)
     ((Sh<uint32_t>*)E.L.cstep)[i] = 0;
   chain_prepare(E, ctl, top, L0, K, S);

@@ -115,6 +115,20 @@ struct Ctl {
   uint32_t chain_k, chain_slot, chain_stop, chain_novf, chain_nochain, chain_len, chain_nbak;
   uint32_t chain_kcur;  // dual engine: the next chain's length (doubles after a fully accepted chain)
   uint64_t chain_tot[5];  // updates, w_out, compares, ed increases, row bytes of one chain pass
+  uint32_t deal_cnt[kWaves];  // chain_prepare: reads per wave expected to need an ED increase
+  // the chain walk's grouped ED increases (chain_group_heavy): the chain's
+  // uniform arguments, in LDS rather than in call registers
+  Gm<uint32_t>* gh_nwf;  // the node's wavefront rows
+  Gm<uint32_t>* gh_swf;  // slot S's rows (first-rewrite copies)
+  const Gm<uint8_t>* gh_rbytes;
+  const Gm<uint8_t>* gh_con;
+  Sh<uint2>* gh_rt;
+  Sh<RState>* gh_tmp;
+  Sh<ChainStep>* gh_cstep;
+  Sh<uint32_t>* gh_list;
+  Sh<uint8_t>* gh_perm;  // the walk's read order
+  uint32_t gh_L0, gh_wcap, gh_list_n, gh_flags;  // flags: early | cost_mode << 1
+  int32_t gh_wc;
   uint32_t nkeys[2];
   uint8_t keys[2][kKout];
   double vals[2][kKout];
@@ -184,6 +198,7 @@ struct Lds {
   Sh<uint32_t>* cwb;     // [nmax]
   Sh<uint32_t>* cpc;     // [K+1]
   Sh<uint8_t>* cpred;    // [K+2]
+  Sh<uint8_t>* cperm;    // [nmax] the chain walk's read at position p (wave p % kEW, lane p / kEW)
   Sh<HeapEntry>* heap;
   Sh<uint32_t>* freestack;
   Sh<SlotMeta>* meta;
@@ -208,6 +223,7 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
   l.cwb = nullptr;
   l.cpc = nullptr;
   l.cpred = nullptr;
+  l.cperm = nullptr;
   if (K) {
     // (engine_shared chain_lds_bytes; side s of a per-side array at s * its
     // one-side size, the dual chain's steps are DualSteps)
@@ -227,6 +243,8 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
     p += align16((uint64_t)(K + 1) * 4);
     l.cpred = p;
     p += align16(S * (K + 2));
+    l.cperm = p;
+    p += align16(nmax);
   }
   l.heap = (Sh<HeapEntry>*)p;
   p += (uint64_t)pcap * sizeof(HeapEntry);

@@ -271,7 +271,7 @@ inline uint32_t env_chain_kinds() {
 }
 // chain LDS (per side S = chain_sides: the dual engine's chains walk both):
 //   steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves][4] | nom[S][K+1][nmax] u16 |
-//   win[S][4*m4][68 B] (read windows) | wb[S][nmax] u32 | pc[K+1] u32 | pred[S][K+2] u8
+//   win[S][4*m4][68 B] (read windows) | wb[S][nmax] u32 | pc[K+1] u32 | pred[S][K+2] u8 | perm[nmax] u8
 __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K, uint32_t sides = 1) {
   if (K == 0) return 0;
   const uint64_t S = chain_sides(sides);
@@ -283,6 +283,7 @@ __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K, u
   t += align16(S * nmax * 4);
   t += align16((uint64_t)(K + 1) * 4);
   t += align16(S * (K + 2));
+  t += align16(nmax);  // the walk's read order
   return t;
 }
 
