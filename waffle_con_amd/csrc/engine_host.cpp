@@ -648,16 +648,22 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
                         std::vector<EngineOut>& outs) {
   L.caps = caps;
   L.grid = std::min<uint32_t>((uint32_t)std::max(1, caps.per_cu) * (uint32_t)ctx->n_cu, std::max(1u, caps.conc));
-  // the ring (pinned host memory) holds the published, unfinished problems:
-  // at most a grid and a quarter of them (the backlog below) and their read
-  // tables. Sized for that, not for the largest batch: a call per locus from
-  // many threads (per-thread contexts) would otherwise pin 160 MB each.
+  // the ring (pinned host memory) holds the published problems and their
+  // read tables, from the oldest unfinished one to the newest: at most a grid
+  // and a quarter of them are unfinished at once (the backlog below), but a
+  // long sub-problem keeps its entry while the sub-problems published after
+  // it come and go, so the span grows with the call's work. Sized for the
+  // call (16 sub-problems per problem it was given, up to 65,536 entries and
+  // 8M read-table slots): a 10,000-locus cfg5 call with a ring of 4,096
+  // entries stalled publication behind its slowest sub-problems (49 vs 30 s),
+  // while one locus per call from many threads keeps a small ring each.
   auto pow2 = [](uint64_t x) {
     uint64_t p = 1;
     while (p < x) p <<= 1;
     return p;
   };
-  const uint32_t kQcap = (uint32_t)std::min<uint64_t>(1u << 16, std::max<uint64_t>(1024, pow2(2ull * L.grid + 64)));
+  const uint32_t kQcap = (uint32_t)std::min<uint64_t>(
+      1u << 16, std::max<uint64_t>({1024, pow2(2ull * L.grid + 64), pow2(16ull * items.size())}));
   const uint32_t kQslots =
       (uint32_t)std::min<uint64_t>(1u << 23, std::max<uint64_t>(1u << 16, pow2((uint64_t)kQcap * caps.nmax)));
   L.P = 2 * L.grid;  // two output slots per workgroup
