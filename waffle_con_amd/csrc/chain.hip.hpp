@@ -223,12 +223,16 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
       if (f.e != kInactive) {
         const uint32_t wb = E.L.cwb[r], blen = E.rlen(r);
         const Sh<uint8_t>* win = E.L.cwin + (uint64_t)cwin_slot(r, E.n) * kWinStride;
-        bool any = false, lives = false;
+        bool any = false, lives = false, fail = false;
+        uint32_t m0 = K;
 #pragma unroll
         for (int k = 0; k < kF; ++k) {
           if (!((f.mask >> k) & 1u)) continue;
           const uint32_t bo = f.fd[k] + f.e - f.fi[k], q = bo - wb;
-          if (f.fd[k] + f.off != L0 || bo >= blen || q >= 64u) continue;
+          if (f.fd[k] + f.off != L0 || bo >= blen || q >= 64u) {
+            fail = true;
+            continue;
+          }
           any = true;
           const uint32_t lim = min(K, min(blen - bo, 64u - q));
           uint32_t c = 0;
@@ -241,8 +245,12 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
             c += 8;
           }
           lives |= c >= lim;
+          m0 = min(m0, min(c, lim));
         }
         hv = any && !lives;
+        // the walk's first quiet run (lane_run at step 1, which returns 0 when
+        // a live tip is not at the end)
+        E.L.cm0[r] = (uint8_t)(fail || !any ? 0u : m0);
       }
     }
     const uint64_t hm = ballot(hv);
@@ -492,8 +500,9 @@ __device__ __noinline__ GHOut chain_group_heavy(Lo<Ctl>& ctl, uint32_t j, uint32
   const uint32_t jl = (uint32_t)__shfl((int)j, (int)lsel, 64);
   const uint32_t e_in = gact ? gtmp->e : 0u;
   Gm<uint32_t>* gwf = nwf + (uint64_t)rl * wcap;
-  const Gm<uint8_t>* rd = rbytes + (uint64_t)rt[rl].x * 16;
-  const uint32_t blen = rt[rl].y;
+  // (the read table: the LDS copy, or the HBM tables in the dual engine)
+  const Gm<uint8_t>* rd = rt ? rbytes + (uint64_t)rt[rl].x * 16 : rbytes + ctl.gh_roff[ctl.gh_rbegin + rl];
+  const uint32_t blen = rt ? rt[rl].y : ctl.gh_rlenp[ctl.gh_rbegin + rl];
   if (kFirst) {
     const bool first = gact && !((bak >> lsel) & 1ull);
     if (first) {
@@ -524,8 +533,10 @@ __device__ __noinline__ GHOut chain_group_heavy(Lo<Ctl>& ctl, uint32_t j, uint32
     const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)e_out, (int)(16 * q));
     WaveCounters cnt = {0, 0, 0, 0, 0, 0};
     uint32_t eo = 0;
-    const bool okq = wave_edinc_mem(gtmp0 + q, nwf + (uint64_t)rq * wcap, eq, rbytes + (uint64_t)rt[rq].x * 16,
-                                    rt[rq].y, con, L0 + jq, wc, early, wcap, cnt, eo);
+    const Gm<uint8_t>* rdq = rt ? rbytes + (uint64_t)rt[rq].x * 16 : rbytes + ctl.gh_roff[ctl.gh_rbegin + rq];
+    const uint32_t blq = rt ? rt[rq].y : ctl.gh_rlenp[ctl.gh_rbegin + rq];
+    const bool okq = wave_edinc_mem(gtmp0 + q, nwf + (uint64_t)rq * wcap, eq, rdq, blq, con, L0 + jq, wc, early,
+                                    wcap, cnt, eo);
     if (lane == 0) {
       t_ed += (uint32_t)cnt.edinc;
       t_up += (uint32_t)cnt.updates;
@@ -607,6 +618,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     blen = E.rlen(r);
   }
   const bool active = has && f.e != kInactive;
+  const uint32_t m0 = active ? (uint32_t)E.L.cm0[r] : 0u;  // the first quiet run (chain_prepare)
   Gm<uint32_t>* wf_row = v.wf + (uint64_t)r * E.wcap;
   uint32_t t_upd = 0, t_wout = 0, t_cmp = 0;
   uint64_t bak = 0;  // lanes whose row was backed up (wave-uniform)
@@ -677,7 +689,13 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
       // ---- this read's quiet run from step j ----
       if (ffon && j < K && f.mask != 0 && f.maxb != blen) {
         uint32_t nlive;
-        const uint32_t m = lane_run(f, W, pred, blen, L0 + j - 1, j, K - j + 1, kb, nlive);
+        uint32_t m;
+        if (j == 1) {  // chain_prepare computed it (cm0)
+          m = min(m0, K);
+          nlive = (uint32_t)__popc(f.mask);
+        } else {
+          m = lane_run(f, W, pred, blen, L0 + j - 1, j, K - j + 1, kb, nlive);
+        }
         // the run's last push nominates the byte after the run: the step path takes it
         const uint32_t Q = m >= 1 ? min(m - 1, lim - j) : 0u;
         if (Q > 0) {
@@ -1060,6 +1078,9 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
     ctl.gh_rbytes = E.rbytes;
     ctl.gh_con = E.sv(top, 0).con;
     ctl.gh_rt = E.L.rt;
+    ctl.gh_roff = E.roff;
+    ctl.gh_rlenp = E.rlenp;
+    ctl.gh_rbegin = E.P.read_begin;
     ctl.gh_tmp = E.L.ctmp;
     ctl.gh_cstep = E.L.cstep;
     ctl.gh_list = E.L.list;

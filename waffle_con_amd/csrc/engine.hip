@@ -122,7 +122,10 @@ struct Ctl {
   Gm<uint32_t>* gh_swf;  // slot S's rows (first-rewrite copies)
   const Gm<uint8_t>* gh_rbytes;
   const Gm<uint8_t>* gh_con;
-  Sh<uint2>* gh_rt;
+  Sh<uint2>* gh_rt;  // (null in the dual engine: the HBM tables below)
+  const Gm<uint64_t>* gh_roff;
+  const Gm<uint32_t>* gh_rlenp;
+  uint32_t gh_rbegin;
   Sh<RState>* gh_tmp;
   Sh<ChainStep>* gh_cstep;
   Sh<uint32_t>* gh_list;
@@ -199,6 +202,7 @@ struct Lds {
   Sh<uint32_t>* cpc;     // [K+1]
   Sh<uint8_t>* cpred;    // [K+2]
   Sh<uint8_t>* cperm;    // [nmax] the chain walk's read at position p (wave p % kEW, lane p / kEW)
+  Sh<uint8_t>* cm0;      // [nmax] each read's first quiet run (chain_prepare)
   Sh<HeapEntry>* heap;
   Sh<uint32_t>* freestack;
   Sh<SlotMeta>* meta;
@@ -224,6 +228,7 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
   l.cpc = nullptr;
   l.cpred = nullptr;
   l.cperm = nullptr;
+  l.cm0 = nullptr;
   if (K) {
     // (engine_shared chain_lds_bytes; side s of a per-side array at s * its
     // one-side size, the dual chain's steps are DualSteps)
@@ -245,6 +250,8 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
     p += align16(S * (K + 2));
     l.cperm = p;
     p += align16(nmax);
+    l.cm0 = p;
+    p += align16(nmax);
   }
   l.heap = (Sh<HeapEntry>*)p;
   p += (uint64_t)pcap * sizeof(HeapEntry);
@@ -260,7 +267,9 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
   p += align16((uint64_t)list_entries(sides, nmax) * 4);
   l.ce = sides == 2 ? (Sh<uint16_t>*)p : nullptr;
   if (sides == 2) p += align16((uint64_t)kDualChildBatch * 2 * nmax * 2);
-  l.rt = (Sh<uint2>*)p;
+  // the single engine's read table (the dual engine reads the HBM tables: at
+  // 200 reads the 1.6 KB cost cfg3 its third workgroup per CU)
+  l.rt = sides == 1 ? (Sh<uint2>*)p : nullptr;
   return l;
 }
 
@@ -469,8 +478,12 @@ struct Eng {
   // a read's bytes and length from the LDS read table (init_problem fills it
   // from the HBM tables: one dependent HBM round trip less wherever a phase
   // loads read bytes)
-  __device__ const Gm<uint8_t>* read(uint32_t r) const { return rbytes + (uint64_t)L.rt[WC_IX(r, nmax)].x * 16; }
-  __device__ uint32_t rlen(uint32_t r) const { return L.rt[WC_IX(r, nmax)].y; }
+  __device__ const Gm<uint8_t>* read(uint32_t r) const {
+    return L.rt ? rbytes + (uint64_t)L.rt[WC_IX(r, nmax)].x * 16 : rbytes + roff[P.read_begin + WC_IX(r, nmax)];
+  }
+  __device__ uint32_t rlen(uint32_t r) const {
+    return L.rt ? L.rt[WC_IX(r, nmax)].y : rlenp[P.read_begin + WC_IX(r, nmax)];
+  }
   __device__ __forceinline__ TrackerRef tracker(Lo<Ctl>& ctl, int k) const {
     const uint64_t L2 = lcap + 2;
     return TrackerRef{trk + 2 * k * L2, trk + (2 * k + 1) * L2, &ctl.trk_total[k], &ctl.trk_thr[k],
@@ -743,7 +756,7 @@ __device__ inline void init_problem(Eng& E, Lo<Ctl>& ctl) {
   for (uint32_t i = tid; i < E.pcap; i += kEB) E.L.freestack[i] = E.pcap - 1 - i;
   for (uint32_t i = tid; i < 4 * (E.lcap + 2); i += kEB) E.trk[i] = 0;
   // the read table in LDS (reads start 16-byte aligned in every arena)
-  for (uint32_t r = tid; r < E.n; r += kEB)
+  for (uint32_t r = tid; E.L.rt && r < E.n; r += kEB)
     E.L.rt[r] = make_uint2((uint32_t)(E.roff[E.P.read_begin + r] >> 4), E.rlenp[E.P.read_begin + r]);
   __syncthreads();
   SideView v = E.sv(0, 0);

@@ -271,7 +271,7 @@ inline uint32_t env_chain_kinds() {
 }
 // chain LDS (per side S = chain_sides: the dual engine's chains walk both):
 //   steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves][4] | nom[S][K+1][nmax] u16 |
-//   win[S][4*m4][68 B] (read windows) | wb[S][nmax] u32 | pc[K+1] u32 | pred[S][K+2] u8 | perm[nmax] u8
+//   win[S][4*m4][68 B] (read windows) | wb[S][nmax] u32 | pc[K+1] u32 | pred[S][K+2] u8 | perm[nmax] u8 | m0[nmax] u8
 __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K, uint32_t sides = 1) {
   if (K == 0) return 0;
   const uint64_t S = chain_sides(sides);
@@ -284,6 +284,7 @@ __host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K, u
   t += align16((uint64_t)(K + 1) * 4);
   t += align16(S * (K + 2));
   t += align16(nmax);  // the walk's read order
+  t += align16(nmax);  // each read's first quiet run
   return t;
 }
 
@@ -317,8 +318,8 @@ __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uin
   t += align16((uint64_t)list_entries(sides, nmax) * 4);
   // dual engine: the children's edit distances per (child, side, read) of one build pass (prune + cost), u16
   if (sides == 2) t += align16((uint64_t)kDualChildBatch * 2 * nmax * 2);
-  // the claimed problem's read table (offset / 16, length) per read
-  t += align16((uint64_t)nmax * 8);
+  // the single engine's read table of the claimed problem (offset / 16, length) per read
+  if (sides == 1) t += align16((uint64_t)nmax * 8);
   return align16(t);
 }
 
