@@ -166,12 +166,12 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     for (uint32_t u = 0; u < kPer; ++u) {
       const uint32_t t = 1 + wave + kEW * u;
       const uint32_t q = bo_tip + t - wb;
-      xs[u] = (bo_tip != kInactive && t < K && bo_tip + t < blen && q < 64u) ? (uint32_t)win[q] : 0x100u;
+      xs[u] = (bo_tip != kInactive && t <= K && bo_tip + t < blen && q < 64u) ? (uint32_t)win[q] : 0x100u;
     }
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u) {
       const uint32_t t = 1 + wave + kEW * u;
-      if (t >= K) break;
+      if (t > K) break;  // (t = K predicts N_K's child: chain_votes decides N_K too)
       const uint32_t x = xs[u];
       // plurality of x over the wave (ties: the first-seen symbol); a
       // first-seen symbol held by a strict majority is the plurality
@@ -198,10 +198,13 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
         rem &= ~mm;
       }
       if (best == 0x100u) {
-        if (lane == 0) atomicMin(&ctl.chain_stop, t);  // nothing to predict N_{t+1} from
+        if (lane == 0 && t < K) atomicMin(&ctl.chain_stop, t);  // nothing to predict N_{t+1} from
         break;
       }
-      if (lane == 0) E.L.cpred[t + 1] = (uint8_t)best;
+      if (lane == 0) {
+        E.L.cpred[t + 1] = (uint8_t)best;
+        if (t == K) ctl.chain_pk = 1;
+      }
     }
   }
   __syncthreads();
@@ -864,7 +867,10 @@ __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t Keff, uint32_t
   const uint32_t wsym = cfg.wildcard >= 0 ? (uint32_t)(uint8_t)cfg.wildcard : 0x100u;
   const uint32_t jl = (uint32_t)lane;  // Keff <= K < 64: one step per lane
   const bool lact = jl >= 1 && jl <= Keff;
-  const uint32_t pred = lact && jl < K ? (uint32_t)E.L.cpred[jl + 1] : 0x100u;
+  // N_K's next symbol is predicted too (chain_prepare, chain_pk): a full chain
+  // decides N_K's votes, and its pop can be replayed like the others
+  const bool pk = Keff == K && uni(ctl.chain_pk) != 0;
+  const uint32_t pred = lact && (jl < K || pk) ? (uint32_t)E.L.cpred[jl + 1] : 0x100u;
   SUB_T0(ta);
   if (Keff > 0 && (uint32_t)wave_id() < E.n) {
     uint32_t np = 0, no = 0, nend = 0, nmul = 0, nfrac = 0, vpx = 0, vox = 0;
@@ -922,7 +928,7 @@ __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t Keff, uint32_t
   // present drops it from the candidates (consensus.rs:556-561), and P > 0 is
   // one.
   int dec = 0;  // 1 ok, 0 not ok, -1 undecided
-  if (jl >= 1 && jl < Keff) {
+  if (jl >= 1 && (jl < Keff || (pk && jl == K))) {
     const auto& st = E.L.cstep[jl];
     const uint64_t P = st.po & 0xFFFFFFFFull, O = st.po >> 32;
     const uint64_t M = (uint64_t)kVoteDen * cfg.min_count;
@@ -1053,6 +1059,7 @@ template <bool kDual>
 __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
   const int tid = threadIdx.x;
   if (tid == 0) {
+    ctl.chain_pk = 0;
     // (the dual engine's chains end at forks of its search more often: their
     // length adapts, so a chain that ends early wastes few speculative steps)
     const uint32_t K = min(kDual ? min(E.chain, ctl.chain_kcur) : E.chain, E.lcap - L0);
@@ -1070,6 +1077,9 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
   }
   __syncthreads();
   const uint32_t K = uni(ctl.chain_k);
+  // (reset only here: every wave has read the previous chain's chain_next in
+  // the kernel's loop condition before it reached the barrier above)
+  if (tid == 0) ctl.chain_next = 0;
   if (K == 0) return 0;
   const uint32_t S = uni(ctl.chain_slot);
   if (tid == 0) {  // chain_group_heavy's arguments (read after chain_prepare's barriers)
@@ -1108,11 +1118,17 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
   chain_votes(E, ctl, Keff, K);
   __syncthreads();
   PH_MARK(10);
+  // A full chain whose N_K has exactly one passing candidate (its predicted
+  // child) replays N_K's pop too, and its child starts the next chain at
+  // once (single engine; the kernel falls back to pushing that child when
+  // the next chain does not start): no literal pop between the chains.
+  // Only where the next chain can start (room for two more steps).
+  const bool ext = !kDual && Keff == K && uni(ctl.chain_pk) != 0 && L0 + K + 2 <= E.lcap;
   if (wave_id() == 0) {
-    const uint32_t js = chain_accept(E, ctl, L0, Keff);
+    const uint32_t js = chain_accept(E, ctl, L0, ext ? K + 1 : Keff);
     if (tid == 0) {
       ctl.chain_len = js;
-      if (js == K && Keff == K) {  // the speculative pass is the committed work
+      if (js >= K && Keff == K) {  // the speculative pass is the committed work
         ctl.cnt[S_UPDATES] += ctl.chain_tot[0];
         ctl.cnt[S_WOUT] += ctl.chain_tot[1];
         ctl.cnt[S_COMPARES] += ctl.chain_tot[2];
@@ -1125,8 +1141,9 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
   __syncthreads();
   PH_MARK(11);
   const uint32_t jstar = uni(ctl.chain_len);
+  const bool full = jstar >= K && Keff == K;  // (jstar = K + 1: N_K popped too)
   SideView v = E.sv(top, 0), b = E.sv(S, 0);
-  if (jstar == K && Keff == K) {
+  if (full) {
     // every step accepted: the speculative final state is the node
     for (uint32_t r = tid; r < E.n; r += kEB) {
       const RRaw t = rstate_load(&b.rs[r]);
@@ -1171,7 +1188,7 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
   }
   __syncthreads();
   if (tid == 0) {
-    if (!(jstar == K && Keff == K)) {  // the replay pass is the committed work
+    if (!full) {  // the replay pass is the committed work
       ctl.cnt[S_UPDATES] += ctl.chain_tot[0];
       ctl.cnt[S_WOUT] += ctl.chain_tot[1];
       ctl.cnt[S_COMPARES] += ctl.chain_tot[2];
@@ -1179,10 +1196,10 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
       ctl.cnt[S_ROWB] += ctl.chain_tot[4];
     }
 #ifdef WC_PHASE_PROF
-    ctl.ph[15] += 1ull + ((jstar == K && Keff == K) ? (1ull << 20) : 0ull) + ((uint64_t)jstar << 40);
+    ctl.ph[15] += 1ull + (full ? (1ull << 20) : 0ull) + ((uint64_t)min(jstar, K) << 40);
 #endif
     E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = S;
-    if (kDual) ctl.chain_kcur = (jstar == K && Keff == K) ? min(2 * K, E.chain) : max(4u, jstar + 1);
+    if (kDual) ctl.chain_kcur = full ? min(2 * K, E.chain) : max(4u, jstar + 1);
     // the queue as the literal pops leave it: each N_j (j < j*) was pushed,
     // then popped as the maximum, which moves the other entries along its
     // path (their tie order depends on the layout)
@@ -1209,7 +1226,14 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
         }
       }
     }
-    if (jstar > 0) {
+    if (jstar == K + 1) {
+      // N_K was popped (virtually, like N_1..N_K-1): its one child, the
+      // predicted symbol, is the kernel's next chain (or, if that chain does
+      // not start, its literal push); nothing is queued
+      E.L.meta[top].len[0] = L0 + K;
+      ctl.chain_next = 1;
+      ctl.chain_sym = E.L.cpred[K + 1];
+    } else if (jstar > 0) {
       const auto& st = E.L.cstep[jstar];
       const uint32_t clen = L0 + jstar;
       E.L.meta[top].len[0] = clen;

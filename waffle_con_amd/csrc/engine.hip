@@ -114,6 +114,9 @@ struct Ctl {
   // linear-chain run-ahead (run_chain)
   uint32_t chain_k, chain_slot, chain_stop, chain_novf, chain_nochain, chain_len, chain_nbak;
   uint32_t chain_kcur;  // dual engine: the next chain's length (doubles after a fully accepted chain)
+  uint32_t chain_pk;    // chain_prepare predicted N_K's next symbol (cpred[K + 1])
+  uint32_t chain_next;  // the chain ended with N_K popped virtually: its one child (chain_sym) starts the next
+  uint32_t chain_sym;
   uint64_t chain_tot[5];  // updates, w_out, compares, ed increases, row bytes of one chain pass
   uint32_t deal_cnt[kWaves];  // chain_prepare: reads per wave expected to need an ED increase
   // the chain walk's grouped ED increases (chain_group_heavy): the chain's
@@ -2056,10 +2059,23 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
       }
       // ---- one child and nothing else queued: linear-chain run-ahead ----
       // (past the last activation point every read of this lineage is active)
+      uint32_t plen = len;  // the expanded node's length (a chain that popped its last node moves it)
       if (nc == 1 && A.chain && uni(ctl.heap_n) == 0 && (E.P.n_active == E.n || len >= E.P.max_act)) {
-        const uint32_t jstar =
-            run_chain_single(E, ctl, top, len, uni((int32_t)ctl.ch_s[0][0]));
+        uint32_t jstar = run_chain_single(E, ctl, top, plen, uni((int32_t)ctl.ch_s[0][0]));
         PH_MARK(14);
+        // a full chain that also popped its last node N_K (one child, no
+        // queue): that child starts the next chain at once
+        while (jstar && uni(ctl.chain_next)) {
+          plen += jstar - 1;
+          const int s1 = uni((int32_t)ctl.chain_sym);
+          jstar = run_chain_single(E, ctl, top, plen, s1);
+          PH_MARK(14);
+          if (!jstar) {
+            // the next chain did not start: N_K's one child is pushed literally below
+            if (tid == 0) ctl.ch_s[0][0] = (int16_t)s1;
+            __syncthreads();
+          }
+        }
         if (jstar) continue;
       }
       // ---- push every child: clones first, the last child in place ----
@@ -2078,18 +2094,18 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
         __syncthreads();
         if (uni(ctl.status) != ST_OK) break;
         const uint32_t slot = uni(ctl.cur_slot);
-        if (slot != top) copy_side<true>(E, top, 0, slot, 0, len);
-        if (tid == 0) E.sv(slot, 0).con[len] = (uint8_t)ctl.ch_s[c][0];
+        if (slot != top) copy_side<true>(E, top, 0, slot, 0, plen);
+        if (tid == 0) E.sv(slot, 0).con[plen] = (uint8_t)ctl.ch_s[c][0];
         __syncthreads();
         PH_MARK(4);
         // clones read the parent from LDS and write their own slot; the last
         // child is pushed in place on the LDS copy
         const int sym = uni((int32_t)ctl.ch_s[c][0]);
-        if (slot != top) push_sides<true, false>(E, ctl, slot, sym, -1, len + 1, 0, true, E.L.rinfo);
-        else push_sides<true, true>(E, ctl, slot, sym, -1, len + 1, 0, true, E.L.rinfo);
+        if (slot != top) push_sides<true, false>(E, ctl, slot, sym, -1, plen + 1, 0, true, E.L.rinfo);
+        else push_sides<true, true>(E, ctl, slot, sym, -1, plen + 1, 0, true, E.L.rinfo);
         // reads whose offset activates at this length (consensus.rs:327-335)
-        if (len + 1 <= E.P.max_act) {
-          single_activate(E, ctl, slot, slot == top, len + 1);
+        if (plen + 1 <= E.P.max_act) {
+          single_activate(E, ctl, slot, slot == top, plen + 1);
         }
         if (tid == 0) {
           if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;
@@ -2097,7 +2113,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
           else if (ctl.ovf) ctl.status = limit_status(ctl.ovf);
           ctl.ch_cost[c] = ctl.cost_acc;
           ctl.ch_slot[c] = slot;
-          E.L.meta[slot].len[0] = len + 1;
+          E.L.meta[slot].len[0] = plen + 1;
         }
         __syncthreads();
         if (uni(ctl.status) != ST_OK) break;
@@ -2106,8 +2122,8 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
       if (tid == 0) {
         TrackerRef t = E.tracker(ctl, 0);
         for (uint32_t c = 0; c < nc; ++c) {
-          t.insert(len + 1);
-          heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{ctl.ch_cost[c], len + 1, ctl.ch_slot[c]});
+          t.insert(plen + 1);
+          heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{ctl.ch_cost[c], plen + 1, ctl.ch_slot[c]});
         }
         // the last child's nominations are in LDS: reuse them if it is popped next
         ctl.cache_slot = ctl.ch_slot[nc - 1];
