@@ -113,17 +113,27 @@ def _single_results(res, n, cost, L, return_errors):
     cnt = as_np(cnt_p, shape=(max(n, 1),)).tolist()
     pack = (seq, idx, sc, owner)
     out, k = [], 0
-    mk = Consensus._packed
+    new = object.__new__
+    ok = _lib.WC_OK
+    # (Consensus._packed inlined: one object per result, its arenas viewed in place)
     for p in range(n):
-        if st[p] != _lib.WC_OK:
+        c_p = cnt[p]
+        if st[p] != ok:
             e = _lib.WaffleConError(L.wc_results_error(res, p).decode(), st[p])
             if not return_errors:
                 raise e
             out.append(e)
-            k += cnt[p]
+            k += c_p
             continue
-        out.append([mk(pack, j, cost) for j in range(k, k + cnt[p])])
-        k += cnt[p]
+        row = []
+        for j in range(k, k + c_p):
+            c = new(Consensus)
+            c._sequence = c._scores = None
+            c._consensus_cost = cost
+            c._src = (pack, j)
+            row.append(c)
+        out.append(row)
+        k += c_p
     return out
 
 
