@@ -238,15 +238,19 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
           }
           any = true;
           const uint32_t lim = min(K, min(blen - bo, 64u - q));
-          uint32_t c = 0;
-          while (c < lim) {
-            const uint64_t mm = nz_bytes(lds_bytes8(win, q + c) ^ lds_bytes8(E.L.cpred, 1 + c));
-            if (mm) {
-              c += (uint32_t)__builtin_ctzll(mm) >> 3;
-              break;
-            }
-            c += 8;
-          }
+          // the first mismatch within K <= 40 bases: five 8-byte compares,
+          // all loaded under one wait (bytes past the window or the
+          // predictions are read but never counted: c is clamped to lim)
+          static_assert(kChainMax <= 40, "five 8-byte chunks cover a chain");
+          uint64_t mmv[5];
+#pragma unroll
+          for (uint32_t u = 0; u < 5; ++u)
+            mmv[u] = nz_bytes(lds_bytes8(win, q + 8 * u) ^ lds_bytes8(E.L.cpred, 1 + 8 * u));
+          uint32_t c = 40;
+#pragma unroll
+          for (int u = 4; u >= 0; --u)
+            if (mmv[u]) c = 8 * (uint32_t)u + ((uint32_t)__builtin_ctzll(mmv[u]) >> 3);
+          c = min(c, lim);
           lives |= c >= lim;
           m0 = min(m0, min(c, lim));
         }
@@ -875,15 +879,30 @@ __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t Keff, uint32_t
   if (Keff > 0 && (uint32_t)wave_id() < E.n) {
     uint32_t np = 0, no = 0, nend = 0, nmul = 0, nfrac = 0, vpx = 0, vox = 0;
     const Sh<uint16_t>* col = E.L.cnom + (lact ? jl : 0u);
-    for (uint32_t r = (uint32_t)wave_id(); r < E.n; r += kEW) {
-      const uint32_t c = lact ? (uint32_t)col[r * (K + 1)] : 0u;
-      if (c & kNomEnd) nend++;  // (kNomEnd only with kNomActive)
-      if (c & kNomOne) {
+    // eight reads' codes per batch, loaded under one wait
+    for (uint32_t r0 = (uint32_t)wave_id(); r0 < E.n; r0 += 8u * kEW) {
+      uint32_t cc[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const uint32_t r = r0 + u * kEW;
+        cc[u] = lact && r < E.n ? (uint32_t)col[r * (K + 1)] : 0u;
+      }
+      uint32_t ovfm = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const uint32_t c = cc[u];
+        if (c & kNomEnd) nend++;  // (kNomEnd only with kNomActive)
         const uint32_t s0 = (c & kNomQuiet) ? pred : (c & kNomSymMask);
-        if (s0 == pred) np++;
-        else if (s0 != wsym) no++;
-      } else if (c & kNomOvf) {
-        const ChainOvf q = E.L.covf[c & kNomSymMask];
+        if (c & kNomOne) {
+          if (s0 == pred) np++;
+          else if (s0 != wsym) no++;
+        }
+        if (c & kNomOvf) ovfm |= 1u << u;
+      }
+      while (ovfm) {  // multi-symbol reads (rare): their fractions
+        const uint32_t u = (uint32_t)__builtin_ctz(ovfm);
+        ovfm &= ovfm - 1;
+        const ChainOvf q = E.L.covf[cc[u] & kNomSymMask];
         const uint32_t unit = vote_unit(q.split());
         bool frac = false;
         for (uint32_t k = 0; k < q.n(); ++k) {
