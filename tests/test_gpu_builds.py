@@ -2,7 +2,10 @@
 build at 4 waves/SIMD (WC_NARROW=0 WC_LOWLAT=0), the same at 2 waves/SIMD
 (engine_lowlat.hip, the default for launches of at most 2 problems per CU),
 the 128-thread build (engine_narrow.hip; WC_NARROW bit 0 = single engine,
-bit 1 = dual engine, default 2) and the global-state build (WC_GSTATE), and each dual build with dual_hot forced on. The build is
+bit 1 = dual engine, default 2), the global-state build (WC_GSTATE), the
+1024-thread single engine (engine_cu.hip, the default for batch launches of
+at most one problem per CU; WC_CU=1 forces it, WC_CU=0 keeps it off in the
+other variants) and each dual build with dual_hot forced on. The build is
 picked per launch from the environment (engine_host.cpp plan_caps), so one
 process exercises all of them. Sequences, scores and every work counter must
 equal the oracle's."""
@@ -20,7 +23,7 @@ KEYS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "no
         "peak_queue_size", "row_bytes")
 BUILDS = {"wide": {"WC_NARROW": "0", "WC_LOWLAT": "0"}, "lowlat": {"WC_NARROW": "0"},
           "narrow-single": {"WC_NARROW": "1"}, "narrow-dual": {"WC_NARROW": "2"}, "narrow": {"WC_NARROW": "3"},
-          "gstate": {"WC_GSTATE": "1"},
+          "gstate": {"WC_GSTATE": "1"}, "cu": {"WC_CU": "1"},
           # the dual engine with the popped node's RStates in LDS (dual_hot: an
           # opt-in knob, measured not to pay; forced here in every dual build)
           "wide-hot": {"WC_NARROW": "0", "WC_LOWLAT": "0", "WC_DUAL_HOT": "2"},
@@ -29,9 +32,10 @@ BUILDS = {"wide": {"WC_NARROW": "0", "WC_LOWLAT": "0"}, "lowlat": {"WC_NARROW": 
 
 @pytest.fixture(params=sorted(BUILDS))
 def build(request):
-    old = {k: os.environ.get(k) for k in ("WC_NARROW", "WC_GSTATE", "WC_LOWLAT", "WC_DUAL_HOT")}
+    old = {k: os.environ.get(k) for k in ("WC_NARROW", "WC_GSTATE", "WC_LOWLAT", "WC_DUAL_HOT", "WC_CU")}
     for k in old:
         os.environ.pop(k, None)
+    os.environ["WC_CU"] = "0"
     os.environ.update(BUILDS[request.param])
     yield request.param
     for k, v in old.items():

@@ -72,8 +72,7 @@ __device__ __forceinline__ uint64_t lds_bytes8(const Sh<uint8_t>* a, uint32_t q)
 
 // LDS window slot of read r (the walk deals read r to wave r % kEW, lane
 // r / kEW): the lanes of one wave read consecutive slots (engine_shared.hpp
-// kWinStride). kEW * ceil(n / kEW) <= 4 * win_m4(n) slots, so the carve of
-// win_m4 fits every build's wave count.
+// kWinStride). kEW * ceil(n / kEW) <= win_slots(nmax, kEW), the carve.
 __device__ __forceinline__ uint32_t cwin_slot(uint32_t r, uint32_t n) {
   return (r % (uint32_t)kEW) * ((n + kEW - 1) / (uint32_t)kEW) + r / (uint32_t)kEW;
 }
@@ -208,6 +207,7 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     }
   }
   __syncthreads();
+  SUB_T1(44, tb);
   // the predicted symbols extend the node's own consensus buffer in place
   // (positions >= L0 are not part of the node)
   if (tid >= 1 && (uint32_t)tid <= K) v.con[L0 + tid - 1] = E.L.cpred[tid];
@@ -426,6 +426,9 @@ __device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, 
     atomicAdd((unsigned long long*)&tot[2], (unsigned long long)cnt.compares);
     atomicAdd((unsigned long long*)&tot[3], (unsigned long long)cnt.edinc);
     atomicAdd((unsigned long long*)&tot[4], (unsigned long long)cnt.rowb);
+#ifdef WC_PHASE_PROF
+    for (int k = 0; k < 3; ++k) atomicAdd((unsigned long long*)&tot[5 + k], (unsigned long long)cnt.tq[k]);
+#endif
   }
   return ok ? e_out : kInactive;
 }
@@ -740,6 +743,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     uint64_t hm = ballot(pend);
     if (!hm) break;
     SUB_CNT(19, __popcll(hm));
+    SUB_WADD(46, __popcll(hm));
     SUB_T0(tb);
 // The 2-waves-per-SIMD build (WC_LOWLAT, 256 VGPRs) runs the edit-distance
 // increases of up to four reads at once (chain_group_heavy); in the 4-wave build the call's
@@ -851,6 +855,7 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
     atomicAdd((unsigned long long*)&ctl.chain_tot[2], (unsigned long long)s_cmp);
   }
   SUB_T1(18, tw);
+  SUB_WADD(45, __builtin_amdgcn_s_memtime() - tw);
 }
 
 // (D) Step aggregates, then per chain node N_j, j < Keff: ok[j] = exactly one
@@ -1077,6 +1082,7 @@ __device__ inline uint32_t chain_accept(Eng& E, Lo<Ctl>& ctl, uint32_t L0, uint3
 template <bool kDual>
 __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
   const int tid = threadIdx.x;
+  SUB_T0(te);
   if (tid == 0) {
     ctl.chain_pk = 0;
     // (the dual engine's chains end at forks of its search more often: their
@@ -1090,7 +1096,7 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
       ctl.chain_novf = 0;
       ctl.chain_nochain = 0;
       ctl.chain_nbak = 0;
-      for (int k = 0; k < 5; ++k) ctl.chain_tot[k] = 0;
+      for (int k = 0; k < (int)(sizeof(ctl.chain_tot) / 8); ++k) ctl.chain_tot[k] = 0;
       E.L.cpred[1] = (uint8_t)s1;
     }
   }
@@ -1122,6 +1128,7 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
   }
   for (uint32_t i = tid; i < (K + 1) * (uint32_t)(sizeof(ChainStep) / 4); i += kEB)
     ((Sh<uint32_t>*)E.L.cstep)[i] = 0;
+  SUB_T1(43, te);
   chain_prepare(E, ctl, top, L0, K, S);
   __syncthreads();
   PH_MARK(8);
@@ -1216,6 +1223,10 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
     }
 #ifdef WC_PHASE_PROF
     ctl.ph[15] += 1ull + (full ? (1ull << 20) : 0ull) + ((uint64_t)min(jstar, K) << 40);
+    for (int k = 0; k < 3; ++k) {  // wave_heavy's timers over every wave (both passes)
+      ctl.ph[48 + k] += ctl.chain_tot[5 + k];
+      ctl.chain_tot[5 + k] = 0;
+    }
 #endif
     E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = S;
     if (kDual) ctl.chain_kcur = full ? min(2 * K, E.chain) : max(4u, jstar + 1);

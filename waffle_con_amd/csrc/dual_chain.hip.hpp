@@ -48,7 +48,7 @@ __device__ __forceinline__ DualChainArea dual_area(const Eng& E) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     a.nom[s] = E.L.cnom + (uint64_t)s * (K + 1) * E.nmax;
-    a.win[s] = E.L.cwin + (uint64_t)s * 4 * win_m4(E.nmax) * kWinStride;
+    a.win[s] = E.L.cwin + (uint64_t)s * win_slots(E.nmax, chain_waves(kEW)) * kWinStride;
     a.wb[s] = E.L.cwb + (uint64_t)s * E.nmax;
     a.pred[s] = E.L.cpred + (uint64_t)s * (K + 2);
   }

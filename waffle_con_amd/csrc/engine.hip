@@ -117,8 +117,12 @@ struct Ctl {
   uint32_t chain_pk;    // chain_prepare predicted N_K's next symbol (cpred[K + 1])
   uint32_t chain_next;  // the chain ended with N_K popped virtually: its one child (chain_sym) starts the next
   uint32_t chain_sym;
+#ifdef WC_PHASE_PROF
+  uint64_t chain_tot[8];  // (+ wave_heavy's timers, WaveCounters::tq)
+#else
   uint64_t chain_tot[5];  // updates, w_out, compares, ed increases, row bytes of one chain pass
-  uint32_t deal_cnt[kWaves];  // chain_prepare: reads per wave expected to need an ED increase
+#endif
+  uint32_t deal_cnt[kEW];  // chain_prepare: reads per wave expected to need an ED increase
   // the chain walk's grouped ED increases (chain_group_heavy): the chain's
   // uniform arguments, in LDS rather than in call registers
   Gm<uint32_t>* gh_nwf;  // the node's wavefront rows
@@ -179,6 +183,11 @@ struct Ctl {
   do {                                    \
     if (threadIdx.x == 0) ctl.ph[(k)] += (n); \
   } while (0)
+// every wave's lane 0 adds a count to k (sums over the waves)
+#define SUB_WADD(k, n)                                                                    \
+  do {                                                                                    \
+    if (lane_id() == 0) atomicAdd((unsigned long long*)&ctl.ph[(k)], (unsigned long long)(n)); \
+  } while (0)
 #else
 #define PH_MARK(k) \
   do {             \
@@ -191,6 +200,9 @@ struct Ctl {
   } while (0)
 #define SUB_CNT(k, n) \
   do {                \
+  } while (0)
+#define SUB_WADD(k, n) \
+  do {                 \
   } while (0)
 #endif
 
@@ -240,11 +252,11 @@ __device__ inline Lds carve(Sh<uint8_t>* smem, uint32_t sides, uint32_t pcap, ui
     l.covf = (Sh<ChainOvf>*)p;
     p += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
     l.ctmp = (Sh<RState>*)p;
-    p += (uint64_t)kWaves * 4 * 64;
+    p += (uint64_t)chain_waves(kEW) * 4 * 64;
     l.cnom = (Sh<uint16_t>*)p;
     p += align16(S * (K + 1) * nmax * 2);
     l.cwin = p;
-    p += align16(S * 4 * win_m4(nmax) * kWinStride);
+    p += align16(S * win_slots(nmax, chain_waves(kEW)) * kWinStride);
     l.cwb = (Sh<uint32_t>*)p;
     p += align16(S * nmax * 4);
     l.cpc = (Sh<uint32_t>*)p;
@@ -498,9 +510,11 @@ struct Eng {
 // workgroup-uniform, so each 32-bit word goes through readfirstlane.
 __device__ inline Eng eng_uniform(const Eng& s) {
   static_assert(sizeof(Eng) % 4 == 0, "Eng is copied as words");
-  // words through memcpy (no type-punned access to the pointer fields)
-  uint32_t w[sizeof(Eng) / 4];
-  __builtin_memcpy(w, &s, sizeof(Eng));
+  // words through memcpy (no type-punned access to the pointer fields); the
+  // context is the same in every lane, so lane 0 alone reads it (a context in
+  // scratch is per lane: 64 lanes' reads of it per chain call)
+  uint32_t w[sizeof(Eng) / 4] = {};
+  if (lane_id() == 0) __builtin_memcpy(w, &s, sizeof(Eng));
 #pragma unroll
   for (int i = 0; i < (int)(sizeof(Eng) / 4); ++i) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[i]);
   Eng d;
@@ -2511,6 +2525,7 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
   stream_exit(A);
 }
 
+#ifndef WC_SINGLE_ONLY  // (engine_cu.hip: the single engine only)
 // two kernels, one per dual_hot: in one kernel the two paths' register
 // allocations merge (the 4-wave build spilled 236 VGPRs instead of 84)
 __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
@@ -2525,8 +2540,9 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
   dual_main<true>(A, smem, *(Lo<Ctl>*)&ctl_lds);
 }
 #endif
+#endif  // WC_SINGLE_ONLY
 
-#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT)
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT) && !defined(WC_CU)
 // =====================================================================
 // standalone DWFALite jobs (dynamic_wfa.rs:48-265): one wave per job
 // =====================================================================
@@ -2586,6 +2602,9 @@ __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
 void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(single_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
+// waves per workgroup of this build (the host sizes the per-wave layouts)
+int engine_waves() { return kEW; }
+#ifndef WC_SINGLE_ONLY
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_DUAL_CHAIN_CALL)
   if (a.dual_hot) {
@@ -2595,17 +2614,20 @@ void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStrea
 #endif
   hipLaunchKernelGGL(dual_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
+#endif
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot) {
   int nb = 0;
   hipError_t e = hipSuccess;
   if (sides == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kEB, lds);
+#ifndef WC_SINGLE_ONLY
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_DUAL_CHAIN_CALL)
   else if (dual_hot) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_hot_engine_kernel, kEB, lds);
 #endif
   else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kEB, lds);
+#endif
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
-#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT)
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT) && !defined(WC_CU)
 void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s) {
   hipLaunchKernelGGL(dwfa_jobs_kernel, dim3(n), dim3(64), 0, s, jobs);
 }

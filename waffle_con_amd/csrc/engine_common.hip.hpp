@@ -22,8 +22,9 @@
 namespace WC_ENGINE_NS {
 using namespace ::wc;
 
-// threads per engine workgroup of this build (engine_narrow.hip: 128); the
-// LDS/HBM layouts (engine_shared.hpp) are sized for kBlock = 256, the widest
+// threads per engine workgroup of this build (engine_narrow.hip: 128,
+// engine_cu.hip: 1024); problems have at most kBlock = 256 reads, and the
+// LDS/HBM layouts' per-wave parts are sized for the build (engine_shared.hpp)
 #ifndef WC_BLOCK
 #define WC_BLOCK 256
 #endif
@@ -33,7 +34,7 @@ constexpr int kEW = kEB / 64;
 // 256-thread build (128 VGPRs) spills more with the extra control flow than it
 // saves (cfg3 -6%), the 128-thread build has the registers (cfg5 +4%)
 constexpr bool kSlotBound = kEB <= 128;
-static_assert(kEB % 64 == 0 && kEB <= kBlock, "engine workgroup size");
+static_assert(kEB % 64 == 0 && kEB <= 64 * kMaxWaves, "engine workgroup size");
 
 // Explicit address spaces: HBM (global) and LDS pointers compile to global_* /
 // ds_* instructions instead of flat_* (which wait on both counters and take
@@ -251,6 +252,9 @@ __device__ __forceinline__ uint32_t rraw_flags(const RRaw& s) { return s.a.w >> 
 struct WaveCounters {
   uint32_t updates, w_out, compares, edinc, finalizes;
   uint32_t rowb;  // wavefront-row bytes read + written by updates (finalizes: read) that grow e
+#ifdef WC_PHASE_PROF
+  uint64_t tq[3];  // wave_heavy's register path: row load, increase loop, store + rebuild (cycles)
+#endif
 };
 
 // ---- packed match runs (dynamic_wfa.rs:122-150) ----
@@ -940,7 +944,14 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
   const uint32_t w_in = W;
   uint32_t v[kRegQ];
   bool regs = W + 2 <= 64u * kRegQ;
+#ifdef WC_PHASE_PROF
+  const uint64_t t_a = __builtin_amdgcn_s_memtime();
+#endif
   if (regs) regs_load(v, wf, W);
+#ifdef WC_PHASE_PROF
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint64_t t_b = __builtin_amdgcn_s_memtime();
+#endif
   if (bak) regs_store(v, bak, W);
   do {
     if (W + 2 > wcap) return false;
@@ -962,6 +973,9 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
     }
     cnt.edinc++;
   } while (mo + off < olen && !(early && mb == blen));
+#ifdef WC_PHASE_PROF
+  const uint64_t t_c = __builtin_amdgcn_s_memtime();
+#endif
   cnt.updates++;
   cnt.w_out += W;
   cnt.rowb += 4 * (w_in + W);
@@ -973,6 +987,12 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
     __builtin_amdgcn_wave_barrier();
     wave_rebuild(wf, e, off, blen, olen, rsp);
   }
+#ifdef WC_PHASE_PROF
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  cnt.tq[0] += t_b - t_a;
+  cnt.tq[1] += t_c - t_b;
+  cnt.tq[2] += __builtin_amdgcn_s_memtime() - t_c;
+#endif
   e_out = e;
   return true;
 }

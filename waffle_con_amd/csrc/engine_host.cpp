@@ -80,7 +80,7 @@ uint64_t hbm_share(const wc_ctx* ctx, uint64_t cached, double frac) {
 // the same occupancy. Retry outcomes raise them per item (log2 multipliers).
 int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vector<SubProb>& items,
                      const std::vector<uint32_t>& ids, uint64_t hbm_budget, Caps& c, std::string& err,
-                     uint32_t max_per_cu) {
+                     uint32_t max_per_cu, bool cu_ok) {
   uint32_t nmax = 1, maxlen = 1, wx = 0, px = 0, lx = 0, rx = 0;
   bool any_act = false;
   for (uint32_t id : ids) {
@@ -167,8 +167,19 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   const char* lenv = getenv("WC_LOWLAT");
   c.lowlat = !gstate && !c.narrow && ids.size() <= 2ull * (uint64_t)ctx->n_cu && !(lenv && atoi(lenv) == 0);
   if (sides == 2 && chain > 0 && !gstate) c.narrow = c.lowlat = false;  // the chain build (wcd)
+  // a batch launch of at most one problem per CU runs the 1024-thread single
+  // engine (engine_cu.hip): one workgroup of 16 waves per problem, so a
+  // chain walk's reads and their edit-distance increases spread over 16 waves
+  // instead of 4. WC_CU=0 disables it, WC_CU=1 forces it (test hook)
+  const char* wenv = getenv("WC_CU");
+  const int wmode = wenv ? atoi(wenv) : 2;
+  c.cu = cu_ok && sides == 1 && !gstate && chain > 0 && wmode != 0 &&
+           (wmode == 1 || ids.size() <= (uint64_t)ctx->n_cu);
+  if (c.cu) c.narrow = c.lowlat = false;
+  c.waves = c.cu ? (uint32_t)std::max(wcu::engine_waves(), kWaves) : (uint32_t)kWaves;
   c.dual_hot = false;
   auto occupancy = [&](size_t l) {
+    if (c.cu) return wcu::engine_blocks_per_cu(sides, l);
     if (sides == 2 && chain > 0 && !gstate) return wcd::engine_blocks_per_cu(sides, l);
     return c.narrow ? wcn::engine_blocks_per_cu(sides, l, c.dual_hot)
                     : (c.lowlat ? wcl::engine_blocks_per_cu(sides, l, c.dual_hot)
@@ -197,9 +208,9 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   // literal pop between chains); take the longest one whose LDS still gives
   // the workgroups per CU of the default length (results do not depend on it)
   if (sides == 1 && !chain_env && chain > 0 && !gstate) {
-    const int occ = occupancy((size_t)lds_bytes(sides, pcap, nmax, chain));
+    const int occ = occupancy((size_t)lds_bytes(sides, pcap, nmax, chain, 0, c.waves));
     for (uint32_t k = chain + 1; k <= kChainMax; ++k) {
-      const uint64_t l = lds_bytes(sides, pcap, nmax, k);
+      const uint64_t l = lds_bytes(sides, pcap, nmax, k, 0, c.waves);
       if (l > 60 * 1024 || occupancy((size_t)l) < occ) break;
       chain = k;
     }
@@ -231,7 +242,7 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   }
   c.conc = (uint32_t)conc;
   c.gstate = gstate;
-  c.gsb = align16(lds_bytes(sides, pcap, nmax, chain, c.dual_hot));
+  c.gsb = align16(lds_bytes(sides, pcap, nmax, chain, c.dual_hot, c.waves));
   c.lds = gstate ? 0 : (size_t)c.gsb;
   c.per_cu = gstate ? wcg::engine_blocks_per_cu(sides, 0) : occupancy(c.lds);
   c.wsb = ws_bytes(sides, pcap, nmax, c.wcap, c.lcap);
@@ -327,6 +338,8 @@ int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
     else wcg::launch_dual_engine(a, L.grid, 0, L.stream);
   } else if (caps.sides == 2 && caps.chain > 0) {
     wcd::launch_dual_engine(a, L.grid, caps.lds, L.stream);
+  } else if (caps.cu) {
+    wcu::launch_single_engine(a, L.grid, caps.lds, L.stream);
   } else if (caps.narrow) {
     if (caps.sides == 1) wcn::launch_single_engine(a, L.grid, caps.lds, L.stream);
     else wcn::launch_dual_engine(a, L.grid, caps.lds, L.stream);
@@ -394,7 +407,7 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   const uint64_t hbytes = L.off_out + (uint64_t)P * caps.ob;
   if (!L.host.ensure(hbytes, true)) return set_err(ctx, WC_E_HIP, "pinned host allocation failed (results)");
   memset(L.host.p, 0, L.off_out);  // done flags, status, counters
-  if (caps.act_m && !L.act.ensure(act_scr_u64(caps.act_m) * 8 * L.grid))
+  if (caps.act_m && !L.act.ensure(act_scr_u64(caps.act_m, caps.waves) * 8 * L.grid))
     return set_err(ctx, WC_E_HIP, "device allocation failed (activation scratch)");
   if (!L.probs.ensure(P * sizeof(DevProblem)) || !L.sroff.ensure(L.h_sroff.size() * 8) ||
       !L.srlen.ensure(L.h_srlen.size() * 4) || !L.ract.ensure(L.h_ract.size() * 8) ||
@@ -438,7 +451,7 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   a.work_counter = (uint32_t*)L.counter.p;
   a.act_m = caps.act_m;
   a.act_scr = caps.act_m ? (uint64_t*)L.act.p : nullptr;
-  a.act_stride = caps.act_m ? act_scr_u64(caps.act_m) : 0;
+  a.act_stride = caps.act_m ? act_scr_u64(caps.act_m, caps.waves) : 0;
   // debug phase cycle counters (WC_PHASES=<file>, WC_PHASE_PROF builds only)
   if (getenv("WC_PHASES") && L.phases.ensure(kPhases * 8)) {
     a.phases = (unsigned long long*)L.phases.p;
@@ -448,8 +461,8 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d dual_hot=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
-            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, (int)caps.dual_hot, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
+    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d cu=%d dual_hot=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
+            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, (int)caps.cu, (int)caps.dual_hot, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
   return WC_OK;
 }
 
@@ -574,7 +587,7 @@ int run_engine(wc_ctx* ctx, wc_batch* b, const wc_config& cfg, uint32_t sides, s
     if (run.empty()) run.swap(later);
     Caps caps;
     std::string err;
-    int rc = plan_caps(ctx, cfg, sides, items, run, hbm_share(ctx, L->ws.cap, 0.5), caps, err);
+    int rc = plan_caps(ctx, cfg, sides, items, run, hbm_share(ctx, L->ws.cap, 0.5), caps, err, 4, true);
     if (rc != WC_OK) {
       for (uint32_t id : run) {
         out[id].status = rc;
@@ -690,7 +703,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   int64_t* qract = (int64_t*)(rh + off_ract);
   uint32_t* qrlen = (uint32_t*)(rh + off_rlen);
   const uint64_t wsb = caps.wsb + rtab_bytes(caps.nmax) + kGuard;
-  if (caps.act_m && !L.act.ensure(act_scr_u64(caps.act_m) * 8 * L.grid))
+  if (caps.act_m && !L.act.ensure(act_scr_u64(caps.act_m, caps.waves) * 8 * L.grid))
     return set_err(ctx, WC_E_HIP, "device allocation failed (activation scratch)");
   if (!L.ws.ensure(wsb * L.grid + 64) || !L.counter.ensure(4))
     return set_err(ctx, WC_E_HIP, "device allocation failed (workspace)");
@@ -728,7 +741,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.done = (uint32_t*)dh;
   a.act_m = caps.act_m;
   a.act_scr = caps.act_m ? (uint64_t*)L.act.p : nullptr;
-  a.act_stride = caps.act_m ? act_scr_u64(caps.act_m) : 0;
+  a.act_stride = caps.act_m ? act_scr_u64(caps.act_m, caps.waves) : 0;
   a.stream = 1;
   a.qcap = kQcap;
   a.qslots = kQslots;

@@ -8,6 +8,9 @@ namespace wc {
 
 constexpr int kBlock = 256;       // threads per engine workgroup (4 waves)
 constexpr int kWaves = kBlock / 64;
+// the widest single-engine build (engine_cu.hip: 1024 threads for launches of
+// at most one problem per CU); problems still have at most kBlock reads
+constexpr int kMaxWaves = 16;
 constexpr int kKmax = 8;          // distinct symbols at one read's tips
 constexpr int kKout = 14;         // distinct symbols voted across a node side (16-bucket table)
 constexpr uint32_t kInactive = 0xFFFFFFFFu;  // Option<DWFALite>::None
@@ -143,9 +146,9 @@ __host__ __device__ inline uint64_t rtab_bytes(uint32_t nmax) {
 // staging stride of one read pulled from host memory (EngineArgs::hreads): its
 // bytes rounded up to 16, then 64 zero bytes (the engine's over-read margin)
 __host__ __device__ inline uint64_t rstage_stride(uint32_t maxlen) { return ((uint64_t)maxlen + 15) / 16 * 16 + 64; }
-constexpr int kPhases = 48;  // 32..39: chain statistics of the dual engine (engine.hip, dual chain call site); 40..: single-engine chain counters
+constexpr int kPhases = 56;  // 32..39: chain statistics of the dual engine (engine.hip, dual chain call site); 40..: single-engine chain counters
 // offset-activation scratch per workgroup (u64): per wave two lane-interleaved pair arrays of m entries
-__host__ __device__ inline uint64_t act_scr_u64(uint32_t m) { return (uint64_t)kWaves * 2 * m * 64; }  // 0..15 block phases, 16..31 wave-0 sub-phases
+__host__ __device__ inline uint64_t act_scr_u64(uint32_t m, uint32_t waves = kWaves) { return (uint64_t)waves * 2 * m * 64; }  // 0..15 block phases, 16..31 wave-0 sub-phases
 
 // ---- byte layouts (host and device compute them identically) ----
 __host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
@@ -181,7 +184,7 @@ __host__ __device__ inline uint64_t ws_bytes(uint32_t sides, uint32_t pcap, uint
   uint64_t t = (uint64_t)pcap * slot_bytes(sides, nmax, wcap, lcap);
   t += align16((uint64_t)4 * (lcap + 2) * 4);
   t += align16((uint64_t)2 * (lcap + 2) * 4);
-  t += align16((uint64_t)kWaves * (wcap + 2) * 4);
+  t += align16((uint64_t)kMaxWaves * (wcap + 2) * 4);  // per wave of the widest build
   return align16(t);
 }
 __host__ __device__ inline uint64_t result_bytes(uint32_t sides, uint32_t nmax, uint32_t lcap) {
@@ -254,6 +257,14 @@ static_assert(sizeof(ChainOvf) == 16, "ChainOvf layout");
 constexpr uint32_t kWinStride = 68;
 __host__ __device__ inline uint32_t win_m4(uint32_t nmax) { return (nmax + 3) / 4; }
 __host__ __device__ inline uint32_t win_slot(uint32_t r, uint32_t m4) { return (r & 3u) * m4 + (r >> 2); }
+// window slots one side's carve holds for a build of `waves` waves (the single
+// engine deals read r to wave r % waves: waves * ceil(n / waves) slots)
+__host__ __device__ inline uint32_t win_slots(uint32_t nmax, uint32_t waves) {
+  const uint32_t m = waves * ((nmax + waves - 1) / waves);
+  return m > 4 * win_m4(nmax) ? m : 4 * win_m4(nmax);
+}
+// the chain area's per-wave parts are carved for at least kWaves waves
+__host__ __device__ constexpr uint32_t chain_waves(uint32_t waves) { return waves > (uint32_t)kWaves ? waves : (uint32_t)kWaves; }
 // aggregates of one speculative step of the dual-node chain (dual_chain.hip.hpp)
 struct DualStep {
   uint64_t cost;   // sum over reads of the cheaper side's cost
@@ -272,14 +283,16 @@ inline uint32_t env_chain_kinds() {
 // chain LDS (per side S = chain_sides: the dual engine's chains walk both):
 //   steps[K+1] | ovf[kChainOvf] | tmp RState[kWaves][4] | nom[S][K+1][nmax] u16 |
 //   win[S][4*m4][68 B] (read windows) | wb[S][nmax] u32 | pc[K+1] u32 | pred[S][K+2] u8 | perm[nmax] u8 | m0[nmax] u8
-__host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K, uint32_t sides = 1) {
+__host__ __device__ inline uint64_t chain_lds_bytes(uint32_t nmax, uint32_t K, uint32_t sides = 1,
+                                                    uint32_t waves = kWaves) {
   if (K == 0) return 0;
   const uint64_t S = chain_sides(sides);
+  waves = chain_waves(waves);
   uint64_t t = align16((uint64_t)(K + 1) * (S == 2 ? sizeof(DualStep) : sizeof(ChainStep)));
   t += align16((uint64_t)kChainOvf * sizeof(ChainOvf));
-  t += (uint64_t)kWaves * 4 * 64;  // per wave, one RState per 16-lane group
+  t += (uint64_t)waves * 4 * 64;  // per wave, one RState per 16-lane group
   t += align16(S * (K + 1) * nmax * 2);
-  t += align16(S * 4 * win_m4(nmax) * kWinStride);
+  t += align16(S * win_slots(nmax, waves) * kWinStride);
   t += align16(S * nmax * 4);
   t += align16((uint64_t)(K + 1) * 4);
   t += align16(S * (K + 2));
@@ -307,9 +320,9 @@ __host__ __device__ inline uint32_t hot_sides(uint32_t sides, uint32_t chain, ui
 // LDS: hot RStates[hot_sides][nmax] | chain area | heap | freestack | meta | rinfo[sides][nmax] | fe[sides][nmax] |
 //      heavy list[list_entries] u32 | (dual) child e[kDualChildBatch][2][nmax] u16 | read table [nmax] u32x2
 __host__ __device__ inline uint64_t lds_bytes(uint32_t sides, uint32_t pcap, uint32_t nmax, uint32_t chain,
-                                              uint32_t dual_hot = 0) {
+                                              uint32_t dual_hot = 0, uint32_t waves = kWaves) {
   uint64_t t = (uint64_t)hot_sides(sides, chain, dual_hot) * nmax * sizeof(RState);
-  t += chain_lds_bytes(nmax, chain, sides);
+  t += chain_lds_bytes(nmax, chain, sides, waves);
   t += (uint64_t)pcap * sizeof(HeapEntry);
   t += align16((uint64_t)pcap * 4);
   t += (uint64_t)pcap * sizeof(SlotMeta);

@@ -36,6 +36,11 @@ void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hi
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 }  // namespace wcl
+namespace wcu {  // engine_cu.hip: the 1024-thread single engine (launches of <= one problem per CU)
+void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
+int engine_waves();
+}  // namespace wcu
 namespace wcd {  // engine_dchain.hip: the dual engine with chains (launches with caps.chain > 0)
 void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);

@@ -30,6 +30,8 @@ struct Caps {
   bool gstate = false;  // search state in HBM (engine_gstate.hip): it does not fit LDS
   bool narrow = false;  // 128-thread build (engine_narrow.hip)
   bool lowlat = false;  // 256-thread build at 2 waves/SIMD (engine_lowlat.hip)
+  bool cu = false;      // 1024-thread single engine, one workgroup per CU (engine_cu.hip)
+  uint32_t waves = wc::kWaves;  // waves per workgroup the per-wave layouts are sized for
   bool dual_hot = false;  // dual engine: the popped node's RStates in LDS (EngineArgs::dual_hot)
   uint64_t gsb = 0;     // its bytes per workgroup
   uint32_t conc = 0;    // workgroups the HBM share was planned for
@@ -101,7 +103,7 @@ uint64_t hbm_share(const wc_ctx* ctx, uint64_t cached, double frac);
 // Capacities of one launch over items[ids]; see engine_host.cpp
 int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vector<SubProb>& items,
               const std::vector<uint32_t>& ids, uint64_t hbm_budget, Caps& c, std::string& err,
-              uint32_t max_per_cu = 4);
+              uint32_t max_per_cu = 4, bool cu_ok = false);
 // launches the engine of `caps` (LDS or global-state build) on L's stream
 int launch_kernel(wc_ctx* ctx, Launch& L, wc::EngineArgs& a, const Caps& caps);
 // launch slot k of the context (created on first use)
