@@ -8,7 +8,11 @@
 # Every pass is its own timeout-bounded run. Outputs under gpurun_out/prof_<tag>/;
 # tools/pmc_summary.py condenses them into profiles/.
 #   bash tools/profile_round.sh <tag> [bench args...]
+# PASSES="kt fetch write" limits the passes (default: all six). The default
+# bench line also runs the cfg5 leg: give cfg2 runs --cfg5-loci 0.
 set -e
+PASSES=${PASSES:-"kt fetch write sq1 sq2 tcc"}
+on() { case " $PASSES " in *" $1 "*) return 0;; esac; return 1; }
 TAG=${1:-r02}
 shift || true
 ARGS="$@"
@@ -20,24 +24,36 @@ mkdir -p $OUT
 ( while sleep 30; do date >> $OUT/heartbeat.log; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
+if on kt; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
   python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e $ARGS > $OUT/kt_bench.json
 echo "kt done"
+fi
+if on fetch; then
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
   python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/fetch_bench.json
 echo "fetch done"
+fi
+if on write; then
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
   python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/write_bench.json
 echo "write done"
+fi
+if on sq1; then
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
   SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $OUT/sq1 -o run -- \
   python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/sq1_bench.json
 echo "sq1 done"
+fi
+if on sq2; then
 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SMEM \
   SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/sq2 -o run -- \
   python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/sq2_bench.json
 echo "sq2 done"
+fi
+if on tcc; then
 timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum \
   --output-format csv -d $OUT/tcc -o run -- \
   python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e $ARGS > $OUT/tcc_bench.json
 echo "profile $TAG done"
+fi
