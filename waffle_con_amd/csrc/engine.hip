@@ -1889,6 +1889,7 @@ WC_SINGLE_FN void single_activate(Eng& E, Lo<Ctl>& ctl, uint32_t slot, bool hot,
 // =====================================================================
 // ConsensusDWFA engine (consensus.rs:139-351)
 // =====================================================================
+#ifndef WC_DUAL_ONLY  // (engine_cu_dual.hip: the dual engine only)
 __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SINGLE_WAVES_PER_EU))) single_engine_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
@@ -2151,6 +2152,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
   }
   stream_exit(A);
 }
+#endif  // WC_DUAL_ONLY
 
 // =====================================================================
 // DualConsensusDWFA engine (dual_consensus.rs:240-787)
@@ -2599,9 +2601,11 @@ __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
 
 #endif
 
+#ifndef WC_DUAL_ONLY
 void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(single_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
+#endif
 // waves per workgroup of this build (the host sizes the per-wave layouts)
 int engine_waves() { return kEW; }
 #ifndef WC_SINGLE_ONLY
@@ -2618,7 +2622,11 @@ void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStrea
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot) {
   int nb = 0;
   hipError_t e = hipSuccess;
+#ifndef WC_DUAL_ONLY
   if (sides == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kEB, lds);
+#else
+  if (sides == 1) return 1;
+#endif
 #ifndef WC_SINGLE_ONLY
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_DUAL_CHAIN_CALL)
   else if (dual_hot) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_hot_engine_kernel, kEB, lds);

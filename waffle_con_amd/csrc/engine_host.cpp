@@ -173,13 +173,17 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   // instead of 4. WC_CU=0 disables it, WC_CU=1 forces it (test hook)
   const char* wenv = getenv("WC_CU");
   const int wmode = wenv ? atoi(wenv) : 2;
-  c.cu = cu_ok && sides == 1 && !gstate && chain > 0 && wmode != 0 &&
-           (wmode == 1 || ids.size() <= (uint64_t)ctx->n_cu);
+  // The dual engine's 1024-thread build (engine_cu_dual.hip, no chains) runs
+  // only when forced: it measured slower on one deep locus (cfg4 24.6 vs
+  // 22.8 s), its per-pop serial sections and 110 spilled VGPRs
+  // (77 at 4 waves) outweigh the wider per-read phases.
+  const bool cu_fit = !gstate && wmode != 0 && (wmode == 1 || ids.size() <= (uint64_t)ctx->n_cu);
+  c.cu = cu_ok && cu_fit && (sides == 1 ? chain > 0 : chain == 0 && wmode == 1);
   if (c.cu) c.narrow = c.lowlat = false;
-  c.waves = c.cu ? (uint32_t)std::max(wcu::engine_waves(), kWaves) : (uint32_t)kWaves;
+  c.waves = c.cu ? (uint32_t)std::max(sides == 1 ? wcu::engine_waves() : wcv::engine_waves(), kWaves) : (uint32_t)kWaves;
   c.dual_hot = false;
   auto occupancy = [&](size_t l) {
-    if (c.cu) return wcu::engine_blocks_per_cu(sides, l);
+    if (c.cu) return sides == 1 ? wcu::engine_blocks_per_cu(sides, l) : wcv::engine_blocks_per_cu(sides, l, c.dual_hot);
     if (sides == 2 && chain > 0 && !gstate) return wcd::engine_blocks_per_cu(sides, l);
     return c.narrow ? wcn::engine_blocks_per_cu(sides, l, c.dual_hot)
                     : (c.lowlat ? wcl::engine_blocks_per_cu(sides, l, c.dual_hot)
@@ -339,7 +343,8 @@ int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
   } else if (caps.sides == 2 && caps.chain > 0) {
     wcd::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else if (caps.cu) {
-    wcu::launch_single_engine(a, L.grid, caps.lds, L.stream);
+    if (caps.sides == 1) wcu::launch_single_engine(a, L.grid, caps.lds, L.stream);
+    else wcv::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else if (caps.narrow) {
     if (caps.sides == 1) wcn::launch_single_engine(a, L.grid, caps.lds, L.stream);
     else wcn::launch_dual_engine(a, L.grid, caps.lds, L.stream);
@@ -1220,7 +1225,8 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     bool widened = false;
     for (;;) {
       std::vector<uint32_t> ids(conc, 0);
-      prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(ctx, L->ws.cap, 0.8), caps, err, 8);
+      // (few workgroups, e.g. one deep locus: the 1024-thread dual build)
+      prc = plan_caps(ctx, cfg, 2, env, ids, hbm_share(ctx, L->ws.cap, 0.8), caps, err, 8, true);
       // a first epoch whose workgroups fit more than 4 per CU plans for all of them
       if (prc == WC_OK && !widened && nretry == 0 && !caps.pool_short &&
           std::min<size_t>((size_t)caps.per_cu * ctx->n_cu, conc_cap) > conc) {
