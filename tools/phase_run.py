@@ -123,7 +123,8 @@ def main():
            26: "walk-rounds(w0)", 27: "walk-lane-iterations(w0)", 40: "accept-tracker-steps(w0)",
            41: "accept-tracker-loop(w0)", 42: "walk-lane0-iterations", 43: "chain-entry(w0)",
            44: "prepare-predict-only(w0)", 45: "walk-total(sum over waves)", 46: "walk-heavy-count(all waves)",
-           48: "heavy-row-load(all waves)", 49: "heavy-increase-loop(all waves)", 50: "heavy-store-rebuild(all waves)"}
+           48: "heavy-row-load(all waves)", 49: "heavy-increase-loop(all waves)", 50: "heavy-store-rebuild(all waves)",
+           51: "heavy-call(w0)", 52: "heavy-tail-nominations(w0)"}
     nch = max(1, rep["chains"]["count"])
     rep["sub_cycles_per_chain"] = {SUB[k]: round(cyc[k] / nch, 1) for k in SUB if k < len(cyc)}
     rep["block_cycles_per_chain"] = {PHASES[k]: round(cyc[k] / nch, 1) for k in (8, 9, 10, 11, 14)}

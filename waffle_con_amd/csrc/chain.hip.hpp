@@ -772,8 +772,10 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
         }
         bak |= 1ull << l;
       }
+      SUB_T0(tc);
       const uint32_t e_out = uni(chain_heavy(&E.L.ctmp[4 * wave], v.wf + (uint64_t)rl * E.wcap, E.read(rl), E.rlen(rl), v.con, L0 + jl,
                                              (uint32_t)pred[jl], wc, early, E.wcap, ctl.chain_tot, bdst));
+      SUB_T1(51, tc);
       const bool ok = e_out != kInactive;
       wave_lds_sync();
       if (lane == 0) {
@@ -828,11 +830,13 @@ __device__ inline void chain_walk(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_t L
       wave_lds_sync();
     }
 #endif
+    SUB_T0(td);
     kb = front_bound();  // rebuilt frontiers
     if (pend) {
       pend = false;
       if (j <= jend) step_tail();
     }
+    SUB_T1(52, td);
     SUB_T1(17, tb);
   }
   if (!kFirst && has && !active) {
