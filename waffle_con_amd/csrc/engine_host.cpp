@@ -117,7 +117,9 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   const uint64_t conc = std::max<uint64_t>(1, std::min<uint64_t>(ids.size(), (uint64_t)max_per_cu * ctx->n_cu));
   const uint64_t per_wg = std::max<uint64_t>(16ull << 20, hbm_budget / conc);
   const uint64_t budget = sides == 1 ? (16ull << 20) : std::min<uint64_t>(256ull << 20, per_wg);
-  const uint32_t pmax = sides == 1 ? 256u : 1024u;
+  uint32_t pmax = sides == 1 ? 256u : 1024u;
+  if (const char* e = getenv("WC_SINGLE_PMAX"))  // experiment hook: the single engine's first pool size cap
+    if (sides == 1) pmax = std::max<uint32_t>(16u, (uint32_t)atoi(e));
   uint64_t lmax = sides == 1 ? 40 * 1024 : 52 * 1024;  // dual: still 3 workgroups per CU
   if (const char* e = getenv("WC_DUAL_LDS_KB"))  // experiment hook: LDS budget of the dual node pool
     if (sides == 2) lmax = (uint64_t)atoi(e) * 1024;
