@@ -414,7 +414,12 @@ static_assert(kF == 8, "vote_unit covers split <= 8");
 // Arguments and result by value (no stack objects): returns the new edit
 // distance, or kInactive on wavefront capacity overflow; the work counters go
 // straight to the chain totals.
-__device__ __noinline__ uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
+#ifdef WC_INLINE_HEAVY  // (experiment build: the increase inlined into the walk)
+#define WC_HEAVY_FN __device__ __forceinline__
+#else
+#define WC_HEAVY_FN __device__ __noinline__
+#endif
+WC_HEAVY_FN uint32_t chain_heavy(Sh<RState>* tmp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd, uint32_t blen,
                                              const Gm<uint8_t>* con, uint32_t olen, uint32_t sym, int wc, bool early,
                                              uint32_t wcap, Lo<uint64_t>* tot, Gm<uint32_t>* bak) {
   WaveCounters cnt = {0, 0, 0, 0, 0, 0};
