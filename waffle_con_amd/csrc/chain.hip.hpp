@@ -102,15 +102,21 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     if (rraw_e(h) != kInactive && (rraw_flags(h) & kWide)) atomicOr(&ctl.chain_nochain, 1u);
     Front f;
     front_load(h, f);
-    uint32_t lo = kInactive;
+    uint32_t lo = kInactive, tip = kInactive;
     if (f.e != kInactive) {
       const uint32_t blen = E.rlen(r);
 #pragma unroll
-      for (int k = 0; k < kF; ++k)
-        if ((f.mask >> k) & 1u) lo = min(lo, min(f.fd[k] + f.e - f.fi[k], blen));
+      for (int k = kF - 1; k >= 0; --k)
+        if ((f.mask >> k) & 1u) {
+          const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+          lo = min(lo, min(bo, blen));
+          if (f.fd[k] + f.off == L0 && bo < blen) tip = bo;  // the first tip at the node's end
+        }
     }
     if (lo == kInactive) lo = 0;
     const uint32_t wb = lo & ~15u;
+    // the predictions below read that tip's window offset (cm0 is free until the deal)
+    E.L.cm0[r] = (uint8_t)(tip != kInactive && tip - wb < 64u ? tip - wb : 0xFFu);
     const Gm<uint4>* g = (const Gm<uint4>*)(E.read(r) + wb);
     Sh<uint32_t>* w = (Sh<uint32_t>*)(E.L.cwin + (uint64_t)cwin_slot(r, E.n) * kWinStride);
     const uint4 a0 = g[0], a1 = g[1], a2 = g[2], a3 = g[3];
@@ -140,21 +146,14 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     // upcoming bases of each read's first tip (reads 0..63); every wave
     // predicts the steps t = 1 + wave (mod kEW)
     const uint32_t wave = (uint32_t)wave_id();
-    uint32_t bo_tip = kInactive, blen = 0, wb = 0;
+    // (the window loop left each read's first tip at the node's end as an
+    // offset into its window, 0xFF = none or outside it)
+    uint32_t q0 = 0xFFu, blen = 0, wb = 0;
     const Sh<uint8_t>* win = E.L.cwin + (uint64_t)cwin_slot(min((uint32_t)lane, E.n - 1), E.n) * kWinStride;
     if ((uint32_t)lane < E.n) {
-      Front f;
-      front_load(rstate_load(&E.L.hot[lane]), f);
-      if (f.e != kInactive) {
-        wb = E.L.cwb[lane];
-        blen = E.rlen(lane);
-#pragma unroll
-        for (int k = kF - 1; k >= 0; --k)
-          if ((f.mask >> k) & 1u) {
-            const uint32_t bo = f.fd[k] + f.e - f.fi[k];
-            if (f.fd[k] + f.off == L0 && bo < blen) bo_tip = bo;
-          }
-      }
+      q0 = E.L.cm0[lane];
+      wb = E.L.cwb[lane];
+      blen = E.rlen(lane);
     }
     // all of this wave's bytes under one wait; LDS windows only: a read whose
     // next bases lie past its window does not vote (the prediction is a
@@ -164,8 +163,8 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u) {
       const uint32_t t = 1 + wave + kEW * u;
-      const uint32_t q = bo_tip + t - wb;
-      xs[u] = (bo_tip != kInactive && t <= K && bo_tip + t < blen && q < 64u) ? (uint32_t)win[q] : 0x100u;
+      const uint32_t q = q0 + t;
+      xs[u] = (q0 != 0xFFu && t <= K && wb + q < blen && q < 64u) ? (uint32_t)win[q] : 0x100u;
     }
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u) {
