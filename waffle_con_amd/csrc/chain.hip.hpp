@@ -1295,6 +1295,12 @@ __device__ __forceinline__ uint32_t run_chain_impl(Eng E, Lo<Ctl>& ctl, uint32_t
 __device__ __noinline__ uint32_t run_chain_single(Eng& Eref, Lo<Ctl>& ctl, uint32_t top, uint32_t L0, int s1) {
   return run_chain_impl<false>(eng_uniform(Eref), ctl, top, L0, s1);
 }
+#ifdef WC_CHAIN_REBUILD  // (experiment build: the context rebuilt from the kernel arguments)
+__device__ __noinline__ uint32_t run_chain_single_k(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl,
+                                                    uint32_t top, uint32_t L0, int s1) {
+  return run_chain_impl<false>(callee_eng(kp, P, sbase), ctl, top, L0, s1);
+}
+#endif
 __device__ __noinline__ uint32_t run_chain_dual_single(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl,
                                                        uint32_t top, uint32_t L0, int s1) {
   return run_chain_impl<true>(callee_eng(kp, P, sbase), ctl, top, L0, s1);

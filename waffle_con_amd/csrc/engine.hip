@@ -2076,14 +2076,22 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
       // (past the last activation point every read of this lineage is active)
       uint32_t plen = len;  // the expanded node's length (a chain that popped its last node moves it)
       if (nc == 1 && A.chain && uni(ctl.heap_n) == 0 && (E.P.n_active == E.n || len >= E.P.max_act)) {
+#ifdef WC_CHAIN_REBUILD
+        uint32_t jstar = run_chain_single_k(kernel_args(), E.P, state_base(A, smem), ctl, top, plen, uni((int32_t)ctl.ch_s[0][0]));
+#else
         uint32_t jstar = run_chain_single(E, ctl, top, plen, uni((int32_t)ctl.ch_s[0][0]));
+#endif
         PH_MARK(14);
         // a full chain that also popped its last node N_K (one child, no
         // queue): that child starts the next chain at once
         while (jstar && uni(ctl.chain_next)) {
           plen += jstar - 1;
           const int s1 = uni((int32_t)ctl.chain_sym);
+#ifdef WC_CHAIN_REBUILD
+          jstar = run_chain_single_k(kernel_args(), E.P, state_base(A, smem), ctl, top, plen, s1);
+#else
           jstar = run_chain_single(E, ctl, top, plen, s1);
+#endif
           PH_MARK(14);
           if (!jstar) {
             // the next chain did not start: N_K's one child is pushed literally below
