@@ -189,7 +189,37 @@ class Cfg2:
         if bad:
             raise RuntimeError("engine error: %s" % bad[0])
         self.last = res
+        self.last_st = st
         return st, len(res)
+
+    COUNTERS = ("updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored")
+
+    def extra(self):
+        """One more (untimed) pass of the same launch with per-locus counters and
+        completion times: where the launch's time goes (verdict r4 item 6) and
+        the per-locus counters the CPU check compares (item 2)."""
+        if self.name != "cfg2":
+            return {}
+        res, st = self.batch.consensus(self.cfg, return_errors=True, per_problem=True)
+        pp = st["per_problem"]
+        self._pp = pp
+        self._pp_same = all([(c.sequence(), list(c.scores())) for c in res[i]] ==
+                            [(c.sequence(), list(c.scores())) for c in self.last[i]] for i in range(len(res)))
+        wall = sorted(p["wall_ms"] for p in pp)
+        t100 = wall[-1]
+
+        def q(f):
+            return wall[min(len(wall) - 1, int(f * len(wall)))]
+        # every locus of a cfg2 launch has its own workgroup from t = 0 (1,000 loci
+        # <= 4 workgroups x 256 CUs), so a workgroup slot is busy until its
+        # locus's completion: busy fraction = sum(wall) / (loci x t100)
+        return {"cfg2_launch_profile": {
+            "what": "per-locus completion times inside one 1,000-locus launch (wc_results_problem_stats wall_ms, "
+                    "untimed pass after the timed steps)",
+            "kernel_ms": st["kernel_ms"], "t50_ms": q(0.5), "t90_ms": q(0.9), "t95_ms": q(0.95), "t100_ms": t100,
+            "workgroup_busy_frac": sum(wall) / (len(wall) * t100) if t100 > 0 else None,
+            "slowest_loci": sorted(range(len(pp)), key=lambda i: -pp[i]["wall_ms"])[:5],
+            "results_equal_timed_pass": self._pp_same}}
 
     def config(self):
         return {"workload": "ConsensusDWFA cfg2 throughput: %d loci/GPU x %d reads x %d bp @ %g error, min_count %d"
@@ -258,10 +288,26 @@ class Cfg2:
         upd = sum(c["updates"] for _, c in outs)
         ok = all([(c.sequence(), list(c.scores())) for c in self.last[i]] ==
                  [(r["sequence"], r["scores"]) for r in outs[i][0]] for i in range(n))
-        return {"value": upd / dt, "unit": "updates/s", "loci_per_s": n / dt,
-                "sample": "%d loci of the same workload (seeds %d..%d), C++ oracle, one locus per thread, %.1f s wall"
-                          % (n, self.seeds[0], self.seeds[0] + n - 1, dt),
-                "gpu_matches_cpu_on_sample": ok, "checked": "sequences + per-read scores of every result"}
+        out = {"value": upd / dt, "unit": "updates/s", "loci_per_s": n / dt,
+               "sample": "%d loci of the same workload (seeds %d..%d), C++ oracle, one locus per thread, %.1f s wall"
+                         % (n, self.seeds[0], self.seeds[0] + n - 1, dt),
+               "gpu_matches_cpu_on_sample": ok, "checked": "sequences + per-read scores of every result"}
+        # the search path, not only its answer: every work counter of every
+        # sampled locus (a race that changes the path but not the result shows
+        # here), from the per-locus pass; and the timed steps' totals when the
+        # sample is the whole batch
+        pp = getattr(self, "_pp", None)
+        if pp is not None and self.name == "cfg2":
+            bad = [i for i in range(n) if any(pp[i][k] != outs[i][1][k] for k in self.COUNTERS)]
+            out["counters_match_on_sample"] = not bad and self._pp_same
+            out["counters_checked"] = "%s of each of %d loci (per-locus pass), results of that pass = the timed " \
+                                      "pass's" % ("/".join(self.COUNTERS), n)
+            if bad:
+                out["counter_mismatch_loci"] = bad[:10]
+            if n == len(self.loci):
+                out["timed_step_totals_match"] = all(
+                    self.last_st[k] == sum(c[k] for _, c in outs) for k in self.COUNTERS)
+        return out
 
 
 class Cfg2Api(Cfg2):

@@ -1,6 +1,6 @@
 //! ConsensusDWFA (consensus.rs:76-365): the same constructors, accessors and
 //! errors; consensus() runs the search on the MI355X (device::service_single).
-use std::collections::HashSet;
+use rustc_hash::FxHashSet as HashSet;
 
 use crate::cdwfa_config::{CdwfaConfig, ConsensusCost};
 use crate::device;
@@ -65,7 +65,7 @@ impl<'a> ConsensusDWFA<'a> {
     /// consensus.rs:139-351, on the device. Re-entrant: any number of threads
     /// may call it at once (they share the device's submission service).
     pub fn consensus(&self) -> Result<Vec<Consensus>, Box<dyn std::error::Error>> {
-        let prob = device::Problem::new(&self.sequences, &self.offsets);
+        let prob = device::Problem::new(&self.sequences, &self.offsets)?;
         device::service_single(&self.config, &prob)
     }
 

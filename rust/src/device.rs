@@ -31,7 +31,7 @@ pub(crate) fn err(code: c_int, message: String) -> Box<dyn std::error::Error> {
     Box::new(WcError { code, message })
 }
 
-unsafe fn cstr(p: *const std::os::raw::c_char) -> String {
+pub(crate) unsafe fn cstr(p: *const std::os::raw::c_char) -> String {
     if p.is_null() {
         String::new()
     } else {
@@ -87,12 +87,18 @@ pub(crate) struct Problem {
 }
 
 impl Problem {
-    pub fn new(reads: &[&[u8]], offsets: &[Option<usize>]) -> Problem {
-        Problem {
+    /// One offset per read (the C library reads `n_reads` of each array, so a
+    /// short offsets vector would be read past its end: refused here).
+    pub fn new(reads: &[&[u8]], offsets: &[Option<usize>]) -> Result<Problem, Box<dyn std::error::Error>> {
+        if offsets.len() != reads.len() {
+            return Err(err(ffi::WC_E_BAD_INPUT,
+                           format!("expected {} offsets (one per read), got {}", reads.len(), offsets.len())));
+        }
+        Ok(Problem {
             ptrs: reads.iter().map(|s| s.as_ptr()).collect(),
             lens: reads.iter().map(|s| s.len() as u64).collect(),
             offs: offsets.iter().map(|o| o.map_or(-1, |v| v as i64)).collect(),
-        }
+        })
     }
 
     pub fn raw(&self) -> ffi::wc_problem {
@@ -115,15 +121,34 @@ pub(crate) struct ChainProblem {
 }
 
 impl ChainProblem {
-    pub fn new(chains: &[Vec<&[u8]>], offsets: &[Vec<Option<usize>>], groups: &[Option<usize>]) -> ChainProblem {
-        let levels = chains.first().map_or(0, |c| c.len()) as u32;
-        ChainProblem {
-            levels,
+    /// Every chain has the first chain's level count, one offset per (chain,
+    /// level) and one seed group per chain: the C library reads `n_chains x
+    /// levels` entries of each array, so ragged input would be read past its
+    /// end. The reference would panic indexing it (priority_consensus.rs:172-341);
+    /// here it is an error.
+    pub fn new(chains: &[Vec<&[u8]>], offsets: &[Vec<Option<usize>>], groups: &[Option<usize>])
+               -> Result<ChainProblem, Box<dyn std::error::Error>> {
+        let levels = chains.first().map_or(0, |c| c.len());
+        let bad = |m: String| Err(err(ffi::WC_E_BAD_INPUT, m));
+        if let Some(i) = chains.iter().position(|c| c.len() != levels) {
+            return bad(format!("sequence chain {} has {} levels, expected {}", i, chains[i].len(), levels));
+        }
+        if offsets.len() != chains.len() {
+            return bad(format!("expected {} offset vectors (one per chain), got {}", chains.len(), offsets.len()));
+        }
+        if let Some(i) = offsets.iter().position(|o| o.len() != levels) {
+            return bad(format!("offsets of chain {} have {} entries, expected {}", i, offsets[i].len(), levels));
+        }
+        if groups.len() != chains.len() {
+            return bad(format!("expected {} seed groups (one per chain), got {}", chains.len(), groups.len()));
+        }
+        Ok(ChainProblem {
+            levels: levels as u32,
             ptrs: chains.iter().flat_map(|c| c.iter().map(|s| s.as_ptr())).collect(),
             lens: chains.iter().flat_map(|c| c.iter().map(|s| s.len() as u64)).collect(),
             offs: offsets.iter().flat_map(|c| c.iter().map(|o| o.map_or(-1, |v| v as i64))).collect(),
             groups: groups.iter().map(|g| g.map_or(-1, |v| v as i64)).collect(),
-        }
+        })
     }
 
     pub fn raw(&self) -> ffi::wc_chain_problem {
@@ -269,7 +294,7 @@ thread_local! {
     static CTX: std::cell::RefCell<Option<Ctx>> = const { std::cell::RefCell::new(None) };
 }
 
-fn with_ctx<T>(f: impl FnOnce(*mut ffi::wc_ctx) -> Result<T, Box<dyn std::error::Error>>) -> Result<T, Box<dyn std::error::Error>> {
+pub(crate) fn with_ctx<T>(f: impl FnOnce(*mut ffi::wc_ctx) -> Result<T, Box<dyn std::error::Error>>) -> Result<T, Box<dyn std::error::Error>> {
     CTX.with(|c| {
         let mut c = c.borrow_mut();
         if c.is_none() {
@@ -288,7 +313,7 @@ fn with_ctx<T>(f: impl FnOnce(*mut ffi::wc_ctx) -> Result<T, Box<dyn std::error:
 /// and offsets). Per-locus errors are returned per locus.
 pub fn consensus_batch(cfg: &CdwfaConfig, loci: &[(Vec<&[u8]>, Vec<Option<usize>>)])
                        -> Result<Vec<Result<Vec<Consensus>, Box<dyn std::error::Error>>>, Box<dyn std::error::Error>> {
-    let probs: Vec<Problem> = loci.iter().map(|(r, o)| Problem::new(r, o)).collect();
+    let probs: Vec<Problem> = loci.iter().map(|(r, o)| Problem::new(r, o)).collect::<Result<_, _>>()?;
     let raw: Vec<ffi::wc_problem> = probs.iter().map(|p| p.raw()).collect();
     let c = cfg.to_wc();
     with_ctx(|ctx| {
@@ -305,7 +330,7 @@ pub fn consensus_batch(cfg: &CdwfaConfig, loci: &[(Vec<&[u8]>, Vec<Option<usize>
 /// DualConsensusDWFA::consensus for many loci in one launch.
 pub fn dual_consensus_batch(cfg: &CdwfaConfig, loci: &[(Vec<&[u8]>, Vec<Option<usize>>)])
                             -> Result<Vec<Result<Vec<DualConsensus>, Box<dyn std::error::Error>>>, Box<dyn std::error::Error>> {
-    let probs: Vec<Problem> = loci.iter().map(|(r, o)| Problem::new(r, o)).collect();
+    let probs: Vec<Problem> = loci.iter().map(|(r, o)| Problem::new(r, o)).collect::<Result<_, _>>()?;
     let raw: Vec<ffi::wc_problem> = probs.iter().map(|p| p.raw()).collect();
     let c = cfg.to_wc();
     with_ctx(|ctx| {
@@ -324,7 +349,7 @@ pub fn dual_consensus_batch(cfg: &CdwfaConfig, loci: &[(Vec<&[u8]>, Vec<Option<u
 #[allow(clippy::type_complexity)]
 pub fn priority_consensus_batch(cfg: &CdwfaConfig, loci: &[(Vec<Vec<&[u8]>>, Vec<Vec<Option<usize>>>, Vec<Option<usize>>)])
                                 -> Result<Vec<Result<PriorityConsensus, Box<dyn std::error::Error>>>, Box<dyn std::error::Error>> {
-    let probs: Vec<ChainProblem> = loci.iter().map(|(c, o, g)| ChainProblem::new(c, o, g)).collect();
+    let probs: Vec<ChainProblem> = loci.iter().map(|(c, o, g)| ChainProblem::new(c, o, g)).collect::<Result<_, _>>()?;
     let raw: Vec<ffi::wc_chain_problem> = probs.iter().map(|p| p.raw()).collect();
     let c = cfg.to_wc();
     with_ctx(|ctx| {

@@ -1,6 +1,6 @@
 //! DualConsensusDWFA (dual_consensus.rs:179-800): the same constructors,
 //! accessors and errors; consensus() runs the search on the MI355X.
-use std::collections::HashSet;
+use rustc_hash::FxHashSet as HashSet;
 
 use crate::cdwfa_config::{CdwfaConfig, ConsensusCost};
 use crate::consensus::Consensus;
@@ -91,7 +91,7 @@ impl<'a> DualConsensusDWFA<'a> {
 
     /// dual_consensus.rs:240-787, on the device (re-entrant)
     pub fn consensus(&self) -> Result<Vec<DualConsensus>, Box<dyn std::error::Error>> {
-        let prob = device::Problem::new(&self.sequences, &self.offsets);
+        let prob = device::Problem::new(&self.sequences, &self.offsets)?;
         device::service_dual(&self.config, &prob)
     }
 

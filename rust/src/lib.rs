@@ -2,7 +2,8 @@
 # waffle_con on AMD MI355X
 
 The public API of `waffle_con` v0.4.4 (`cdwfa_config`, `consensus`,
-`dual_consensus`, `priority_consensus`, `sequence_alignment`, `example_gen`)
+`dual_consensus`, `dynamic_wfa`, `example_gen`, `multi_consensus`,
+`pqueue_tracker`, `priority_consensus`, `sequence_alignment`)
 with the dynamic-WFA consensus search running on an MI355X (gfx950): every
 `consensus()` call goes to the device library built from
 `../waffle_con_amd/csrc` (C ABI: `../include/waffle_con.h`, raw bindings in
@@ -38,10 +39,16 @@ pub mod consensus;
 pub mod device;
 /// DualConsensusDWFA and DualConsensus (dual_consensus.rs)
 pub mod dual_consensus;
+/// DWFALite (dynamic_wfa.rs), its updates run on the device
+pub mod dynamic_wfa;
 /// generate_test (example_gen.rs), the reference's RNG restated in the library
 pub mod example_gen;
 /// Raw C ABI of the MI355X library (include/waffle_con.h)
 pub mod ffi;
+/// MultiConsensus (multi_consensus.rs), the deprecated result type
+pub mod multi_consensus;
+/// PQueueTracker (pqueue_tracker.rs)
+pub mod pqueue_tracker;
 /// PriorityConsensusDWFA and PriorityConsensus (priority_consensus.rs)
 pub mod priority_consensus;
 /// wfa_ed / wfa_ed_config (sequence_alignment.rs)

@@ -3,7 +3,7 @@
 //! the reference's LIFO work stack inside the library
 //! (wc_service_priority_consensus) and every DualConsensusDWFA sub-problem runs
 //! in the device's shared launches.
-use std::collections::HashSet;
+use rustc_hash::FxHashSet as HashSet;
 
 use crate::cdwfa_config::{CdwfaConfig, ConsensusCost};
 use crate::consensus::Consensus;
@@ -77,7 +77,7 @@ impl<'a> PriorityConsensusDWFA<'a> {
 
     /// priority_consensus.rs:172-341, on the device (re-entrant)
     pub fn consensus(&self) -> Result<PriorityConsensus, Box<dyn std::error::Error>> {
-        let prob = device::ChainProblem::new(&self.sequences, &self.offsets, &self.seed_groups);
+        let prob = device::ChainProblem::new(&self.sequences, &self.offsets, &self.seed_groups)?;
         device::service_priority(&self.config, &prob)
     }
 

@@ -175,3 +175,48 @@ def test_batch_path_requests_under_lane_traffic():
     assert _run_threads(jobs, 16) == exp
     s1 = _stats()
     assert s1["fallback"] - s0["fallback"] == 4 + 2
+
+
+def test_destroy_during_threaded_priority_calls():
+    """wc_service_destroy while PriorityConsensusDWFA calls are inside: the
+    calls already in submit further sub-problems (and retries) after stop is
+    set; the service thread keeps serving them until the last one leaves, so
+    every such call completes with the oracle's result and destroy returns.
+    Calls that start after stop are refused (WC_E_HIP)."""
+    import time
+    from waffle_con_amd import _lib, synth
+    from waffle_con_amd.cdwfa_config import CdwfaConfig
+    from waffle_con_amd.priority_consensus import priority_service_call
+    cfg = CdwfaConfig(wildcard=ord("*"))
+    svc = _lib.Service(0)
+    loci = [synth.cfg5_locus(s) for s in (20, 21, 22, 23)]
+    out, refused, errors = [None] * len(loci), [], []
+
+    def call(i):
+        try:
+            (r,), _ = priority_service_call(([list(map(bytes, ch)) for ch in loci[i]], None, None), cfg,
+                                            svc=svc)
+            out[i] = {"consensuses": [[hip._cons(c) for c in chain] for chain in r.consensuses()],
+                      "sequence_indices": list(r.sequence_indices())}
+        except _lib.WaffleConError as e:
+            refused.append((i, e))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=call, args=(i,)) for i in range(len(loci))]
+    for t in th:
+        t.start()
+    time.sleep(0.5)  # the calls are inside, with sub-problems to go
+    t0 = time.time()
+    svc.close()
+    t_destroy = time.time() - t0
+    for t in th:
+        t.join(60)
+        assert not t.is_alive(), "a priority call hung across wc_service_destroy"
+    assert not errors, errors
+    done = [i for i in range(len(loci)) if out[i] is not None]
+    assert len(done) + len(refused) == len(loci)
+    assert done, "no call was inside the service when it was destroyed"
+    for i in done:
+        assert out[i] == orc.priority_consensus(loci[i], wildcard=ord("*"))
+    print("destroy took %.2f s, %d calls completed, %d refused" % (t_destroy, len(done), len(refused)))

@@ -154,11 +154,61 @@ def test_public_api_surface_matches_the_reference():
                                   "wildcard: Option<u8>) -> usize"],
         "example_gen.rs": ["pub fn generate_test(alphabet_size: u8, seq_len: usize, num_samples: usize, "
                            "error_rate: f64) -> (Vec<u8>, Vec<Vec<u8>>)"],
+        # dynamic_wfa.rs:12-265
+        "dynamic_wfa.rs": ["#[derive(Clone, Debug, Eq, Hash, PartialEq)] pub struct DWFALite",
+                           "impl Default for DWFALite",
+                           "pub fn new(wildcard: Option<u8>, allow_early_termination: bool) -> DWFALite",
+                           "pub fn set_offset(&mut self, offset: usize)",
+                           "pub fn update(&mut self, baseline_seq: &[u8], other_seq: &[u8]) -> "
+                           "Result<usize, Box<dyn std::error::Error>>",
+                           "pub fn finalize(&mut self, baseline_seq: &[u8], other_seq: &[u8]) -> "
+                           "Result<(), Box<dyn std::error::Error>>",
+                           "pub fn maximum_baseline_distance(&self) -> usize",
+                           "pub fn maximum_other_distance(&self) -> usize",
+                           "pub fn reached_baseline_end(&self, baseline_seq: &[u8]) -> bool",
+                           "pub fn get_extension_candidates(&self, baseline_seq: &[u8], other_seq: &[u8]) -> "
+                           "HashMap<u8, usize>",
+                           "use rustc_hash::FxHashMap as HashMap;",
+                           "pub fn edit_distance(&self) -> usize", "pub fn wavefront(&self) -> &[usize]",
+                           "Cannot push more bases after finalizing a DWFA", "Cannot finalize a DWFA twice.",
+                           "ffi::wc_dwfa_batch"],
+        # ragged or short inputs are refused before the ABI (never read past an array)
+        "device.rs": ["expected {} offsets (one per read), got {}", "sequence chain {} has {} levels, expected {}",
+                      "offsets of chain {} have {} entries, expected {}",
+                      "expected {} seed groups (one per chain), got {}", ".collect::<Result<_, _>>()?"],
+        # pqueue_tracker.rs:10-144
+        "pqueue_tracker.rs": ["pub struct PQueueTracker",
+                              "pub fn with_capacity(initial_size: usize, capacity_per_size: usize) -> PQueueTracker",
+                              "pub fn insert(&mut self, value: usize)", "pub fn remove(&mut self, value: usize)",
+                              "pub fn increment_threshold(&mut self)",
+                              "pub fn increase_threshold(&mut self, new_threshold: usize)",
+                              "pub fn process(&mut self, value: usize) -> Result<(), Box<dyn std::error::Error>>",
+                              "pub fn processed(&self, value: usize) -> usize",
+                              "pub fn at_capacity(&self, value: usize) -> bool", "pub fn len(&self) -> usize",
+                              "pub fn unfiltered_len(&self) -> usize", "pub fn is_empty(&self) -> bool",
+                              "pub fn threshold(&self) -> usize", "pub fn occupancy(&self, value: usize) -> usize",
+                              "Capacity is full"],
+        # multi_consensus.rs:11-65
+        "multi_consensus.rs": ["#[derive(Debug, PartialEq)] pub struct MultiConsensus",
+                               "pub fn new(consensuses: Vec<Consensus>, sequence_indices: Vec<usize>) -> "
+                               "MultiConsensus",
+                               "pub fn consensuses(&self) -> &[Consensus]",
+                               "pub fn sequence_indices(&self) -> &[usize]"],
     }
     for f, items in want.items():
         src = " ".join(open(os.path.join(ROOT, "rust", "src", f)).read().split())
         for it in items:
             assert it in src, (f, it)
+    # the reference's nine public modules (lib.rs:38-55), each a file of the crate
+    lib_rs = open(os.path.join(ROOT, "rust", "src", "lib.rs")).read()
+    for m in ("cdwfa_config", "consensus", "dual_consensus", "dynamic_wfa", "example_gen", "multi_consensus",
+              "pqueue_tracker", "priority_consensus", "sequence_alignment"):
+        assert "pub mod %s;" % m in lib_rs, m
+        assert os.path.exists(os.path.join(ROOT, "rust", "src", m + ".rs")), m
+    # the reference's FxHash types in the public signatures
+    for f in ("consensus.rs", "dual_consensus.rs", "priority_consensus.rs"):
+        assert "use rustc_hash::FxHashSet as HashSet;" in open(os.path.join(ROOT, "rust", "src", f)).read(), f
     cargo = open(os.path.join(ROOT, "rust", "Cargo.toml")).read()
+    assert 'rustc-hash = "1.1.0"' in cargo
     assert 'name = "waffle_con"' in cargo and "build.rs" in cargo
     assert "gfx950" in open(os.path.join(ROOT, "rust", "build.rs")).read()

@@ -102,6 +102,10 @@ def main():
                 30: "votes-sums(w0)", 31: "active-min-growth(t0)", 22: "prune-setup(t0)", 23: "prune-loop(t0)",
                 24: "prune-atomics(t0)", 25: "prune-barrier1(t0)", 26: "prune-tail(t0)"}
         rep["dual_sub_per_pop"] = {DSUB[k]: round(cyc[k] / np_, 2) for k in DSUB if k < len(cyc)}
+        # the one-wave dual engine (wave_dual.hip.hpp) uses 32..39 for its own timers
+        rep["wave_sub_per_pop"] = {nm: round(cyc[k] / np_, 2) for k, nm in (
+            (32, "hot-load-block"), (33, "hot-loads"), (34, "analysis-lanes"), (35, "analysis-aggregates"),
+            (36, "reached"), (37, "fast-pushes"), (38, "votes"), (39, "selection")) if k < len(cyc)}
         if len(cyc) >= 40:  # chain statistics per kind (engine.hip dual chain call site)
             for kind, b in (("single_consensus_chains", 32), ("dual_chains", 35)):
                 n = max(1, cyc[b])

@@ -290,7 +290,8 @@ def service_enabled():
     return os.environ.get("WAFFLE_CON_SERVICE", "1") != "0"
 
 
-_service_failed = set()
+_service_failed = {}  # device -> (time of the last failed creation, message)
+_SERVICE_RETRY_S = 30.0
 
 
 def service(device=None):
@@ -301,20 +302,42 @@ def service(device=None):
     if device is None:
         device = default_context().device
     svc = _services.get(device)
-    if svc is None and device not in _service_failed:
+    if svc is None and _service_may_try(device):
         with _lock:
             svc = _services.get(device)
-            if svc is None and device not in _service_failed:
+            if svc is None and _service_may_try(device):
                 try:
                     svc = Service(device)
-                except WaffleConError:
-                    _service_failed.add(device)
+                except WaffleConError as e:
+                    # a transient failure (the pinned arena under memory
+                    # pressure) must not turn the service off for good: say
+                    # so once per failure, retry after a back-off
+                    import sys
+                    import time
+                    _service_failed[device] = (time.monotonic(), str(e))
+                    print("[waffle_con] submission service unavailable on device %d (%s); per-call launches "
+                          "for %.0f s" % (device, e, _SERVICE_RETRY_S), file=sys.stderr)
                     return None
+                _service_failed.pop(device, None)
                 _services[device] = svc
                 if len(_services) == 1:
                     import atexit
                     atexit.register(close_services)
     return svc
+
+
+def _service_may_try(device):
+    f = _service_failed.get(device)
+    if f is None:
+        return True
+    import time
+    return time.monotonic() - f[0] >= _SERVICE_RETRY_S
+
+
+def service_failure(device=0):
+    """The last failed service creation on `device` as (monotonic time,
+    message), or None."""
+    return _service_failed.get(device)
 
 
 def close_services():

@@ -2535,7 +2535,21 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
   stream_exit(A);
 }
 
-#ifndef WC_SINGLE_ONLY  // (engine_cu.hip: the single engine only)
+#ifdef WC_WAVE_DUAL
+#include "wave_dual.hip.hpp"
+// one kernel per reads-per-lane count (engine_wave.hip): problems of <= 64
+// reads, and of <= 128 (two reads per lane)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_wave1_kernel(EngineArgs A) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Ctl ctl_lds;
+  dual_main_wave<1>(A, smem, *(Lo<Ctl>*)&ctl_lds);
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_wave2_kernel(EngineArgs A) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Ctl ctl_lds;
+  dual_main_wave<2>(A, smem, *(Lo<Ctl>*)&ctl_lds);
+}
+#elif !defined(WC_SINGLE_ONLY)  // (engine_cu.hip: the single engine only)
 // two kernels, one per dual_hot: in one kernel the two paths' register
 // allocations merge (the 4-wave build spilled 236 VGPRs instead of 84)
 __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_engine_kernel(EngineArgs A) {
@@ -2552,7 +2566,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUA
 #endif
 #endif  // WC_SINGLE_ONLY
 
-#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT) && !defined(WC_CU)
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT) && !defined(WC_CU) && !defined(WC_WAVE_DUAL)
 // =====================================================================
 // standalone DWFALite jobs (dynamic_wfa.rs:48-265): one wave per job
 // =====================================================================
@@ -2616,7 +2630,19 @@ void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStr
 #endif
 // waves per workgroup of this build (the host sizes the per-wave layouts)
 int engine_waves() { return kEW; }
-#ifndef WC_SINGLE_ONLY
+#ifdef WC_WAVE_DUAL
+void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
+  if (a.nmax <= 64) hipLaunchKernelGGL(dual_wave1_kernel, dim3(grid), dim3(64), lds, s, a);
+  else hipLaunchKernelGGL(dual_wave2_kernel, dim3(grid), dim3(64), lds, s, a);
+}
+// workgroups per CU of the build that runs problems of nmax reads
+int wave_blocks_per_cu(uint32_t nmax, size_t lds) {
+  int nb = 0;
+  const hipError_t e = nmax <= 64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave1_kernel, 64, lds)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave2_kernel, 64, lds);
+  return e == hipSuccess && nb > 0 ? nb : 1;
+}
+#elif !defined(WC_SINGLE_ONLY)
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_DUAL_CHAIN_CALL)
   if (a.dual_hot) {
@@ -2627,6 +2653,7 @@ void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStrea
   hipLaunchKernelGGL(dual_engine_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
 #endif
+#ifndef WC_WAVE_DUAL
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot) {
   int nb = 0;
   hipError_t e = hipSuccess;
@@ -2643,7 +2670,8 @@ int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot) {
 #endif
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
-#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT) && !defined(WC_CU)
+#endif
+#if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT) && !defined(WC_CU) && !defined(WC_WAVE_DUAL)
 void launch_dwfa_jobs(DwfaDevJob* jobs, uint32_t n, hipStream_t s) {
   hipLaunchKernelGGL(dwfa_jobs_kernel, dim3(n), dim3(64), 0, s, jobs);
 }

@@ -42,14 +42,15 @@ void persistent_begin() {
   std::lock_guard<std::mutex> g(g_persist_mu);
   g_persist_running++;
 }
+// The parked buffers are freed under the lock: a persistent_begin on another
+// thread (and the launch that follows it) waits for these frees, which would
+// otherwise wait for that new persistent kernel (the deadlock the deferral
+// exists to prevent).
 void persistent_end() {
-  std::vector<std::pair<void*, bool>> go;
-  {
-    std::lock_guard<std::mutex> g(g_persist_mu);
-    if (--g_persist_running > 0) return;
-    go.swap(g_parked);
-  }
-  for (auto& b : go) (void)(b.second ? hipHostFree(b.first) : hipFree(b.first));
+  std::lock_guard<std::mutex> g(g_persist_mu);
+  if (--g_persist_running > 0) return;
+  for (auto& b : g_parked) (void)(b.second ? hipHostFree(b.first) : hipFree(b.first));
+  g_parked.clear();
 }
 bool free_deferred(void* p, bool host) {
   std::lock_guard<std::mutex> g(g_persist_mu);
@@ -182,9 +183,17 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   const bool cu_fit = !gstate && wmode != 0 && (wmode == 1 || ids.size() <= (uint64_t)ctx->n_cu);
   c.cu = cu_ok && cu_fit && (sides == 1 ? chain > 0 : chain == 0 && wmode == 1);
   if (c.cu) c.narrow = c.lowlat = false;
+  // The dual engine on one wave per problem (engine_wave.hip): dual searches
+  // without offsets of at most 128 reads, whose popped node stays in LDS with
+  // its tip bytes in registers. WC_WAVE=1 enables it.
+  const char* wvenv = getenv("WC_WAVE");
+  c.wave = sides == 2 && chain == 0 && !gstate && !any_act && nmax <= 128 && wvenv && atoi(wvenv) == 1 &&
+           lds_bytes(sides, pcap, nmax, 0, 1) <= kLdsMax;
+  if (c.wave) c.narrow = c.lowlat = c.cu = false;
   c.waves = c.cu ? (uint32_t)std::max(sides == 1 ? wcu::engine_waves() : wcv::engine_waves(), kWaves) : (uint32_t)kWaves;
   c.dual_hot = false;
   auto occupancy = [&](size_t l) {
+    if (c.wave) return wcw::wave_blocks_per_cu(nmax, l);
     if (c.cu) return sides == 1 ? wcu::engine_blocks_per_cu(sides, l) : wcv::engine_blocks_per_cu(sides, l, c.dual_hot);
     if (sides == 2 && chain > 0 && !gstate) return wcd::engine_blocks_per_cu(sides, l);
     return c.narrow ? wcn::engine_blocks_per_cu(sides, l, c.dual_hot)
@@ -199,7 +208,8 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   // by default: WC_DUAL_HOT=1 turns it on where it costs the launch no
   // workgroups (same occupancy, or room for every problem anyway),
   // WC_DUAL_HOT=2 wherever the LDS allows.
-  if (sides == 2 && chain == 0 && !gstate) {
+  if (c.wave) c.dual_hot = true;  // (the LDS carve of its hot node)
+  if (sides == 2 && chain == 0 && !gstate && !c.wave) {
     const char* henv = getenv("WC_DUAL_HOT");
     const int hmode = henv ? atoi(henv) : 0;
     const uint64_t lhot = lds_bytes(sides, pcap, nmax, 0, 1);
@@ -344,6 +354,8 @@ int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
     else wcg::launch_dual_engine(a, L.grid, 0, L.stream);
   } else if (caps.sides == 2 && caps.chain > 0) {
     wcd::launch_dual_engine(a, L.grid, caps.lds, L.stream);
+  } else if (caps.wave) {
+    wcw::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else if (caps.cu) {
     if (caps.sides == 1) wcu::launch_single_engine(a, L.grid, caps.lds, L.stream);
     else wcv::launch_dual_engine(a, L.grid, caps.lds, L.stream);
@@ -468,8 +480,8 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   if (krc != WC_OK) return krc;
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d cu=%d dual_hot=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
-            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, (int)caps.cu, (int)caps.dual_hot, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
+    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d cu=%d wave=%d dual_hot=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
+            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, (int)caps.cu, (int)caps.wave, (int)caps.dual_hot, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
   return WC_OK;
 }
 
@@ -764,9 +776,9 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   }
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u narrow=%d lowlat=%d dual_hot=%d\n",
+    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u narrow=%d lowlat=%d wave=%d dual_hot=%d\n",
             L.grid, caps.per_cu, caps.lds, caps.pcap, caps.wcap, caps.lcap, caps.nmax, caps.rmax, (int)caps.narrow,
-            (int)caps.lowlat, (int)caps.dual_hot);
+            (int)caps.lowlat, (int)caps.wave, (int)caps.dual_hot);
 
   // publication state: seq -> item, read-ring position; incomplete seqs in order
   std::vector<uint32_t> seq_item;

@@ -46,6 +46,10 @@ void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipS
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 int engine_waves();
 }  // namespace wcv
+namespace wcw {  // engine_wave.hip: the dual engine on one wave per problem (no offsets, <= 128 reads)
+void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+int wave_blocks_per_cu(uint32_t nmax, size_t lds);
+}  // namespace wcw
 namespace wcd {  // engine_dchain.hip: the dual engine with chains (launches with caps.chain > 0)
 void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);

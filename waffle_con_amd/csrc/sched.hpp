@@ -31,6 +31,7 @@ struct Caps {
   bool narrow = false;  // 128-thread build (engine_narrow.hip)
   bool lowlat = false;  // 256-thread build at 2 waves/SIMD (engine_lowlat.hip)
   bool cu = false;      // 1024-thread single engine, one workgroup per CU (engine_cu.hip)
+  bool wave = false;    // the dual engine on one wave per problem (engine_wave.hip)
   uint32_t waves = wc::kWaves;  // waves per workgroup the per-wave layouts are sized for
   bool dual_hot = false;  // dual engine: the popped node's RStates in LDS (EngineArgs::dual_hot)
   uint64_t gsb = 0;     // its bytes per workgroup

@@ -528,10 +528,14 @@ void service_loop(wc_service* S) {
         }
       }
     }
-    if (S->stop && S->ready.empty() && S->fbq.empty() && !ln.running) break;
+    // A stopping service still serves the calls already inside: a priority
+    // call submits its next sub-problem, and a retried or failed-lane request
+    // comes back through fbq, after stop is set. It ends with the last of them
+    // (~InFlight wakes it).
+    if (S->stop && S->inflight == 0 && S->ready.empty() && S->fbq.empty() && !ln.running) break;
     if (!progress) {
       if (!ln.running && S->ready.empty() && S->fbq.empty())
-        S->cv_svc.wait(lk, [&] { return S->stop || !S->ready.empty() || !S->fbq.empty(); });
+        S->cv_svc.wait(lk, [&] { return (S->stop && S->inflight == 0) || !S->ready.empty() || !S->fbq.empty(); });
       else S->cv_svc.wait_for(lk, std::chrono::microseconds(20));
     }
   }
@@ -551,7 +555,10 @@ struct InFlight {
   ~InFlight() {
     if (!ok) return;
     std::lock_guard<std::mutex> g(S->mu);
-    if (--S->inflight == 0) S->cv_idle.notify_all();
+    if (--S->inflight == 0) {
+      S->cv_idle.notify_all();
+      S->cv_svc.notify_all();  // a stopping service thread waits for the last call
+    }
   }
 };
 
@@ -609,7 +616,7 @@ std::unique_ptr<Req> submit(wc_service* S, uint32_t sides, const wc_config* cfg,
       return q;
     }
     S->cv_arena.wait(lk, [&] { return S->stop || arena_alloc(S, total, q->aoff); });
-    if (S->stop) {  // (the in-flight count keeps the service alive: the request still completes)
+    if (S->stop) {  // (the service thread runs until inflight is 0: the request still completes)
       lk.unlock();
       queue_fallback(S, q.get(), p);
       return q;

@@ -105,12 +105,14 @@ def priority_consensus_batch(problems, config=None, context=None, return_errors=
         L.wc_results_free(res)
 
 
-def priority_service_call(problem, config):
+def priority_service_call(problem, config, svc=None):
     """One PriorityConsensusDWFA::consensus through the device's submission
     service (wc_service_priority_consensus): this thread unwinds the LIFO
     stack, the sub-problems share the service's persistent launches with every
-    other caller. None when the device has no service."""
-    svc = _lib.service()
+    other caller. None when the device has no service. `svc`: a given
+    _lib.Service instead of the process-wide one."""
+    if svc is None:
+        svc = _lib.service()
     if svc is None:
         return None
     L = _lib.lib()
