@@ -711,6 +711,21 @@ class Cfg4(Cfg5):
         self.busy_s = self.static_s = time.perf_counter() - t0
         return st, 1
 
+    def cpu(self, threads, target_s):
+        """The C++ oracle on the same locus, one thread (about two minutes),
+        checked against the GPU's result."""
+        o = orc()
+        t0 = time.perf_counter()
+        res, c = o.priority_consensus(self.L[0], counters=True, wildcard=ord("*"))
+        dt = time.perf_counter() - t0
+        g = self.last[0]
+        ok = ([[x.sequence() for x in ch] for ch in g.consensuses()] ==
+              [[x["sequence"] for x in ch] for ch in res["consensuses"]] and
+              list(g.sequence_indices()) == list(res["sequence_indices"]))
+        return {"value": c["updates"] / dt, "unit": "updates/s", "loci_per_s": 1.0 / dt, "seconds": dt, "cores": 1,
+                "sample": "the whole cfg4 locus, C++ oracle, one thread, %.1f s" % dt,
+                "gpu_matches_cpu_on_sample": ok}
+
     def config(self):
         return {"workload": "PriorityConsensusDWFA cfg4: one locus, 4 haplotypes x 50 reads x 8 kb, inserted "
                             "segments {0, 25, 60, 150} bp + 3 SNVs each, 0.5% error, wildcard '*'",
@@ -718,9 +733,6 @@ class Cfg4(Cfg5):
 
     def data(self):
         return "synthetic: synth.cfg4_locus(4 + rank)"
-
-    def cpu(self, threads, target_s):
-        return None  # the oracle needs ~2 min for this locus; measured separately
 
 
 class Cfg5Api:
@@ -1012,6 +1024,14 @@ def main():
         cfg5_leg["roofline"] = rl5
         if rank == 0 and tail["heaviest_latency_under_load_s"] is not None:
             cfg5_leg["tail"]["heaviest_latency_alone_s"] = C5.heaviest_alone(tail["heaviest_locus"])
+        if rank == 0 and world == 1 and tail["slowest_locus"] is not None and tail["slowest_locus"] >= 0:
+            # the critical path a larger GPU count cannot shorten: the slowest
+            # locus of the batch, alone; 8 GPUs cannot finish the batch before
+            # it, so t_1gpu / (8 x that) bounds the 8-GPU efficiency
+            alone = C5.heaviest_alone(tail["slowest_locus"])
+            cfg5_leg["tail"]["slowest_latency_alone_s"] = alone
+            crit = max(alone, cfg5_leg["tail"].get("heaviest_latency_alone_s") or 0.0)
+            cfg5_leg["tail"]["projected_8gpu_eff"] = min(1.0, el5 / (8.0 * crit)) if crit > 0 else None
         if rank == 0 and not a.no_cpu:
             # bounded oracle check of sampled loci (and, at N=1, the CPU baseline)
             cores, aff, quota = usable_cpus()

@@ -20,6 +20,10 @@ sys.path.insert(0, ROOT)
 PHASES = {0: "pop-broadcast", 1: "analyze", 2: "finalize", 3: "votes+select", 4: "clone-copy", 5: "push-thread",
           6: "push-heavy", 7: "heap-insert", 8: "chain-prepare", 9: "chain-walk", 10: "chain-votes",
           11: "chain-accept", 12: "votes-wave", 13: "pop-logic", 14: "chain-total"}
+# the one-wave dual engine's own counters (wave_dual.hip.hpp; 32..39 and 53..55)
+WAVE_SUB = {32: "hot-load-block", 33: "hot-loads", 34: "analysis-lanes", 35: "general-end-or-wide",
+            36: "general-weighted-or-odd-split", 37: "fast-pushes", 38: "votes", 39: "general-children",
+            53: "heavy-calls", 54: "heavy-cycles", 55: "heavy-items"}
 # the dual engine marks the same ids: 10 = activation, 11 = prune + cost
 DUAL_PHASES = dict(PHASES)
 DUAL_PHASES.update({10: "activate", 11: "prune+cost"})
@@ -103,9 +107,7 @@ def main():
                 24: "prune-atomics(t0)", 25: "prune-barrier1(t0)", 26: "prune-tail(t0)"}
         rep["dual_sub_per_pop"] = {DSUB[k]: round(cyc[k] / np_, 2) for k in DSUB if k < len(cyc)}
         # the one-wave dual engine (wave_dual.hip.hpp) uses 32..39 for its own timers
-        rep["wave_sub_per_pop"] = {nm: round(cyc[k] / np_, 2) for k, nm in (
-            (32, "hot-load-block"), (33, "hot-loads"), (34, "analysis-lanes"), (35, "analysis-aggregates"),
-            (36, "reached"), (37, "fast-pushes"), (38, "votes"), (39, "selection")) if k < len(cyc)}
+        rep["wave_sub_per_pop"] = {nm: round(cyc[k] / np_, 2) for k, nm in WAVE_SUB.items() if k < len(cyc)}
         if len(cyc) >= 40:  # chain statistics per kind (engine.hip dual chain call site)
             for kind, b in (("single_consensus_chains", 32), ("dual_chains", 35)):
                 n = max(1, cyc[b])

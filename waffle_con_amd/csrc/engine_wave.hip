@@ -9,5 +9,7 @@
 #define WC_ENGINE_NS wcw
 #define WC_BLOCK 64
 #define WC_WAVES_PER_EU 2
+#ifndef WC_DUAL_WAVES_PER_EU
 #define WC_DUAL_WAVES_PER_EU 2
+#endif
 #include "engine.hip"

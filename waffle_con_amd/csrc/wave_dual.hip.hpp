@@ -26,55 +26,32 @@
 // Problems with offsets (activation) run on the block engines (the host never
 // plans this build for them).
 
-// ---- the hot format: a slot RState with the frontier left uncompacted ----
-// word 3 = nscmp | live-slot mask << 16 | flags << 24 (slot RStates keep nf in
-// byte 2; a kWide or inactive read keeps its slot RState as it is)
-__device__ __forceinline__ RRaw hot_pack(const Front& f) {
-  RRaw s;
-  s.a = make_uint4(f.e, f.off, f.maxb, (f.nscmp & 0xFFFFu) | (f.mask << 16));
-  s.b = make_uint4(f.fi[0] | f.fi[1] << 16, f.fi[2] | f.fi[3] << 16, f.fi[4] | f.fi[5] << 16, f.fi[6] | f.fi[7] << 16);
-  s.c = make_uint4(f.fd[0], f.fd[1], f.fd[2], f.fd[3]);
-  s.d = make_uint4(f.fd[4], f.fd[5], f.fd[6], f.fd[7]);
-  return s;
-}
-__device__ __forceinline__ void hot_unpack(const RRaw& s, Front& f) {
-  front_load(s, f);
-  f.mask = (s.a.w >> 16) & 0xFFu;
-}
-// a slot RState (compacted: nf live slots) in the hot format
-__device__ __forceinline__ RRaw slot_to_hot(RRaw s) {
-  if (rraw_e(s) != kInactive && !(rraw_flags(s) & kWide)) {
-    const uint32_t nf = (s.a.w >> 16) & 0xFFu;
-    s.a.w = (s.a.w & 0xFF00FFFFu) | (((1u << nf) - 1u) << 16);
-  }
-  return s;
-}
-// and back (front_store compacts the live slots)
-__device__ __forceinline__ void hot_to_slot(Gm<RState>* p, const RRaw& s) {
-  if (rraw_e(s) != kInactive && !(rraw_flags(s) & kWide)) {
-    Front f;
-    hot_unpack(s, f);
-    front_store(p, f);
-  } else {
-    rstate_store(p, s);
-  }
-}
-
+// ---- the hot copy: the popped node's RStates (slot format) in LDS ----
+// Lds::hot[side * nmax + r] is authoritative while the node is hot: pushes
+// (front_store) and the ED-increase loops (wave_heavy's rebuild) write it
+// there; the slot gets it back (a raw copy) when another node is popped.
 // ---- tip bytes: the read byte behind every tip of a frontier ----
-// (thread_tips' x[k], packed: byte k of lo/hi, valid bit k; 0x100 = no tip)
+// (thread_tips' x[k] for the frontier as front_store compacts it: entry k is
+// the k-th live slot in ascending order; byte k of lo/hi, valid bit k)
 struct Tips {
   uint32_t lo, hi, valid;
 };
 __device__ __forceinline__ Tips tips_fetch(const Front& f, const Gm<uint8_t>* rd, uint32_t blen, uint32_t len) {
-  uint32_t x[kF];
-  thread_tips(f, GlobalBytes{rd}, blen, len, x);
   Tips t = {0, 0, 0};
+  uint32_t rank = 0;
+  const uint32_t hi = f.mask ? 32u - (uint32_t)__builtin_clz(f.mask) : 0u;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
-    if (x[k] == 0x100u) continue;
-    t.valid |= 1u << k;
-    if (k < 4) t.lo |= (x[k] & 0xFFu) << (8 * k);
-    else t.hi |= (x[k] & 0xFFu) << (8 * (k - 4));
+    if ((uint32_t)k >= hi) break;
+    if (!(f.mask & (1u << k))) continue;
+    const uint32_t bo = f.fd[k] + f.e - f.fi[k];
+    if (f.fd[k] + f.off == len && bo < blen) {
+      const uint32_t b = rd[bo];
+      t.valid |= 1u << rank;
+      if (rank < 4) t.lo |= b << (8 * rank);
+      else t.hi |= b << (8 * (rank - 4));
+    }
+    rank++;
   }
   return t;
 }
@@ -144,8 +121,8 @@ __device__ __forceinline__ void hot_writeback(Eng& E, uint32_t slot, bool dual) 
   for (int j = 0; j < R; ++j) {
     const uint32_t r = (uint32_t)lane + 64u * j;
     if (r >= E.n) continue;
-    hot_to_slot(&E.sv(slot, 0).rs[r], rstate_load(&E.L.hot[r]));
-    if (dual) hot_to_slot(&E.sv(slot, 1).rs[r], rstate_load(&E.L.hot[E.nmax + r]));
+    rstate_store(&E.sv(slot, 0).rs[r], rstate_load(&E.L.hot[r]));
+    if (dual) rstate_store(&E.sv(slot, 1).rs[r], rstate_load(&E.L.hot[E.nmax + r]));
   }
 }
 template <int R>
@@ -158,8 +135,8 @@ __device__ __forceinline__ void hot_fetch_slot(Eng& E, uint32_t slot, bool dual)
     const RRaw a = rstate_load(&E.sv(slot, 0).rs[r]);
     RRaw b = a;
     if (dual) b = rstate_load(&E.sv(slot, 1).rs[r]);
-    rstate_store(&E.L.hot[r], slot_to_hot(a));
-    if (dual) rstate_store(&E.L.hot[E.nmax + r], slot_to_hot(b));
+    rstate_store(&E.L.hot[r], a);
+    if (dual) rstate_store(&E.L.hot[E.nmax + r], b);
   }
 }
 
@@ -167,7 +144,7 @@ __device__ __forceinline__ void hot_fetch_slot(Eng& E, uint32_t slot, bool dual)
 // register allocation does not carry theirs. The callee rebuilds the engine
 // context from the kernel arguments (callee_eng); the hot area is the carve's
 // start, so sbase = Lds::hot. ----
-enum : uint32_t { WR_GENERAL_POP = 0, WR_GENERAL_VOTES = 1, WR_HEAVY = 2 };
+enum : uint32_t { WR_GENERAL_POP = 0, WR_VOTES_SELECT = 1, WR_HEAVY = 2, WR_CHILDREN = 3 };
 
 // dual_main's thread-0 selection (dual_consensus.rs:520-734): thresholds from
 // the votes in ctl.keys/vals, then the children in the reference's order
@@ -268,8 +245,7 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
   const uint32_t n = E.n;
   if (op == WR_HEAVY) {
     // the ED-increase loops (and wide frontiers) of the in-place push: one
-    // read per wave, through the slot; the rebuilt RState goes back to the
-    // hot copy
+    // read per wave, on the hot copy (the rows are the slot's)
     const uint32_t nl[2] = {a0, a1};
     const int sy[2] = {(int32_t)a2, (int32_t)a3};
     const uint32_t nh = uni(ctl.nheavy);
@@ -279,30 +255,48 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
       const uint32_t sd = it >= n ? 1u : 0u, r = it - sd * n;
       SideView v = E.sv(top, sd);
       uint32_t e = 0;
-      const bool ok = wave_heavy(&v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con, nl[sd],
-                                 (uint8_t)sy[sd], cfg.wildcard, early, E.wcap, cnt, e);
-      __threadfence_block();
+      const bool ok = wave_heavy(&E.L.hot[sd * E.nmax + r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
+                                 nl[sd], (uint8_t)sy[sd], cfg.wildcard, early, E.wcap, cnt, e);
       __builtin_amdgcn_wave_barrier();
-      if (!ok) {
-        if (lane == 0) atomicOr(&ctl.ovf, 4u);
-        continue;
-      }
-      if (lane == 0) rstate_store(&E.L.hot[sd * E.nmax + r], slot_to_hot(rstate_load(&v.rs[r])));
+      if (!ok && lane == 0) atomicOr(&ctl.ovf, 4u);
     }
     flush_counters(ctl, cnt);
     __syncthreads();
     return;
   }
+  const SlotMeta tm = meta_get(E.L.meta[top]);
+  Sh<RInfo>* R0 = E.L.rinfo;
+  Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
+  if (op == WR_VOTES_SELECT) {
+    // the votes from the pop's RInfo (weighted, or splits that round, or
+    // several children to order) and dual_main's selection; the caller
+    // builds a single in-place child itself
+    for (uint32_t side = 0; side < (tdual ? 2u : 1u); ++side) {
+      const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, n, weighted, tdual, ctl.multi[side] != 0,
+                                 cfg.wildcard);
+      if (!ok && lane == 0) atomicOr(&ctl.ovf, (uint32_t)LIM_VOTES);
+    }
+    __syncthreads();
+    if (tid == 0) wave_select_t0(cfg, ctl, tm, tdual);
+    __syncthreads();
+    return;
+  }
   // the rest of the pop with the block engines' code (dual_main), from the
   // slot: the hot node goes back there first and is dropped
-  const SlotMeta tm = meta_get(E.L.meta[top]);
   const uint32_t tlens[2] = {tm.len[0], tm.len[1]};
   hot_writeback<R>(E, top, tdual);
   __threadfence_block();
   if (tid == 0) ctl.hot_slot = kNoSlot;
   __syncthreads();
-  Sh<RInfo>* R0 = E.L.rinfo;
-  Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
+  if (op == WR_CHILDREN) {  // after WR_VOTES_SELECT: several children, or an activate_dual split
+    if (tlens[0] + 1 > E.lcap || tlens[1] + 1 > E.lcap) {
+      if (tid == 0) ctl.status = ST_RETRY | ST_RETRY_LCAP;
+      __syncthreads();
+      return;
+    }
+    dual_build_children<false>(E, ctl, top, tm, tdual, uni(ctl.nchild));
+    return;
+  }
   if (op == WR_GENERAL_POP) {
     const uint64_t full_min = (uint64_t)a0 | (uint64_t)a1 << 32;
     const uint32_t oslot = a2;
@@ -391,11 +385,8 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
   __syncthreads();
   if (uni(ctl.status) != ST_OK) return;
   const uint32_t nc = uni(ctl.nchild);
-  if (nc == 0) {
-    if (tid == 0) {
-      E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top;
-      ctl.action = 3;  // no child (the main loop pushes nothing)
-    }
+  if (nc == 0) {  // no child: the slot is free (the main loop pushes nothing)
+    if (tid == 0) E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top;
     __syncthreads();
     return;
   }
@@ -409,93 +400,251 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
 
 // per-lane read pointers and lengths of the claimed problem (read lane + 64 j)
 template <int R>
-struct LaneReads {
+struct LaneReads {  // (R <= 2)
   const Gm<uint8_t>* rd[R];
   uint32_t bl[R];
 };
 
+// ---- register-resident search control ----
+// The pop loop keeps the search control (heap size, free-stack top, the
+// trackers' totals and thresholds, the work counters) in uniform registers:
+// in LDS, thread 0 read and wrote each of them with a full LDS round trip, one
+// after the other. The general path (wave_rare) still reads Ctl, so the
+// fields it uses are synced around each call.
+struct WCtl {
+  uint32_t heap_n, nfree, hot, hot_dual, am_len, n_ret, status;
+  uint64_t max_err;
+  uint64_t far[2], lastc[2], total[2], thr[2];
+  uint64_t pops, explored, ignored, peakq, updates, w_out, compares;
+};
+__device__ __forceinline__ void wctl_to_ctl(const WCtl& W, Lo<Ctl>& ctl) {
+  if (threadIdx.x == 0) {
+    ctl.nfree = W.nfree;
+    ctl.n_ret = W.n_ret;
+    ctl.max_err = W.max_err;
+    ctl.status = W.status;
+    ctl.hot_slot = W.hot;
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void wctl_from_ctl(WCtl& W, Lo<Ctl>& ctl) {
+  W.nfree = uni(ctl.nfree);
+  W.n_ret = uni(ctl.n_ret);
+  W.max_err = ((uint64_t)uni((uint32_t)(ctl.max_err >> 32)) << 32) | uni((uint32_t)ctl.max_err);
+  W.status = uni(ctl.status);
+  W.hot = uni(ctl.hot_slot);
+}
+// priority-queue 1.x on the LDS heap with the size in a register: the
+// reference's sift rules (strict comparisons), with the
+// path's entries compared by lanes in parallel instead of one level at a time.
+__device__ __forceinline__ HeapEntry heap_uni(const HeapEntry& e);
+__device__ __forceinline__ uint64_t heap_cost(const HeapEntry& e) { return e.cost; }
+// push (sift-up): e enters at position n and moves up while its parent has a
+// lower priority. The ancestors' priorities never decrease going up (the heap
+// property), so the ancestors e passes are exactly a prefix of the path: lane
+// k reads ancestor k + 1 levels up, one ballot finds how many e passes, and
+// those move one level down in one parallel store.
+__device__ __forceinline__ void wheap_push(Sh<HeapEntry>* h, uint32_t n, HeapEntry e) {
+  const uint32_t lane = (uint32_t)lane_id();
+  const uint32_t depth = 31u - (uint32_t)__builtin_clz(n + 1);  // ancestors of position n
+  bool less = false;
+  uint32_t child = 0;
+  HeapEntry a{};
+  if (lane < depth) {
+    const uint32_t anc = ((n + 1) >> (lane + 1)) - 1;
+    child = ((n + 1) >> lane) - 1;
+    a = h[anc];
+    less = prio_less(a, e);
+  }
+  const uint64_t m = ballot(less);
+  const uint32_t k = (uint32_t)__builtin_ctzll(~m);  // ancestors e moves past
+  if (lane < k) h[child] = a;
+  if (lane == 0) h[((n + 1) >> k) - 1] = e;
+}
+// pop: the root leaves, the last entry x (at position n after the pop) sifts
+// down from the root. At node i the larger child (left on ties) takes i's
+// place while x has a lower priority than it. Lanes compute that decision
+// for the nodes of the top levels in parallel; the path is then a walk over
+// two ballot masks, and the entries on it move up in one parallel store.
+// Below the top levels (heaps of more than 63 entries) the walk goes on
+// level by level.
+__device__ __forceinline__ HeapEntry wheap_pop(Sh<HeapEntry>* h, uint32_t n) {
+  const uint32_t lane = (uint32_t)lane_id();
+  const HeapEntry top = heap_uni(h[0]);
+  const HeapEntry x = heap_uni(h[n]);
+  if (n <= 1) {
+    if (lane == 0) h[0] = x;
+    return top;
+  }
+  // node `lane` of the top 63: its larger child and whether x moves past it
+  bool go = false, right = false;
+  HeapEntry cm{};
+  {
+    const uint32_t l = 2 * lane + 1, r = 2 * lane + 2;
+    if (lane < 63 && l < n) {
+      const HeapEntry hl = h[l];
+      cm = hl;
+      if (r < n) {
+        const HeapEntry hr = h[r];
+        if (prio_less(hl, hr)) {
+          right = true;
+          cm = hr;
+        }
+      }
+      go = prio_less(x, cm);
+    }
+  }
+  const uint64_t gm = ballot(go), rm = ballot(right);
+  uint64_t path = 0;  // nodes (< 64) whose entry is replaced by their larger child's
+  uint32_t i = 0;
+  while (i < 63 && ((gm >> i) & 1ull)) {
+    path |= 1ull << i;
+    i = 2 * i + 1 + (uint32_t)((rm >> i) & 1ull);
+  }
+  if ((path >> lane) & 1ull) h[lane] = cm;
+  if (i >= 63) {
+    // deeper levels, one at a time (x is still moving)
+    for (;;) {
+      const uint32_t l = 2 * i + 1, r = 2 * i + 2;
+      uint32_t largest = i;
+      HeapEntry best = x;
+      if (l < n) {
+        const HeapEntry hl = heap_uni(h[l]);
+        const HeapEntry hr = heap_uni(h[r < n ? r : l]);
+        if (prio_less(best, hl)) {
+          largest = l;
+          best = hl;
+        }
+        if (r < n && prio_less(best, hr)) {
+          largest = r;
+          best = hr;
+        }
+      }
+      if (largest == i) break;
+      if (lane == 0) h[i] = best;
+      i = largest;
+    }
+  }
+  if (lane == 0) h[i] = x;
+  return top;
+}
+__device__ __forceinline__ HeapEntry heap_uni(const HeapEntry& e) {
+  HeapEntry u;
+  u.cost = ((uint64_t)uni((uint32_t)(e.cost >> 32)) << 32) | uni((uint32_t)e.cost);
+  u.len = uni(e.len);
+  u.slot = uni(e.slot);
+  return u;
+}
+
 // ---- the in-place child of a one-child pop (dual_build_children for nc == 1,
-// no activate_dual): pushes on the hot state, ED increases through the slot,
-// prune + cost + Some counts in one lane pass; new tip bytes into tx ----
+// no activate_dual): pushes on the hot state, ED increases through the slot
+// (out of line), prune + cost + Some counts in one lane pass; new tip bytes
+// into tx. Returns the child's cost; its metadata goes to the slot. ----
 template <int R>
-__device__ __forceinline__ void wave_push_inplace(Eng& E, Lo<Ctl>& ctl, KArgs kp, uint32_t top, const SlotMeta& tm,
-                                                  bool tdual, const LaneReads<R>& lr, Tips (&tx)[R][2]) {
-  const int tid = threadIdx.x, lane = lane_id();
+__device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs kp, WCtl& W, uint32_t top,
+                                                   const SlotMeta& tm, bool tdual, uint32_t kind, const int (&sy)[2],
+                                                   const LaneReads<R>& lr, Tips (&tx)[R][2], uint32_t (&nl)[2]) {
+  const int lane = lane_id();
   const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
   const uint32_t n = E.n;
-  if (tid == 0) {
-    ctl.ch_slot[0] = top;
-    ctl.ch_cost[0] = 0;
-    SlotMeta m = tm;
-    const uint32_t kind = ctl.ch_kind[0];
+  // the child's symbols, locks and lengths (the metadata goes out with its
+  // Some counts below)
+  SlotMeta m = tm;
 #pragma unroll
-    for (int sd = 0; sd < 2; ++sd) {
-      const int sym = ctl.ch_s[0][sd];
-      if (sym >= 0) {
-        E.sv(top, sd).con[WC_IX(m.len[sd], E.lcap)] = (uint8_t)sym;
-        m.len[sd]++;
-      } else if (kind == 0) {
-        m.flags |= (sd == 0 ? 2u : 4u);  // lock_sequence
-      }
+  for (int sd = 0; sd < 2; ++sd) {
+    if (sy[sd] >= 0) {
+      if (lane == 0) E.sv(top, sd).con[WC_IX(m.len[sd], E.lcap)] = (uint8_t)sy[sd];
+      m.len[sd]++;
+    } else if (kind == 0) {
+      m.flags |= (sd == 0 ? 2u : 4u);  // lock_sequence
     }
-    meta_put(E.L.meta[top], m);
-    ctl.nheavy = 0;
   }
-  __syncthreads();
-  PH_MARK(4);
-  const int sy[2] = {uni((int32_t)ctl.ch_s[0][0]), uni((int32_t)ctl.ch_s[0][1])};
-  const uint32_t nl[2] = {uni(E.L.meta[top].len[0]), uni(E.L.meta[top].len[1])};
-  WaveCounters tc = {0, 0, 0, 0, 0, 0};
-  uint32_t refetch = 0;  // bit 2j+sd: tips to fetch after the heavy pass
+  nl[0] = m.len[0];
+  nl[1] = m.len[1];
+  uint32_t upd = 0, wout = 0, cmps = 0, nheavy = 0;
+  uint32_t ee[R][2];  // the child's edit distances (kInactive = None)
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const uint32_t r = (uint32_t)lane + 64u * j;
     const bool live = r < n;
-    const Gm<uint8_t>* rd = lr.rd[j];
-    const uint32_t blen = lr.bl[j];
 #pragma unroll
     for (int sd = 0; sd < 2; ++sd) {
       bool heavy = false;
-      if (live && (sd == 0 || tdual) && sy[sd] >= 0) {
+      ee[j][sd] = kInactive;
+      if (live && (sd == 0 || tdual)) {
         Sh<RState>* hp = &E.L.hot[sd * E.nmax + r];
         const RRaw s = rstate_load(hp);
-        if (rraw_e(s) != kInactive) {
+        ee[j][sd] = rraw_e(s);
+        if (rraw_e(s) != kInactive && sy[sd] >= 0) {
           if (rraw_flags(s) & kWide) {
-            heavy = true;  // the slot's RState is current (a wide read's hot copy is the slot's)
+            heavy = true;  // (wave_heavy's full-scan push)
           } else {
             Front f;
-            hot_unpack(s, f);
+            front_load(s, f);
             uint32_t x[kF];
             tips_unpack(tx[j][sd], x);
             uint32_t cmp = 0;
-            SideView v = E.sv(top, sd);
-            heavy = thread_apply(f, x, blen, nl[sd] - 1, (uint8_t)sy[sd], cfg.wildcard, early,
-                                 v.wf + (uint64_t)r * E.wcap, cmp);
-            tc.compares += cmp;
-            if (heavy) {
-              front_store(&v.rs[r], f);  // the ED-increase loop reads it from the slot
-            } else {
-              rstate_store(hp, hot_pack(f));
-              tc.updates++;
-              tc.w_out += 2 * f.e + 1;
-              tx[j][sd] = tips_fetch(f, rd, blen, nl[sd]);
+            heavy = thread_apply(f, x, lr.bl[j], nl[sd] - 1, (uint8_t)sy[sd], cfg.wildcard, early,
+                                 E.sv(top, sd).wf + (uint64_t)r * E.wcap, cmp);
+            cmps += cmp;
+            front_store(hp, f);  // (a heavy read's ED-increase loop goes on from it)
+            if (!heavy) {
+              upd++;
+              wout += 2 * f.e + 1;
+              ee[j][sd] = f.e;
+              tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], nl[sd]);
             }
           }
         }
       }
-      if (heavy) refetch |= 1u << (2 * j + sd);
-      const uint32_t k = agg_append(&ctl.nheavy, heavy);
-      if (heavy) E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))] = sd * n + r;
+      // heavy items into the work list (ballot prefix, no atomics)
+      const uint64_t hm = ballot(heavy);
+      if (heavy) {
+        const uint32_t k = nheavy + (uint32_t)__popcll((unsigned long long)(hm & ((1ull << lane) - 1ull)));
+        E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))] = sd * n + r;
+      }
+      nheavy += (uint32_t)__popcll((unsigned long long)hm);
     }
   }
-  flush_thread_counters(ctl, tc);
-  __syncthreads();
-  PH_MARK(5);
-  if (uni(ctl.nheavy))
+  W.updates += wave_sum_u32(upd);
+  W.w_out += wave_sum_u32(wout);
+  W.compares += wave_sum_u32(cmps);
+  if (nheavy) {
+    // the ED-increase loops, out of line; then the rebuilt states and their
+    // tip bytes from the hot copy
+    SUB_CNT(53, 1);
+    SUB_CNT(55, nheavy);
+    SUB_T0(t_hv);
+    if (lane == 0) {
+      ctl.nheavy = nheavy;
+      ctl.ovf = 0;
+    }
+    __syncthreads();
     wave_rare<R>(kp, E.P, (Sh<uint8_t>*)E.L.hot, ctl, WR_HEAVY, top, tdual, nl[0], nl[1], (uint32_t)sy[0],
                  (uint32_t)sy[1], 0);
-  PH_MARK(6);
+    SUB_T1(54, t_hv);
+    const uint32_t ovf = uni(ctl.ovf);
+    if (ovf & 16u) W.status = WC_E_INVARIANT_CODE;
+    else if (ovf & 4u) W.status = ST_RETRY | ST_RETRY_WCAP;
+    else if (ovf) W.status = limit_status(ovf);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t r = (uint32_t)lane + 64u * j;
+      if (r >= n) continue;
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        if ((sd == 1 && !tdual) || sy[sd] < 0) continue;
+        const RRaw s = rstate_load(&E.L.hot[sd * E.nmax + r]);
+        if (ee[j][sd] == rraw_e(s) && ee[j][sd] != kInactive && !(rraw_flags(s) & kWide)) continue;
+        ee[j][sd] = rraw_e(s);
+        if (rraw_e(s) == kInactive || (rraw_flags(s) & kWide)) continue;
+        Front f;
+        front_load(s, f);
+        tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], nl[sd]);
+      }
+    }
+  }
   // prune_dwfa (:1030-1045) of a dual child, then per read the cheaper side's
   // cost (strict <: ties keep consensus 1, :1092-1131) and the Some counts
   uint64_t cost = 0;
@@ -504,16 +653,14 @@ __device__ __forceinline__ void wave_push_inplace(Eng& E, Lo<Ctl>& ctl, KArgs kp
   for (int j = 0; j < R; ++j) {
     const uint32_t r = (uint32_t)lane + 64u * j;
     if (r >= n) continue;
-    Sh<RState>* h0 = &E.L.hot[r];
-    Sh<RState>* h1 = &E.L.hot[E.nmax + r];
-    uint32_t e1 = h0->e;
-    uint32_t e2 = tdual ? h1->e : kInactive;
+    uint32_t e1 = ee[j][0];
+    uint32_t e2 = tdual ? ee[j][1] : kInactive;
     if (tdual && e1 != kInactive && e2 != kInactive) {
       if ((uint64_t)e1 + cfg.dual_max_ed_delta < (uint64_t)e2) {
-        h1->e = kInactive;
+        E.L.hot[E.nmax + r].e = kInactive;
         e2 = kInactive;
       } else if ((uint64_t)e2 + cfg.dual_max_ed_delta < (uint64_t)e1) {
-        h0->e = kInactive;
+        E.L.hot[r].e = kInactive;
         e1 = kInactive;
       }
     }
@@ -523,42 +670,188 @@ __device__ __forceinline__ void wave_push_inplace(Eng& E, Lo<Ctl>& ctl, KArgs kp
     if (best != ~0ull) cost += best;
     c0 += e1 != kInactive;
     c1 += e2 != kInactive;
-    // tips of the reads that went through the ED-increase loop
-#pragma unroll
-    for (int sd = 0; sd < 2; ++sd) {
-      if (!((refetch >> (2 * j + sd)) & 1u)) continue;
-      const RRaw s = rstate_load(sd ? h1 : h0);
-      if (rraw_e(s) == kInactive || (rraw_flags(s) & kWide)) continue;
-      Front f;
-      hot_unpack(s, f);
-      tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], nl[sd]);
-    }
   }
   cost = wave_sum_u64(cost);
-  c0 = wave_sum_u32(c0);
-  c1 = wave_sum_u32(c1);
-  if (tid == 0) {
-    if (ctl.ovf & 16u) ctl.status = WC_E_INVARIANT_CODE;
-    else if (ctl.ovf & 4u) ctl.status = ST_RETRY | ST_RETRY_WCAP;
-    else if (ctl.ovf) ctl.status = limit_status(ctl.ovf);
-    auto& m = E.L.meta[top];
-    m.nsome[0] = c0;
-    m.nsome[1] = c1;
-    ctl.ch_cost[0] = cost;
-    ctl.ch_len[0] = max(nl[0], nl[1]);
+  m.nsome[0] = wave_sum_u32(c0);
+  m.nsome[1] = wave_sum_u32(c1);
+  if (lane == 0) meta_put(E.L.meta[top], m);
+  return cost;
+}
+
+// per-lane multi-symbol nominations (read lane + 64 j) for the exact votes
+struct MultiNom {
+  uint32_t lo, hi;  // symbols (bytes, iteration order)
+  uint32_t occ_lo, occ_hi;  // their occurrences (bytes)
+  uint32_t split;
+};
+
+// the vote of key `key` on one side in eighths: 8 per single-symbol voter,
+// occ * 8 / split per multi-symbol voter (split in {1, 2, 4, 8})
+template <int R>
+__device__ __forceinline__ uint32_t votes8(uint32_t key, const uint32_t (&ys)[R], const uint64_t (&mmask)[R],
+                                           const MultiNom (&mn)[R]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    c += 8u * (uint32_t)__popcll((unsigned long long)ballot(ys[j] == key));
+    uint64_t mm = mmask[j];
+    while (mm) {
+      const int l = __builtin_ctzll(mm);
+      mm &= mm - 1;
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].lo, l);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].hi, l);
+      const uint32_t olo = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].occ_lo, l);
+      const uint32_t ohi = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].occ_hi, l);
+      const uint32_t split = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].split, l);
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t sk = ((k < 4 ? lo : hi) >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t ok = ((k < 4 ? olo : ohi) >> (8 * (k & 3))) & 0xFFu;
+        if (ok && sk == key) c += ok * (8u / split);
+      }
+    }
   }
-  __syncthreads();
-  PH_MARK(11);
+  return c;
+}
+
+// ---- the votes of one node side on the lean path (consensus.rs:540-564,
+// dual_consensus.rs:1242-1290): the keys (the wildcard dropped when it is not
+// the only one, :556-561) with their votes in exact eighths, their sum and
+// maximum, the threshold min(max(min_count, ceil(min_af * sum)), max)
+// (:520-552), and the keys passing it. With one child the order of the keys
+// (hashbrown) decides nothing, so none is computed. ----
+struct SideVotes {
+  uint32_t npass, nkeys;  // keys passing the threshold, keys
+  int pk;                 // a passing key (the one, when npass == 1)
+  bool split;             // single-consensus node: two candidates pass min_count (split children)
+};
+template <int R>
+__device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const uint32_t (&ys)[R],
+                                                     const uint64_t (&mmask)[R], const MultiNom (&mn)[R]) {
+  const int wc = cfg.wildcard;
+  uint32_t nk = 0, total8 = 0, mx_all = 0, mx_nowc = 0, wc8 = 0;
+  bool wc_in = false, drop = false;
+  uint32_t np = 0, ns = 0, npmc = 0;
+  int pk = -1;
+  uint64_t mc = 0;
+  double thr = 0.0;
+  uint32_t nko = 0;
+  // the common case: every voter nominates one symbol, the same one
+  {
+    uint64_t vm[R], any = 0, mm = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      vm[j] = ballot(ys[j] != 0x100u);
+      any |= vm[j];
+      mm |= mmask[j];
+    }
+    if (!mm) {
+      if (!any) {  // no key: no option but None; thr (unused) from min_count
+        return SideVotes{0, 0, -1, false};
+      }
+      uint32_t first = 0x100u;
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (first == 0x100u && vm[j]) first = (uint32_t)__builtin_amdgcn_readlane((int)ys[j], __builtin_ctzll(vm[j]));
+      bool same = true;
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        same = same && ballot(ys[j] == first) == vm[j];
+        cnt += (uint32_t)__popcll((unsigned long long)vm[j]);
+      }
+      if (same) {
+        // one key, not dropped (it is the only one); it passes min(mc, its own count)
+        return SideVotes{1, 1, (int)first, false};
+      }
+    }
+  }
+  // two passes over the distinct keys (single-symbol voters by ballots, then
+  // the symbols of multi-symbol voters not seen yet): sums, then the threshold
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    SymSet seen = {0, 0, 0, 0};
+    uint64_t rem[R], mrem[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      rem[j] = ballot(ys[j] != 0x100u);
+      mrem[j] = mmask[j];
+    }
+    uint32_t mk = 0;  // next symbol index within the current multi-symbol lane
+    for (;;) {
+      uint32_t key = 0x100u;
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (key == 0x100u && rem[j]) key = (uint32_t)__builtin_amdgcn_readlane((int)ys[j], __builtin_ctzll(rem[j]));
+      if (key == 0x100u) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          while (key == 0x100u && mrem[j]) {
+            const int l = __builtin_ctzll(mrem[j]);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].lo, l);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].hi, l);
+            const uint32_t olo = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].occ_lo, l);
+            const uint32_t ohi = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].occ_hi, l);
+            for (; mk < 8 && key == 0x100u; ++mk) {
+              const uint32_t ok = ((mk < 4 ? olo : ohi) >> (8 * (mk & 3))) & 0xFFu;
+              const uint32_t sk = ((mk < 4 ? lo : hi) >> (8 * (mk & 3))) & 0xFFu;
+              if (ok && !seen.has(sk)) key = sk;
+            }
+            if (mk >= 8) {
+              mrem[j] &= mrem[j] - 1;
+              mk = 0;
+            }
+          }
+        }
+      }
+      if (key == 0x100u) break;
+      seen.add(key);
+#pragma unroll
+      for (int j = 0; j < R; ++j) rem[j] &= ~ballot(ys[j] == key);
+      const uint32_t c8 = votes8<R>(key, ys, mmask, mn);
+      const bool is_wc = wc >= 0 && key == (uint32_t)(uint8_t)wc;
+      if (pass == 0) {
+        nk++;
+        total8 += c8;
+        mx_all = max(mx_all, c8);
+        if (is_wc) {
+          wc_in = true;
+          wc8 = c8;
+        } else {
+          mx_nowc = max(mx_nowc, c8);
+        }
+      } else {
+        if (drop && is_wc) continue;
+        if (!((double)c8 * 0.125 < thr)) {
+          np++;
+          pk = (int)key;
+        }
+        if (!is_wc) {
+          ns++;
+          if ((double)c8 * 0.125 >= (double)mc) npmc++;
+        }
+      }
+    }
+    if (pass == 0) {
+      drop = wc_in && nk > 1;
+      nko = drop ? nk - 1 : nk;
+      const uint32_t sum8 = drop ? total8 - wc8 : total8;
+      const uint32_t mx8 = drop ? mx_nowc : mx_all;
+      mc = max(cfg.min_count, ceil_u64(cfg.min_af * ((double)sum8 * 0.125)));
+      thr = nko ? fmin((double)mc, (double)mx8 * 0.125) : (double)mc;
+    }
+  }
+  return SideVotes{np, nko, pk, npmc > 1 && ns > 1};
 }
 
 // ---- the search: dual_main's pop, with a lean path for the common pop ----
-// The common pop (no read at a consensus end, no wide frontier, every read
-// nominating at most one symbol, unweighted votes, and exactly one child that
-// pushes in place) runs below: analysis on the hot state and prefetched tip
-// bytes, the votes as ballot counts (exact integers), the selection on those
-// counts (with one child the hashbrown order of the keys decides nothing), the
-// lane push. Anything else goes to wave_rare's WR_GENERAL*, which runs the
-// block engines' code for the rest of the pop.
+// The common pop (no read at a consensus end, no wide frontier, unweighted
+// votes whose per-read splits are 1, 2, 4 or 8 tips, and exactly one child
+// that pushes in place) runs below with the search control in registers:
+// analysis on the hot state and prefetched tip bytes, the votes as exact
+// counts of eighths (ballots), the selection on them (with one child the
+// hashbrown order of the keys decides nothing), the lane push. Anything else
+// goes to wave_rare's WR_GENERAL*, the block engines' code for the rest of
+// the pop.
 template <int R>
 __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* smem, Lo<Ctl>& ctl) {
   const int tid = threadIdx.x;
@@ -566,7 +859,6 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
   const DevConfig& cfg = A.cfg;
   const bool early = cfg.early != 0;
   const bool weighted = cfg.weighted != 0;
-  const int wc = cfg.wildcard;
   Eng E = make_eng(A, state_base(A, smem));
   Sh<RInfo>* R0 = E.L.rinfo;
   Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
@@ -582,7 +874,6 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
     E.n = E.P.n_reads;
     Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)oslot * A.out_stride;
     init_problem(E, ctl);
-    if (tid == 0) ctl.hot_prev_dual = 0;  // (here: the hot node has side 2)
     // what this build runs (the host plans it so): no offsets, <= 64 R reads
     if (E.n > 64u * R || E.P.max_act != 0 || E.P.n_active != E.n) {
       if (tid == 0) ctl.status = WC_E_INVARIANT_CODE;
@@ -591,97 +882,104 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
       continue;
     }
     const uint64_t full_min = max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.n));
+    // active_min_count (:497-513) without activations: the root's count at
+    // every length below am_len
+    const uint64_t am0 = full_min;
     bool tips_ok = false;  // tx holds the hot node's tip bytes
+    // (written out: a loop here was not unrolled, which would leave lr in scratch)
     LaneReads<R> lr;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const uint32_t r = (uint32_t)lane + 64u * j;
-      lr.rd[j] = r < E.n ? E.read(r) : E.rbytes;
-      lr.bl[j] = r < E.n ? E.rlen(r) : 0u;
+    {
+      const uint32_t r0 = (uint32_t)lane;
+      lr.rd[0] = E.rbytes + (r0 < E.n ? E.roff[E.P.read_begin + r0] : 0ull);
+      lr.bl[0] = r0 < E.n ? E.rlenp[E.P.read_begin + r0] : 0u;
+      if constexpr (R > 1) {
+        const uint32_t r1 = (uint32_t)lane + 64u;
+        lr.rd[R - 1] = E.rbytes + (r1 < E.n ? E.roff[E.P.read_begin + r1] : 0ull);
+        lr.bl[R - 1] = r1 < E.n ? E.rlenp[E.P.read_begin + r1] : 0u;
+      }
     }
     const KArgs kp = kernel_args();
     Sh<uint8_t>* const sbase = (Sh<uint8_t>*)E.L.hot;
+    // init_problem left: the root in the heap and tracker 0, slot 0 taken
+    WCtl W;
+    W.heap_n = 1;
+    W.nfree = E.pcap - 1;
+    W.hot = kNoSlot;
+    W.hot_dual = 0;
+    W.am_len = 1;
+    W.n_ret = 0;
+    W.status = ST_OK;
+    W.max_err = ~0ull;
+    W.far[0] = W.far[1] = W.lastc[0] = W.lastc[1] = W.thr[0] = W.thr[1] = 0;
+    W.total[0] = 1;
+    W.total[1] = 0;
+    W.pops = W.explored = W.ignored = W.peakq = W.updates = W.w_out = W.compares = 0;
+    const uint64_t L2 = E.lcap + 2;
+    Gm<uint32_t>* const lc[2] = {E.trk, E.trk + 2 * L2};
+    Gm<uint32_t>* const pc[2] = {E.trk + L2, E.trk + 3 * L2};
+    const uint64_t cap = cfg.max_capacity_per_size;
 
     for (;;) {
       // ---- pop (dual_consensus.rs:340-397) ----
-      if (tid == 0) {
-        if (ctl.heap_n == 0) {
-          ctl.action = 2;
-        } else {
-          const uint32_t plen = E.L.heap[0].len;
-          const uint32_t pc_pre[2] = {E.tracker(ctl, 0).processed(plen), E.tracker(ctl, 1).processed(plen)};
-          const uint64_t am_pre = plen < ctl.am_len ? E.active_min[WC_IX(plen, E.lcap + 2)] : 0;
-          ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)ctl.heap_n);
-          ctl.cnt[S_POPS]++;
-          for (int k = 0; k < 2; ++k) {
-            TrackerRef t = E.tracker(ctl, k);
-            while ((ctl.trk_total[k] > cfg.max_queue_size || ctl.last_constraint[k] >= cfg.max_nodes_wo_constraint) &&
-                   ctl.trk_thr[k] < ctl.farthest[k]) {
-              t.increment_threshold();
-              ctl.last_constraint[k] = 0;
-            }
-          }
-          HeapEntry top = heap_pop(E.L.heap, ctl.heap_n, E.pcap);
-          const auto& m = E.L.meta[top.slot];
-          const uint32_t dual = m.flags & 1u;
-          TrackerRef t = E.tracker(ctl, dual);
-          t.remove(top.len);
-          ctl.top_slot = top.slot;
-          ctl.top_len = top.len;
-          ctl.top_cost = top.cost;
-          ctl.top_dual = dual;
-          const uint64_t am = am_pre;
-          const bool imbalanced = dual && (m.nsome[0] < am || m.nsome[1] < am);
-          if (top.len >= ctl.am_len) ctl.status = WC_E_INVARIANT_CODE;
-          const bool at_cap = pc_pre[dual] >= t.cap;
-          if (top.cost > ctl.max_err || top.len < ctl.trk_thr[dual] || at_cap || imbalanced) {
-            ctl.cnt[S_IGNORED]++;
-            E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top.slot;
-            if (top.slot == ctl.hot_slot) ctl.hot_slot = kNoSlot;  // its state is dropped with the slot
-            ctl.action = 1;
-          } else {
-            ctl.farthest[dual] = max(ctl.farthest[dual], (uint64_t)top.len);
-            ctl.last_constraint[dual]++;
-            t.process_unchecked(top.len);
-            ctl.cnt[S_EXPLORED]++;
-            ctl.action = 0;
-            // the popped node's state into the hot area, unless it is there
-            // (the in-place child of the previous pop); the previous hot node,
-            // still queued, goes back to its slot first
-            ctl.hot_prev = ctl.hot_slot;
-            ctl.hot_load = top.slot != ctl.hot_slot;
-          }
-          trace_pop(A, prob, top, dual | (ctl.action << 1) | (m.nsome[0] << 8) | (m.nsome[1] << 20), (uint32_t)am);
+      if (W.heap_n == 0) break;
+      const uint32_t plen = uni(E.L.heap[0].len);
+      // the processed counts of the top's length, loaded first (HBM, under
+      // one wait) while the threshold walks and the sift run
+      const uint32_t pc_pre0 = trk_load(&pc[0][WC_IX(plen, L2)]), pc_pre1 = trk_load(&pc[1][WC_IX(plen, L2)]);
+      const uint64_t am = plen < W.am_len ? am0 : 0;
+      W.peakq = max(W.peakq, (uint64_t)W.heap_n);
+      W.pops++;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        while ((W.total[k] > cfg.max_queue_size || W.lastc[k] >= cfg.max_nodes_wo_constraint) && W.thr[k] < W.far[k]) {
+          W.total[k] -= uni(trk_load(&lc[k][WC_IX(W.thr[k], L2)]));  // increment_threshold
+          W.thr[k]++;
+          W.lastc[k] = 0;
         }
-        ctl.n_end[0] = ctl.n_end[1] = 0;
-        ctl.multi[0] = ctl.multi[1] = 0;
-        ctl.n_either = 0;
-        ctl.nheavy = 0;
-        ctl.ovf = 0;
       }
-      __syncthreads();
+      W.heap_n--;
+      const HeapEntry top = wheap_pop(E.L.heap, W.heap_n);
+      const SlotMeta tm = meta_get(E.L.meta[top.slot]);
+      const uint32_t dual = uni(tm.flags) & 1u;
+      const uint32_t ns0 = uni(tm.nsome[0]), ns1 = uni(tm.nsome[1]);
+      // tracker(dual).remove(len)
+      if (lane == 0) atomicSub((uint32_t*)&lc[dual][WC_IX(top.len, L2)], 1u);
+      if (top.len >= W.thr[dual]) W.total[dual]--;
+      const bool imbalanced = dual && (ns0 < am || ns1 < am);
+      if (top.len >= W.am_len) W.status = WC_E_INVARIANT_CODE;
+      const bool at_cap = uni(dual ? pc_pre1 : pc_pre0) >= cap;
+      if (A.trace && lane == 0) {
+        const uint32_t act = (top.cost > W.max_err || top.len < W.thr[dual] || at_cap || imbalanced) ? 1u : 0u;
+        trace_pop(A, prob, top, dual | (act << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
+      }
+      if (top.cost > W.max_err || top.len < W.thr[dual] || at_cap || imbalanced) {
+        W.ignored++;
+        if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = top.slot;
+        W.nfree++;
+        if (top.slot == W.hot) W.hot = kNoSlot;  // its state is dropped with the slot
+        continue;
+      }
+      W.far[dual] = max(W.far[dual], (uint64_t)top.len);
+      W.lastc[dual]++;
+      if (lane == 0) atomicAdd((uint32_t*)&pc[dual][WC_IX(top.len, L2)], 1u);  // process_unchecked
+      W.explored++;
+      if (W.status != ST_OK) break;
       PH_MARK(13);
-      if (uni(ctl.action) == 2) break;
-      if (uni(ctl.action) == 1) continue;
-      if (uni(ctl.status) != ST_OK) break;
 
-      const uint32_t top = uni(ctl.top_slot);
-      const uint32_t tlen = uni(ctl.top_len);
-      const bool tdual = uni(ctl.top_dual) != 0;
-      const SlotMeta tm = meta_get(E.L.meta[top]);
-      const uint32_t tlens[2] = {tm.len[0], tm.len[1]};
+      const uint32_t topslot = top.slot;
+      const uint32_t tlen = top.len;
+      const bool tdual = dual != 0;
+      const uint32_t tlens[2] = {uni(tm.len[0]), uni(tm.len[1])};
+      const uint32_t tflags = uni(tm.flags);
       SUB_T0(t_hot);
-      if (uni(ctl.hot_load)) {
+      if (topslot != W.hot) {
         SUB_CNT(33, 1);
-        const uint32_t prev = uni(ctl.hot_prev);
-        if (prev != kNoSlot) hot_writeback<R>(E, prev, uni(ctl.hot_prev_dual) != 0);
-        hot_fetch_slot<R>(E, top, tdual);
+        // the previous hot node, still queued, goes back to its slot first
+        if (W.hot != kNoSlot) hot_writeback<R>(E, W.hot, W.hot_dual != 0);
+        hot_fetch_slot<R>(E, topslot, tdual);
         tips_ok = false;
-        if (tid == 0) {
-          ctl.hot_slot = top;
-          ctl.hot_prev_dual = tdual ? 1u : 0u;
-        }
-        __syncthreads();
+        W.hot = topslot;
+        W.hot_dual = tdual ? 1u : 0u;
       }
       SUB_T1(32, t_hot);
 
@@ -689,15 +987,18 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
       // prefetched tip bytes; the nominations also go to RInfo (the general
       // path reads them there) ----
       SUB_T0(t_an);
-      uint32_t ys[R][2];  // the read's one nominated symbol (0x100: none or not a voter)
-      bool any_wide = false, any_end = false, any_multi = false;
+      uint32_t ys[2][R];  // the read's one nominated symbol (0x100: none, several, or not a voter)
+      uint64_t mmask[2][R];  // lanes whose read nominates several symbols
+      MultiNom mn[2][R];
+      bool any_wide = false, any_end = false, any_multi = false, odd_split = false;
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         const uint32_t r = (uint32_t)lane + 64u * j;
         const bool live = r < E.n;
 #pragma unroll
         for (int sd = 0; sd < 2; ++sd) {
-          ys[j][sd] = 0x100u;
+          ys[sd][j] = 0x100u;
+          mn[sd][j] = MultiNom{0, 0, 0, 0, 1};
           bool wide = false, end = false, multi = false;
           if (live && (sd == 0 || tdual)) {
             Sh<RInfo>* out = (sd ? R1 : R0) + r;
@@ -710,7 +1011,7 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
               wide = true;
             } else {
               Front f;
-              hot_unpack(s, f);
+              front_load(s, f);
               if (!tips_ok) tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], tlens[sd]);
               uint32_t x[kF];
               tips_unpack(tx[j][sd], x);
@@ -718,126 +1019,64 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
               rinfo_store(out, o, f.e);
               end = o.end != 0;
               multi = o.n > 1;
-              if (o.n == 1) ys[j][sd] = byte_at(o.sym, 0);
+              if (o.n == 1) ys[sd][j] = byte_at(o.sym, 0);
+              if (multi) {
+                mn[sd][j] = MultiNom{(uint32_t)o.sym, (uint32_t)(o.sym >> 32), (uint32_t)o.occ,
+                                     (uint32_t)(o.occ >> 32), o.split};
+                if (o.split > 8u || (o.split & (o.split - 1u))) odd_split = true;
+              }
             }
           }
+          mmask[sd][j] = ballot(multi);
           any_wide |= ballot(wide) != 0;
           any_end |= ballot(end) != 0;
-          any_multi |= ballot(multi) != 0;
+          any_multi |= mmask[sd][j] != 0;
         }
       }
+      odd_split = ballot(odd_split) != 0;
       tips_ok = true;
       SUB_T1(34, t_an);
-      // ---- active_min_count growth (dual_consensus.rs:497-513; no activation
-      // in this build, so the count stays the root's) ----
-      if (tid == 0 && ctl.am_len == tlen + 1 && tlen + 1 < E.lcap + 2) {
-        const uint32_t nt = E.total_active[tlen];
-        E.total_active[tlen + 1] = nt;
-        E.active_min[tlen + 1] = (uint32_t)max(cfg.min_count, ceil_u64(cfg.min_af * (double)nt));
-        ctl.am_len++;
-      }
+      // active_min_count growth (:497-513): the count at every new length is
+      // the root's (no activation in this build)
+      if (W.am_len == tlen + 1 && tlen + 1 < E.lcap + 2) W.am_len++;
       PH_MARK(1);
+
+      uint32_t nchild = 2;  // (0 or 1: decided on the lean path)
+      int child[2] = {-1, -1};
+      uint32_t kind = tdual ? 0u : 1u;
+      uint32_t nc = 1;
+      uint64_t ccost = 0;
+      uint32_t clen = 0;
+      bool general = false;  // children from Ctl (the block engines' passes)
       if (any_wide || any_end) {
-        // wide frontiers (nominated from the row) or a read at a consensus
-        // end (finalize, reached_*): the general pop from its analysis on
-        wave_rare<R>(kp, E.P, sbase, ctl, WR_GENERAL_POP, top, tdual, (uint32_t)full_min, (uint32_t)(full_min >> 32),
-                     oslot, 0, 0);
+        // wide frontiers or a read at a consensus end (finalize, reached_*):
+        // the block engines' code for the rest of the pop, from the slot
+        SUB_CNT(35, 1);
+        if (lane == 0) {
+          ctl.n_end[0] = ctl.n_end[1] = 0;
+          ctl.n_either = 0;
+          ctl.nheavy = 0;
+          ctl.ovf = 0;
+          ctl.multi[0] = ctl.multi[1] = 0;
+        }
+        wctl_to_ctl(W, ctl);
+        wave_rare<R>(kp, E.P, sbase, ctl, WR_GENERAL_POP, topslot, tdual, (uint32_t)full_min,
+                     (uint32_t)(full_min >> 32), oslot, 0, 0);
+        wctl_from_ctl(W, ctl);
+        W.hot = kNoSlot;
+        if (W.status != ST_OK) break;
+        nc = uni(ctl.nchild);
+        general = true;
       } else {
-        // ---- votes (consensus.rs:540-564, dual_consensus.rs:1242-1290):
-        // every voter adds 1.0 to its one symbol, so each key's value is an
-        // exact count. Per side: the keys (wildcard dropped when it is not the
-        // only one, :556-561), their sum and maximum, the threshold
-        // min(max(min_count, ceil(min_af * sum)), max) (:520-552), the keys
-        // passing it ----
-        SUB_T0(t_v);
-        int child[2] = {-1, -1};
-        uint32_t nchild = 2;  // (anything but 0 or 1: the general path)
-        uint32_t kind = tdual ? 0u : 1u;
-        if (!any_multi && !weighted) {
-          uint32_t npass[2] = {0, 0}, nkeys[2] = {0, 0};
-          int pkey[2] = {-1, -1};
-          bool split = false;
-#pragma unroll
-          for (int sd = 0; sd < 2; ++sd) {
-            if (sd == 1 && !tdual) break;
-            // pass 1: distinct keys, their counts, sum and maximum
-            uint64_t rem[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) rem[j] = ballot(ys[j][sd] != 0x100u);
-            uint32_t nk = 0, total = 0, mx_all = 0, mx_nowc = 0, wc_cnt = 0;
-            bool wc_in = false;
-            for (;;) {
-              int jj = -1;
-#pragma unroll
-              for (int j = R - 1; j >= 0; --j)
-                if (rem[j]) jj = j;
-              if (jj < 0) break;
-              uint32_t key = 0;
-#pragma unroll
-              for (int j = 0; j < R; ++j)
-                if (j == jj) key = (uint32_t)__builtin_amdgcn_readlane((int)ys[j][sd], __builtin_ctzll(rem[j]));
-              uint32_t cnt = 0;
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                const uint64_t m = ballot(ys[j][sd] == key);
-                cnt += (uint32_t)__popcll((unsigned long long)m);
-                rem[j] &= ~m;
-              }
-              nk++;
-              total += cnt;
-              mx_all = max(mx_all, cnt);
-              if (wc >= 0 && key == (uint32_t)(uint8_t)wc) {
-                wc_in = true;
-                wc_cnt = cnt;
-              } else {
-                mx_nowc = max(mx_nowc, cnt);
-              }
-            }
-            const bool drop = wc_in && nk > 1;
-            const uint32_t nko = drop ? nk - 1 : nk;
-            const uint32_t sum = drop ? total - wc_cnt : total;
-            const uint32_t mx = drop ? mx_nowc : mx_all;
-            const uint64_t mc = max(cfg.min_count, ceil_u64(cfg.min_af * (double)sum));
-            const double thr = nko ? fmin((double)mc, (double)mx) : (double)mc;
-            // pass 2: keys passing the threshold (and, single-consensus
-            // nodes, the split candidates: non-wildcard keys, those >= mc)
-            uint32_t np = 0, ns = 0, npmc = 0;
-            int pk = -1;
-#pragma unroll
-            for (int j = 0; j < R; ++j) rem[j] = ballot(ys[j][sd] != 0x100u);
-            for (;;) {
-              int jj = -1;
-#pragma unroll
-              for (int j = R - 1; j >= 0; --j)
-                if (rem[j]) jj = j;
-              if (jj < 0) break;
-              uint32_t key = 0;
-#pragma unroll
-              for (int j = 0; j < R; ++j)
-                if (j == jj) key = (uint32_t)__builtin_amdgcn_readlane((int)ys[j][sd], __builtin_ctzll(rem[j]));
-              uint32_t cnt = 0;
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                const uint64_t m = ballot(ys[j][sd] == key);
-                cnt += (uint32_t)__popcll((unsigned long long)m);
-                rem[j] &= ~m;
-              }
-              const bool is_wc = wc >= 0 && key == (uint32_t)(uint8_t)wc;
-              if (drop && is_wc) continue;
-              if (!((double)cnt < thr)) {
-                np++;
-                pk = (int)key;
-              }
-              if (!is_wc) {
-                ns++;
-                if ((double)cnt >= (double)mc) npmc++;
-              }
-            }
-            npass[sd] = np;
-            nkeys[sd] = nko;
-            pkey[sd] = pk;
-            if (!tdual) split = npmc > 1 && ns > 1;
-          }
+        if (!weighted && !odd_split) {
+          // ---- votes and selection on the lean path ----
+          SUB_T0(t_v);
+          const SideVotes sv0 = wave_side_votes<R>(cfg, ys[0], mmask[0], mn[0]);
+          SideVotes sv1 = {0, 0, -1, false};
+          if (tdual) sv1 = wave_side_votes<R>(cfg, ys[1], mmask[1], mn[1]);
+          uint32_t npass[2] = {sv0.npass, sv1.npass};
+          const uint32_t nkeys[2] = {sv0.nkeys, sv1.nkeys};
+          const int pkey[2] = {sv0.pk, sv1.pk};
           if (tdual) {
             // options per side: None first (consensus end, no keys, locked),
             // then the passing keys; children = pairs but (None, None)
@@ -846,8 +1085,8 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
             uint32_t no[2];
 #pragma unroll
             for (int sd = 0; sd < 2; ++sd) {
-              const bool lock = (tm.flags & (sd == 0 ? 2u : 4u)) != 0;
-              const bool fin = early && tm.nsome[sd] == 0;  // (no read at its end here)
+              const bool lock = (tflags & (sd == 0 ? 2u : 4u)) != 0;
+              const bool fin = early && (sd == 0 ? ns0 : ns1) == 0;  // (no read at its end here)
               has_none[sd] = fin || nkeys[sd] == 0 || lock;
               if (lock) npass[sd] = 0;
               no[sd] = (has_none[sd] ? 1u : 0u) + npass[sd];
@@ -858,60 +1097,90 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
           } else {
             // stay-single children, and split children from every pair of
             // candidates when two pass min_count (:655-734)
-            nchild = npass[0] + (split ? 2u : 0u);
+            nchild = npass[0] + (sv0.split ? 2u : 0u);
             child[0] = pkey[0];
           }
+          SUB_T1(38, t_v);
         }
-        SUB_T1(38, t_v);
-        if (nchild == 0) {
-          if (tid == 0) {
-            E.L.freestack[WC_IX(ctl.nfree++, E.pcap)] = top;
-            ctl.hot_slot = kNoSlot;
+        if (nchild >= 2) {
+          // weighted votes, splits that round, or several children (their
+          // order): the block engines' votes and selection (from RInfo)
+          SUB_CNT((weighted || odd_split) ? 36 : 39, 1);
+          if (lane == 0) {
+            ctl.ovf = 0;
+            ctl.multi[0] = ctl.multi[1] = any_multi ? 1u : 0u;
+            ctl.fin[0] = early && ns0 == 0;
+            ctl.fin[1] = tdual && early && ns1 == 0;
+            ctl.status = W.status;
           }
           __syncthreads();
+          wave_rare<R>(kp, E.P, sbase, ctl, WR_VOTES_SELECT, topslot, tdual, 0, 0, 0, 0, 0);
+          W.status = uni(ctl.status);
+          if (W.status != ST_OK) break;
+          nchild = uni(ctl.nchild);
+          if (nchild == 1) {
+            child[0] = uni((int32_t)ctl.ch_s[0][0]);
+            child[1] = uni((int32_t)ctl.ch_s[0][1]);
+            kind = uni((uint32_t)ctl.ch_kind[0]);
+          }
+        }
+        if (nchild == 0) {
+          if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = topslot;
+          W.nfree++;
+          W.hot = kNoSlot;
           PH_MARK(3);
           continue;
         }
-        if (nchild == 1 && (tlens[0] + 1 > E.lcap || tlens[1] + 1 > E.lcap)) {
-          if (tid == 0) ctl.status = ST_RETRY | ST_RETRY_LCAP;
-          __syncthreads();
+        if (tlens[0] + 1 > E.lcap || tlens[1] + 1 > E.lcap) {
+          W.status = ST_RETRY | ST_RETRY_LCAP;
           break;
         }
         PH_MARK(3);
-        if (nchild == 1) {
+        if (nchild == 1 && kind != 2) {
           SUB_CNT(37, 1);
-          if (tid == 0) {
-            ctl.ch_s[0][0] = (int16_t)child[0];
-            ctl.ch_s[0][1] = (int16_t)child[1];
-            ctl.ch_kind[0] = (uint8_t)kind;
-            ctl.nchild = 1;
-          }
-          __syncthreads();
-          wave_push_inplace<R>(E, ctl, kp, top, tm, tdual, lr, tx);  // the hot node becomes the child
+          uint32_t nl[2];
+          ccost = wave_push_fast<R>(E, ctl, kp, W, topslot, tm, tdual, kind, child, lr, tx, nl);
+          clen = max(nl[0], nl[1]);
+          if (W.status != ST_OK) break;
+          PH_MARK(11);
         } else {
-          // several children, or multi-symbol reads / weighted votes: the
-          // block engines' votes, selection and children
-          if (tid == 0) {
-            ctl.multi[0] = ctl.multi[1] = any_multi ? 1u : 0u;
-            ctl.fin[0] = early && tm.nsome[0] == 0;
-            ctl.fin[1] = tdual && early && tm.nsome[1] == 0;
-          }
-          __syncthreads();
-          wave_rare<R>(kp, E.P, sbase, ctl, WR_GENERAL_VOTES, top, tdual, 0, 0, 0, 0, 0);
+          // clones, activate_dual: dual_build_children from the slot
+          wctl_to_ctl(W, ctl);
+          wave_rare<R>(kp, E.P, sbase, ctl, WR_CHILDREN, topslot, tdual, 0, 0, 0, 0, 0);
+          wctl_from_ctl(W, ctl);
+          W.hot = kNoSlot;
+          if (W.status != ST_OK) break;
+          nc = nchild;
+          general = true;
         }
       }
-      if (uni(ctl.status) != ST_OK) break;
-      if (uni(ctl.action) == 3) continue;  // (the general path: no child; the slot is free)
-      if (tid == 0) {
-        for (uint32_t c = 0; c < ctl.nchild; ++c) {
-          const uint32_t k = (E.L.meta[ctl.ch_slot[c]].flags & 1u) ? 1 : 0;
-          E.tracker(ctl, k).insert(ctl.ch_len[c]);
-          heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{ctl.ch_cost[c], ctl.ch_len[c], ctl.ch_slot[c]});
+      // ---- the children into the queue and their trackers ----
+      for (uint32_t c = 0; c < nc; ++c) {
+        uint32_t cslot = topslot;
+        if (general) {
+          cslot = uni(ctl.ch_slot[c]);
+          ccost = ((uint64_t)uni((uint32_t)(ctl.ch_cost[c] >> 32)) << 32) | uni((uint32_t)ctl.ch_cost[c]);
+          clen = uni(ctl.ch_len[c]);
         }
+        const uint32_t k = !general ? (tdual ? 1u : 0u) : ((uni(E.L.meta[cslot].flags) & 1u) ? 1u : 0u);
+        if (lane == 0) atomicAdd((uint32_t*)&lc[k][WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
+        if (clen >= W.thr[k]) W.total[k]++;
+        wheap_push(E.L.heap, W.heap_n, HeapEntry{ccost, clen, cslot});
+        W.heap_n++;
       }
-      __syncthreads();
       PH_MARK(7);
     }
+    // the register state back into Ctl for finish_problem
+    if (lane == 0) {
+      ctl.cnt[S_POPS] += W.pops;
+      ctl.cnt[S_EXPLORED] += W.explored;
+      ctl.cnt[S_IGNORED] += W.ignored;
+      ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], W.peakq);
+      ctl.cnt[S_UPDATES] += W.updates;
+      ctl.cnt[S_WOUT] += W.w_out;
+      ctl.cnt[S_COMPARES] += W.compares;
+    }
+    wctl_to_ctl(W, ctl);
     finish_problem(A, ctl, outp, prob, oslot);
   }
   stream_exit(A);
