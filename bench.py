@@ -271,6 +271,7 @@ class Cfg2:
             free[k % 2].release()
         th.join()
         dt = time.perf_counter() - t0
+        self.e2e_packed = up.last_upload_packed()
         if err:
             raise err[0]
         for b in bufs:
@@ -1128,6 +1129,8 @@ def main():
         line["ranks"] = w_ranks
     if e2e:
         line["e2e_loci_per_s"], line["e2e_upload_ms"], line["e2e_compute_ms"] = e2e
+        if getattr(W, "e2e_packed", None) is not None:  # bytes of the last refill sent 2-bit packed (0 = byte path)
+            line["e2e_upload_packed_bytes"] = W.e2e_packed
         line["e2e_note"] = ("fresh batch every step: Python marshalling + pinned staging + H2D of the reads, "
                             "double-buffered against the previous batch's compute")
     if world == 1 and not a.no_cpu:

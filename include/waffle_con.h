@@ -70,6 +70,17 @@ typedef struct wc_results wc_results;
 int wc_ctx_create(int device, wc_ctx** out);
 void wc_ctx_destroy(wc_ctx* ctx);
 const char* wc_last_error(const wc_ctx* ctx);
+/* Which engine builds this context has launched (no reference counterpart:
+ * the reference has one CPU implementation). Bit k = build k, named by
+ * wc_engine_name(k) ("lds.single", "wave.dual", ...; NULL past the last);
+ * reset != 0 clears the mask after reading it. wc_service_engines_used is the
+ * same for a service's own context. */
+uint32_t wc_engines_used(wc_ctx* ctx, int reset);
+const char* wc_engine_name(uint32_t bit);
+/* Bytes the last batch upload of this context sent 2-bit packed (SURVEY §8(f)
+ * f3; 0 = it took the byte path: small, WC_PACK=0, or a byte outside the
+ * raw-code / ACGT alphabets). */
+uint64_t wc_last_upload_packed(const wc_ctx* ctx);
 
 /* One consensus problem (a locus): its reads and optional activation offsets
  * (add_sequence_offset, consensus.rs:120; NULL or -1 entries = None). */
@@ -153,6 +164,7 @@ int wc_service_consensus(wc_service* s, const wc_config* cfg, const wc_problem* 
 int wc_service_dual_consensus(wc_service* s, const wc_config* cfg, const wc_problem* problem, wc_results** out);
 int wc_service_priority_consensus(wc_service* s, const wc_config* cfg, const wc_chain_problem* problem,
                                   wc_results** out);
+uint32_t wc_service_engines_used(wc_service* svc, int reset);
 int wc_service_get_stats(wc_service* s, wc_service_stats* out);
 const char* wc_service_last_error(wc_service* s);
 

@@ -155,6 +155,9 @@ extern "C" {
     pub fn wc_ctx_create(device: c_int, out: *mut *mut wc_ctx) -> c_int;
     pub fn wc_ctx_destroy(ctx: *mut wc_ctx);
     pub fn wc_last_error(ctx: *const wc_ctx) -> *const c_char;
+    pub fn wc_engines_used(ctx: *mut wc_ctx, reset: c_int) -> u32;
+    pub fn wc_engine_name(bit: u32) -> *const c_char;
+    pub fn wc_last_upload_packed(ctx: *const wc_ctx) -> u64;
 
     pub fn wc_consensus_batch(ctx: *mut wc_ctx, cfg: *const wc_config, n: u32, problems: *const wc_problem,
                               out: *mut *mut wc_results) -> c_int;
@@ -182,6 +185,7 @@ extern "C" {
                                          problem: *const wc_chain_problem, out: *mut *mut wc_results) -> c_int;
     pub fn wc_service_get_stats(s: *mut wc_service, out: *mut wc_service_stats) -> c_int;
     pub fn wc_service_last_error(s: *mut wc_service) -> *const c_char;
+    pub fn wc_service_engines_used(s: *mut wc_service, reset: c_int) -> u32;
 
     pub fn wc_results_free(r: *mut wc_results);
     pub fn wc_results_problems(r: *const wc_results) -> u32;

@@ -128,6 +128,7 @@ EXPORTED = (
     "wc_gen_sample", "wc_gen_free", "wc_wfa_ed_config", "wc_wfa_ed_batch",
     "wc_service_create", "wc_service_destroy", "wc_service_consensus", "wc_service_dual_consensus",
     "wc_service_priority_consensus", "wc_service_get_stats", "wc_service_last_error",
+    "wc_engines_used", "wc_engine_name", "wc_last_upload_packed", "wc_service_engines_used",
 )
 
 
@@ -213,6 +214,14 @@ def lib():
         L.wc_service_get_stats.argtypes = [vp, ctypes.POINTER(WcServiceStats)]
         L.wc_service_last_error.argtypes = [vp]
         L.wc_service_last_error.restype = ctypes.c_char_p
+        L.wc_engines_used.argtypes = [vp, ctypes.c_int]
+        L.wc_engines_used.restype = ctypes.c_uint32
+        L.wc_service_engines_used.argtypes = [vp, ctypes.c_int]
+        L.wc_service_engines_used.restype = ctypes.c_uint32
+        L.wc_engine_name.argtypes = [ctypes.c_uint32]
+        L.wc_engine_name.restype = ctypes.c_char_p
+        L.wc_last_upload_packed.argtypes = [vp]
+        L.wc_last_upload_packed.restype = ctypes.c_uint64
         _lib = L
         return L
 
@@ -232,6 +241,14 @@ class Context:
     def last_error(self):
         return lib().wc_last_error(self.handle).decode()
 
+    def engines_used(self, reset=False):
+        """Names of the engine builds this context has launched (wc_engines_used)."""
+        return engine_names(lib().wc_engines_used(self.handle, int(bool(reset))))
+
+    def last_upload_packed(self):
+        """Bytes the last batch upload sent 2-bit packed (0 = byte path)."""
+        return int(lib().wc_last_upload_packed(self.handle))
+
     def close(self):
         if self.handle:
             lib().wc_ctx_destroy(self.handle)
@@ -242,6 +259,18 @@ class Context:
             self.close()
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
+
+
+def engine_names(mask):
+    """The engine build names (wc_engine_name) of the bits of `mask`."""
+    out, k = [], 0
+    while True:
+        name = lib().wc_engine_name(k)
+        if name is None:
+            return out
+        if mask >> k & 1:
+            out.append(name.decode())
+        k += 1
 
 
 def default_context():
@@ -276,6 +305,9 @@ class Service:
 
     def last_error(self):
         return lib().wc_service_last_error(self.handle).decode()
+
+    def engines_used(self, reset=False):
+        return engine_names(lib().wc_service_engines_used(self.handle, int(bool(reset))))
 
     def close(self):
         if self.handle:

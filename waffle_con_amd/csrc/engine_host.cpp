@@ -334,8 +334,25 @@ void fault_sentinels(EngineArgs& a, const Caps& caps) {
 }
 }  // namespace
 
+// engine builds (wc_engine_name): bit = 2 * build + sides - 1
+const char* const kEngineNames[] = {"lds.single",    "lds.dual",    "narrow.single", "narrow.dual",
+                                    "lowlat.single", "lowlat.dual", "cu.single",     "cu.dual",
+                                    "chain.single",  "chain.dual",  "wave.single",   "wave.dual",
+                                    "gstate.single", "gstate.dual"};
+const uint32_t kNumEngineNames = sizeof(kEngineNames) / sizeof(kEngineNames[0]);
+static uint32_t engine_build(const Caps& caps) {
+  if (caps.gstate) return 6;
+  if (caps.sides == 2 && caps.chain > 0) return 4;
+  if (caps.wave) return 5;
+  if (caps.cu) return 3;
+  if (caps.narrow) return 1;
+  if (caps.lowlat) return 2;
+  return 0;
+}
+
 // launches the engine of `caps` (LDS or global-state build) on L's stream
 int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
+  ctx->engines_used.fetch_or(1u << (2 * engine_build(caps) + (caps.sides == 2 ? 1 : 0)), std::memory_order_relaxed);
   if (caps.gstate) {
     if (!L.gst.ensure((caps.gsb + kGuard) * L.grid)) return set_err(ctx, WC_E_HIP, "device allocation failed (search state)");
     a.gstate = (uint8_t*)L.gst.p;

@@ -9,6 +9,8 @@
 // (wavefront length, node pool, consensus length, result records) are re-run
 // on the device with larger capacities; no consensus work is ever done on the
 // CPU.
+#include <immintrin.h>
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -97,6 +99,74 @@ DevConfig to_dev(const wc_config& c) {
   return d;
 }
 
+// ---- 2-bit packed uploads ----
+// A batch whose reads use one four-symbol alphabet (the raw codes 0..3 of
+// generate_test, or ASCII A/C/G/T) is packed on the host, 2 bits per base,
+// while it is staged (the staging pass reads every byte anyway), crosses PCIe
+// at a quarter of the bytes, and is expanded into the byte arena on the device
+// (pack2.hip). Read r's packed bytes start at roff[r] / 4 (roff is 16-byte
+// aligned); byte t holds bases 4t..4t+3, base 4t+k in bits 2k..2k+1; bases
+// past the read's end pack as code 0 (the device writes zeros there).
+namespace {
+enum PackMode : int { kPackNone = 0, kPackRaw = 1, kPackAcgt = 2 };
+// ASCII A/C/G/T -> (b >> 1) & 3 = 0, 1, 3, 2
+inline int acgt_code(uint8_t x) {
+  switch (x) {
+    case 'A': return 0;
+    case 'C': return 1;
+    case 'G': return 3;
+    case 'T': return 2;
+    default: return -1;
+  }
+}
+bool pack_read_scalar(const uint8_t* s, uint32_t from, uint32_t len, uint8_t* d, int mode) {
+  const uint32_t padded = (len + 15) & ~15u;
+  for (uint32_t i = from; i < padded; i += 4) {
+    uint32_t b = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t pos = i + k;
+      if (pos >= len) continue;
+      const uint8_t x = s[pos];
+      const int c = mode == kPackRaw ? (x < 4 ? (int)x : -1) : acgt_code(x);
+      if (c < 0) return false;
+      b |= (uint32_t)c << (2 * k);
+    }
+    d[i / 4] = (uint8_t)b;
+  }
+  return true;
+}
+// 64 bases -> 16 bytes per step: validate, map to codes, then two
+// multiply-adds combine 4 codes into one byte and a truncation packs 16 of them
+__attribute__((target("avx512f,avx512bw"))) bool pack_read_avx512(const uint8_t* s, uint32_t len, uint8_t* d,
+                                                                   int mode) {
+  uint32_t i = 0;
+  const __m512i w16 = _mm512_set1_epi16(0x0401), w32 = _mm512_set1_epi32(0x00100001);
+  for (; i + 64 <= len; i += 64) {
+    const __m512i x = _mm512_loadu_si512((const void*)(s + i));
+    __m512i c;
+    if (mode == kPackRaw) {
+      if (_mm512_test_epi8_mask(x, _mm512_set1_epi8((char)0xFC))) return false;
+      c = x;
+    } else {
+      const __mmask64 ok = _mm512_cmpeq_epi8_mask(x, _mm512_set1_epi8('A')) |
+                           _mm512_cmpeq_epi8_mask(x, _mm512_set1_epi8('C')) |
+                           _mm512_cmpeq_epi8_mask(x, _mm512_set1_epi8('G')) |
+                           _mm512_cmpeq_epi8_mask(x, _mm512_set1_epi8('T'));
+      if (ok != ~0ull) return false;
+      c = _mm512_and_si512(_mm512_srli_epi16(x, 1), _mm512_set1_epi8(3));
+    }
+    const __m512i t16 = _mm512_maddubs_epi16(c, w16);  // c0 + 4 c1
+    const __m512i t32 = _mm512_madd_epi16(t16, w32);   // (c0 + 4 c1) + 16 (c2 + 4 c3)
+    _mm_storeu_si128((__m128i*)(d + i / 4), _mm512_cvtepi32_epi8(t32));
+  }
+  return pack_read_scalar(s, i, len, d, mode);
+}
+bool have_avx512() {
+  static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
+  return ok;
+}
+}  // namespace
+
 // Copies every read of `problems` into one 16-byte-aligned arena and uploads it.
 // The host side is one pass of memcpy into pinned staging (split over threads
 // by bytes), then a single DMA; the device buffer of `b` is reused when it is
@@ -143,12 +213,6 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
   const uint64_t total = pos + 64;
   std::vector<uint8_t> fallback;
   uint8_t* h = nullptr;
-  if (ctx->upstage.ensure(total)) {
-    h = (uint8_t*)ctx->upstage.p;
-  } else {
-    fallback.resize(total);
-    h = fallback.data();
-  }
   auto fill = [&](uint64_t r0, uint64_t r1) {
     for (uint64_t r = r0; r < r1; ++r) {
       const uint64_t len = rlen[r], pad = ((len + 15) & ~15ull) - len;
@@ -156,6 +220,18 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
       if (pad) memset(h + roff[r] + len, 0, pad);
     }
   };
+  // the alphabet of a packed upload, from the first read (the packer checks
+  // every byte; one outside it sends the whole batch the byte way)
+  int pmode = kPackNone;
+  {
+    const char* pe = getenv("WC_PACK");
+    const bool want_pack = pe ? atoi(pe) != 0 : total >= (16ull << 20);
+    for (uint64_t r = 0; want_pack && r < nr && pmode == kPackNone; ++r)
+      if (rlen[r]) pmode = src[r][0] < 4 ? kPackRaw : (acgt_code(src[r][0]) >= 0 ? kPackAcgt : -1);
+    if (pmode < 0) pmode = kPackNone;
+  }
+  const uint32_t plut = pmode == kPackRaw ? 0x03020100u : ('A' | 'C' << 8 | 'T' << 16 | (uint32_t)'G' << 24);
+  ctx->last_upload_packed = 0;
   // device buffers: reused when large enough, else new ones beside the old
   DevBuf grown[3];
   DevBuf* dst[3] = {&b->reads, &b->roff, &b->rlen};
@@ -174,10 +250,82 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
     for (DevBuf& g : grown) g.release();
     return set_err(ctx, WC_E_HIP, what);
   };
+  auto commit = [&]() {
+    for (int i = 0; i < 3; ++i)
+      if (dst[i] == &grown[i]) {
+        DevBuf* old = i == 0 ? &b->reads : (i == 1 ? &b->roff : &b->rlen);
+        old->release();
+        *old = grown[i];
+        grown[i].p = nullptr;
+        grown[i].cap = 0;
+      }
+    b->ctx = ctx;
+    b->probs.swap(probs);
+    b->roff_h.swap(roff);
+    b->rlen_h.swap(rlen);
+    b->bytes = total;
+    b->valid = true;
+    return (int)WC_OK;
+  };
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  // reads split into contiguous ranges of about equal bytes, one per thread
+  auto split_run = [&](uint64_t r_begin, uint64_t r_end, uint64_t nt, auto fn) {
+    const uint64_t b0 = r_begin < nr ? roff[r_begin] : pos, b1 = r_end < nr ? roff[r_end] : pos;
+    if (nt <= 1 || r_end - r_begin < 2) {
+      fn(r_begin, r_end);
+      return;
+    }
+    std::vector<std::thread> th;
+    uint64_t r0 = r_begin;
+    for (uint64_t t = 0; t < nt; ++t) {
+      const uint64_t want_b = b0 + (b1 - b0) * (t + 1) / nt;
+      uint64_t r1 = r0;
+      while (r1 < r_end && (t + 1 == nt || roff[r1] < want_b)) ++r1;
+      th.emplace_back(fn, r0, r1);
+      r0 = r1;
+    }
+    for (auto& x : th) x.join();
+  };
+  if (pmode != kPackNone && ctx->upstage.ensure(pos / 4 + 16) && ctx->upk.ensure(pos / 4 + 16)) {
+    // packed: every read packed straight from the caller's buffer into pinned
+    // staging (AVX-512 where the CPU has it), one H2D copy of a quarter of the
+    // bytes, the read tables, then the device expands the arena
+    uint8_t* hp = (uint8_t*)ctx->upstage.p;
+    std::atomic<bool> ok{true};
+    const bool simd = have_avx512() && !getenv("WC_PACK_SCALAR");  // (test hook: the scalar packer)
+    split_run(0, nr, std::max<uint64_t>(1, std::min<uint64_t>(hw, pos >> 23)), [&](uint64_t r0, uint64_t r1) {
+      for (uint64_t r = r0; r < r1 && ok.load(std::memory_order_relaxed); ++r) {
+        const bool good = simd ? pack_read_avx512(src[r], rlen[r], hp + roff[r] / 4, pmode)
+                               : pack_read_scalar(src[r], 0, rlen[r], hp + roff[r] / 4, pmode);
+        if (!good) ok.store(false, std::memory_order_relaxed);
+      }
+    });
+    if (ok.load()) {
+      if ((pos && hipMemcpyAsync(ctx->upk.p, hp, pos / 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) ||
+          (!roff.empty() &&
+           hipMemcpyAsync(dst[1]->p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) ||
+          (!rlen.empty() &&
+           hipMemcpyAsync(dst[2]->p, rlen.data(), rlen.size() * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
+        return fail("read upload failed");
+      launch_unpack2((const uint32_t*)ctx->upk.p, (const uint64_t*)dst[1]->p, (const uint32_t*)dst[2]->p, (uint32_t)nr,
+                     plut, (uint8_t*)dst[0]->p, pos, ctx->stream);
+      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
+        return fail("read upload failed (device unpack)");
+      ctx->last_upload_packed = pos / 4;
+      return commit();
+    }
+    // a byte outside the alphabet: the byte path below
+  }
+  // staging buffer of the byte path (the packed path may have used it)
+  if (!ctx->upstage.ensure(total)) {
+    fallback.resize(total);
+    h = fallback.data();
+  } else {
+    h = (uint8_t*)ctx->upstage.p;
+  }
   // chunks of >= 64 MiB (at most 8): the H2D copy of chunk k runs while the
   // host threads stage chunk k + 1; inside a chunk the reads are split into
   // contiguous ranges of about equal bytes, one per thread
-  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   const uint64_t nch = std::max<uint64_t>(1, std::min<uint64_t>(8, total >> 26));
   uint64_t c_r0 = 0;
   for (uint64_t c = 0; c < nch; ++c) {
@@ -186,21 +334,7 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
     while (c_r1 < nr && (c + 1 == nch || roff[c_r1] < want_end)) ++c_r1;
     const uint64_t b0 = c_r0 < nr ? roff[c_r0] : pos;
     const uint64_t b1 = c_r1 < nr ? roff[c_r1] : pos;
-    const uint64_t nt = std::max<uint64_t>(1, std::min<uint64_t>(hw, (b1 - b0) >> 23));  // >= 8 MiB per thread
-    if (nt <= 1 || c_r1 - c_r0 < 2) {
-      fill(c_r0, c_r1);
-    } else {
-      std::vector<std::thread> th;
-      uint64_t r0 = c_r0;
-      for (uint64_t t = 0; t < nt; ++t) {
-        const uint64_t want_b = b0 + (b1 - b0) * (t + 1) / nt;
-        uint64_t r1 = r0;
-        while (r1 < c_r1 && (t + 1 == nt || roff[r1] < want_b)) ++r1;
-        th.emplace_back(fill, r0, r1);
-        r0 = r1;
-      }
-      for (auto& x : th) x.join();
-    }
+    split_run(c_r0, c_r1, std::max<uint64_t>(1, std::min<uint64_t>(hw, (b1 - b0) >> 23)), fill);  // >= 8 MiB per thread
     const bool last = c + 1 == nch;
     if (last) memset(h + pos, 0, 64);
     const uint64_t e1 = last ? total : b1;
@@ -216,22 +350,7 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
       hipMemcpyAsync(dst[2]->p, rlen.data(), rlen.size() * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
     return fail("read table upload failed");
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail("read upload failed");
-  // commit
-  for (int i = 0; i < 3; ++i)
-    if (dst[i] == &grown[i]) {
-      DevBuf* old = i == 0 ? &b->reads : (i == 1 ? &b->roff : &b->rlen);
-      old->release();
-      *old = grown[i];
-      grown[i].p = nullptr;
-      grown[i].cap = 0;
-    }
-  b->ctx = ctx;
-  b->probs.swap(probs);
-  b->roff_h.swap(roff);
-  b->rlen_h.swap(rlen);
-  b->bytes = total;
-  b->valid = true;
-  return WC_OK;
+  return commit();
 }
 
 }  // namespace wch
@@ -362,6 +481,15 @@ void wc_ctx_destroy(wc_ctx* ctx) {
 }
 
 const char* wc_last_error(const wc_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+uint32_t wc_engines_used(wc_ctx* ctx, int reset) {
+  if (!ctx) return 0;
+  return reset ? ctx->engines_used.exchange(0) : ctx->engines_used.load();
+}
+
+const char* wc_engine_name(uint32_t bit) { return bit < wch::kNumEngineNames ? wch::kEngineNames[bit] : nullptr; }
+
+uint64_t wc_last_upload_packed(const wc_ctx* ctx) { return ctx ? ctx->last_upload_packed : 0; }
 
 int wc_batch_create(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch** out) {
   *out = nullptr;

@@ -1,6 +1,7 @@
 // Host-side types shared by the C ABI (host.cpp) and the engine scheduler
 // (engine_host.cpp). Not part of the public interface.
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <array>
@@ -14,6 +15,8 @@
 #include "engine_shared.hpp"
 
 namespace wc {
+void launch_unpack2(const uint32_t* packed, const uint64_t* roff, const uint32_t* rlen, uint32_t nreads, uint32_t lut,
+                    uint8_t* out, uint64_t pos, hipStream_t s);
 void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
@@ -128,6 +131,9 @@ struct wc_ctx {
   std::string err;
   DevBuf jobs;
   HostBuf upstage;  // pinned staging of batch uploads (reused across batches)
+  DevBuf upk;       // 2-bit packed batch uploads before the device expands them (host.cpp pack_reads)
+  uint64_t last_upload_packed = 0;  // bytes the last batch upload sent packed (0 = byte path)
+  std::atomic<uint32_t> engines_used{0};  // wc_engines_used: bit per engine build launched (engine_host.cpp)
   // engine launch slots (engine_host.cpp): each has its own stream and buffers
   std::vector<wch::Launch*> launches;
 };
@@ -207,6 +213,8 @@ int set_err(wc_ctx* ctx, int code, const std::string& msg);
 wc::DevConfig to_dev(const wc_config& c);
 inline uint64_t cost_of_h(uint32_t e, int mode) { return mode == 0 ? (uint64_t)e : (uint64_t)e * (uint64_t)e; }
 int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* b);
+extern const char* const kEngineNames[];
+extern const uint32_t kNumEngineNames;
 
 // One engine problem as the host schedules it: global read ids into a batch
 // arena and each read's activation length (-1 = active at the root).

@@ -947,6 +947,8 @@ int wc_service_priority_consensus(wc_service* s, const wc_config* cfg, const wc_
   return service_priority(s, cfg, problem, out);
 }
 
+uint32_t wc_service_engines_used(wc_service* s, int reset) { return s ? wc_engines_used(s->ctx, reset) : 0; }
+
 int wc_service_get_stats(wc_service* s, wc_service_stats* out) {
   if (!s || !out) return WC_E_BAD_INPUT;
   std::lock_guard<std::mutex> g(s->mu);
