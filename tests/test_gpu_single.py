@@ -58,6 +58,27 @@ def test_chain_length_invariance(chain, L, N, err, seed, monkeypatch):
         assert gc[k] == ec[k], (k, gc[k], ec[k])
 
 
+@pytest.mark.parametrize("chain", ["2", "5", "16", "31", "40"])
+@pytest.mark.parametrize("L,N,err,seed", [(1500, 20, 0.01, 11), (800, 12, 0.04, 12), (600, 9, 0.08, 13)])
+def test_chain_length_invariance_cu(chain, L, N, err, seed, monkeypatch):
+    """The same on the 1024-thread single engine (engine_cu.hip, WC_CU=1),
+    whose chain walk spreads reads over 16 waves: per-call batch path on the
+    default context, whose engine mask must show that build ran."""
+    from waffle_con_amd import _lib
+    monkeypatch.setenv("WAFFLE_CON_SERVICE", "0")
+    monkeypatch.setenv("WC_CU", "1")
+    monkeypatch.setenv("WC_CHAIN", chain)
+    _lib.default_context().engines_used(reset=True)
+    seqs = _gen(L, N, err, seed)
+    cfg = dict(min_count=max(1, N // 4))
+    exp, ec = orc.consensus(seqs, counters=True, **cfg)
+    got, gc = hip.consensus(seqs, counters=True, **cfg)
+    assert _lib.default_context().engines_used(reset=True) == ["cu.single"]
+    assert got == exp
+    for k in COUNTER_KEYS:
+        assert gc[k] == ec[k], (k, gc[k], ec[k])
+
+
 def test_failed_refill_leaves_the_batch_usable():
     """host.cpp upload_batch is transactional: a refill rejected by validation
     changes nothing, so the batch still runs its previous problems."""

@@ -1,6 +1,8 @@
 """One DualConsensusDWFA problem alone, twice (warm-up + measured), for PMC
 passes and A/B runs: the HPC-level sub-problem of cfg5 locus --seed (the
-first level of its chains, all reads), or a cfg3 locus.
+first level of its chains, all reads), the full-read level of the same chains
+(cfg5-full: the level whose sub-problems make most of a deep locus's
+critical path), or a cfg3 locus.
   python tools/one_sub.py --seed 48 [--workload cfg5-hpc|cfg3] [--reps 1]"""
 import argparse
 import json
@@ -14,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cfg5-hpc", choices=("cfg5-hpc", "cfg3"))
+    ap.add_argument("--workload", default="cfg5-hpc", choices=("cfg5-hpc", "cfg5-full", "cfg3"))
     ap.add_argument("--seed", type=int, default=48)
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--phases", default="", help="WC_PHASES file: per-pop phase cycles of the measured runs "
@@ -26,7 +28,8 @@ def main():
     if a.workload == "cfg3":
         p, cfg = synth.cfg3_locus(a.seed), CdwfaConfig()
     else:
-        p, cfg = [ch[0] for ch in synth.cfg5_locus(a.seed)], CdwfaConfig(wildcard=ord("*"))
+        lvl = 1 if a.workload == "cfg5-full" else 0
+        p, cfg = [ch[lvl] for ch in synth.cfg5_locus(a.seed)], CdwfaConfig(wildcard=ord("*"))
     b = w.ResidentBatch([p])
     b.dual_consensus(cfg)
     if a.phases:

@@ -286,62 +286,65 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
     }
     for (auto& x : th) x.join();
   };
-  if (pmode != kPackNone && ctx->upstage.ensure(pos / 4 + 16) && ctx->upk.ensure(pos / 4 + 16)) {
-    // packed: every read packed straight from the caller's buffer into pinned
-    // staging (AVX-512 where the CPU has it), one H2D copy of a quarter of the
-    // bytes, the read tables, then the device expands the arena
+  // chunks of >= 64 MiB of reads (at most 8): the H2D copy of chunk k runs
+  // while the host threads stage chunk k + 1; inside a chunk the reads are
+  // split into contiguous ranges of about equal bytes, one per thread (>= 8 MiB
+  // each). Packed: every read is packed straight from the caller's buffer into
+  // pinned staging (AVX-512 where the CPU has it) and a quarter of the bytes
+  // crosses PCIe into ctx->upk; a byte outside the alphabet stops it and the
+  // whole batch goes again the byte way.
+  bool packed = pmode != kPackNone && ctx->upstage.ensure(pos / 4 + 16) && ctx->upk.ensure(pos / 4 + 16);
+  const bool simd = have_avx512() && !getenv("WC_PACK_SCALAR");  // (test hook: the scalar packer)
+  std::atomic<bool> ok{true};
+  auto pack = [&](uint64_t r0, uint64_t r1) {
     uint8_t* hp = (uint8_t*)ctx->upstage.p;
-    std::atomic<bool> ok{true};
-    const bool simd = have_avx512() && !getenv("WC_PACK_SCALAR");  // (test hook: the scalar packer)
-    split_run(0, nr, std::max<uint64_t>(1, std::min<uint64_t>(hw, pos >> 23)), [&](uint64_t r0, uint64_t r1) {
-      for (uint64_t r = r0; r < r1 && ok.load(std::memory_order_relaxed); ++r) {
-        const bool good = simd ? pack_read_avx512(src[r], rlen[r], hp + roff[r] / 4, pmode)
-                               : pack_read_scalar(src[r], 0, rlen[r], hp + roff[r] / 4, pmode);
-        if (!good) ok.store(false, std::memory_order_relaxed);
-      }
-    });
-    if (ok.load()) {
-      if ((pos && hipMemcpyAsync(ctx->upk.p, hp, pos / 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) ||
-          (!roff.empty() &&
-           hipMemcpyAsync(dst[1]->p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) ||
-          (!rlen.empty() &&
-           hipMemcpyAsync(dst[2]->p, rlen.data(), rlen.size() * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
-        return fail("read upload failed");
-      launch_unpack2((const uint32_t*)ctx->upk.p, (const uint64_t*)dst[1]->p, (const uint32_t*)dst[2]->p, (uint32_t)nr,
-                     plut, (uint8_t*)dst[0]->p, pos, ctx->stream);
-      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
-        return fail("read upload failed (device unpack)");
-      ctx->last_upload_packed = pos / 4;
-      return commit();
+    for (uint64_t r = r0; r < r1 && ok.load(std::memory_order_relaxed); ++r) {
+      const bool good = simd ? pack_read_avx512(src[r], rlen[r], hp + roff[r] / 4, pmode)
+                             : pack_read_scalar(src[r], 0, rlen[r], hp + roff[r] / 4, pmode);
+      if (!good) ok.store(false, std::memory_order_relaxed);
     }
-    // a byte outside the alphabet: the byte path below
-  }
-  // staging buffer of the byte path (the packed path may have used it)
-  if (!ctx->upstage.ensure(total)) {
-    fallback.resize(total);
-    h = fallback.data();
-  } else {
-    h = (uint8_t*)ctx->upstage.p;
-  }
-  // chunks of >= 64 MiB (at most 8): the H2D copy of chunk k runs while the
-  // host threads stage chunk k + 1; inside a chunk the reads are split into
-  // contiguous ranges of about equal bytes, one per thread
+  };
   const uint64_t nch = std::max<uint64_t>(1, std::min<uint64_t>(8, total >> 26));
-  uint64_t c_r0 = 0;
-  for (uint64_t c = 0; c < nch; ++c) {
-    const uint64_t want_end = pos * (c + 1) / nch;
-    uint64_t c_r1 = c_r0;
-    while (c_r1 < nr && (c + 1 == nch || roff[c_r1] < want_end)) ++c_r1;
-    const uint64_t b0 = c_r0 < nr ? roff[c_r0] : pos;
-    const uint64_t b1 = c_r1 < nr ? roff[c_r1] : pos;
-    split_run(c_r0, c_r1, std::max<uint64_t>(1, std::min<uint64_t>(hw, (b1 - b0) >> 23)), fill);  // >= 8 MiB per thread
-    const bool last = c + 1 == nch;
-    if (last) memset(h + pos, 0, 64);
-    const uint64_t e1 = last ? total : b1;
-    if (e1 > b0 && hipMemcpyAsync((uint8_t*)dst[0]->p + b0, h + b0, e1 - b0, hipMemcpyHostToDevice, ctx->stream) !=
-                       hipSuccess)
-      return fail("read upload failed");
-    c_r0 = c_r1;
+  for (int pass = packed ? 0 : 1; pass < 2; ++pass) {
+    const bool pk = pass == 0;
+    if (!pk) {
+      // staging of the byte path (after a packed attempt's copies have drained)
+      if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail("read upload failed");
+      if (!ctx->upstage.ensure(total)) {
+        fallback.resize(total);
+        h = fallback.data();
+      } else {
+        h = (uint8_t*)ctx->upstage.p;
+      }
+    }
+    uint64_t c_r0 = 0;
+    for (uint64_t c = 0; c < nch && (!pk || ok.load()); ++c) {
+      const uint64_t want_end = pos * (c + 1) / nch;
+      uint64_t c_r1 = c_r0;
+      while (c_r1 < nr && (c + 1 == nch || roff[c_r1] < want_end)) ++c_r1;
+      const uint64_t b0 = c_r0 < nr ? roff[c_r0] : pos;
+      const uint64_t b1 = c_r1 < nr ? roff[c_r1] : pos;
+      const uint64_t nt = std::max<uint64_t>(1, std::min<uint64_t>(hw, (b1 - b0) >> 23));
+      const bool last = c + 1 == nch;
+      if (pk) {
+        split_run(c_r0, c_r1, nt, pack);
+        if (!ok.load()) break;
+        if (b1 > b0 && hipMemcpyAsync((uint8_t*)ctx->upk.p + b0 / 4, (uint8_t*)ctx->upstage.p + b0 / 4, (b1 - b0) / 4,
+                                      hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+          return fail("read upload failed");
+      } else {
+        split_run(c_r0, c_r1, nt, fill);
+        if (last) memset(h + pos, 0, 64);
+        const uint64_t e1 = last ? total : b1;
+        if (e1 > b0 && hipMemcpyAsync((uint8_t*)dst[0]->p + b0, h + b0, e1 - b0, hipMemcpyHostToDevice,
+                                      ctx->stream) != hipSuccess)
+          return fail("read upload failed");
+      }
+      c_r0 = c_r1;
+    }
+    if (pk && !ok.load()) continue;  // a byte outside the alphabet
+    packed = pk;
+    break;
   }
   if (!roff.empty() &&
       hipMemcpyAsync(dst[1]->p, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
@@ -349,7 +352,13 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
   if (!rlen.empty() &&
       hipMemcpyAsync(dst[2]->p, rlen.data(), rlen.size() * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
     return fail("read table upload failed");
+  if (packed) {
+    launch_unpack2((const uint32_t*)ctx->upk.p, (const uint64_t*)dst[1]->p, (const uint32_t*)dst[2]->p, (uint32_t)nr,
+                   plut, (uint8_t*)dst[0]->p, pos, ctx->stream);
+    if (hipGetLastError() != hipSuccess) return fail("read upload failed (device unpack)");
+  }
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail("read upload failed");
+  ctx->last_upload_packed = packed ? pos / 4 : 0;
   return commit();
 }
 

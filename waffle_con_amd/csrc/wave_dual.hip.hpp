@@ -564,6 +564,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   nl[1] = m.len[1];
   uint32_t upd = 0, wout = 0, cmps = 0, nheavy = 0;
   uint32_t ee[R][2];  // the child's edit distances (kInactive = None)
+  SUB_T0(t_pl);
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const uint32_t r = (uint32_t)lane + 64u * j;
@@ -610,6 +611,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   W.updates += wave_sum_u32(upd);
   W.w_out += wave_sum_u32(wout);
   W.compares += wave_sum_u32(cmps);
+  SUB_T1(48, t_pl);  // (push: the lane pass and its counters)
   if (nheavy) {
     // the ED-increase loops, out of line; then the rebuilt states and their
     // tip bytes from the hot copy
@@ -647,6 +649,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   }
   // prune_dwfa (:1030-1045) of a dual child, then per read the cheaper side's
   // cost (strict <: ties keep consensus 1, :1092-1131) and the Some counts
+  SUB_T0(t_pc);
   uint64_t cost = 0;
   uint32_t c0 = 0, c1 = 0;
 #pragma unroll
@@ -675,6 +678,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   m.nsome[0] = wave_sum_u32(c0);
   m.nsome[1] = wave_sum_u32(c1);
   if (lane == 0) meta_put(E.L.meta[top], m);
+  SUB_T1(49, t_pc);  // (push: prune, cost, Some counts)
   return cost;
 }
 
@@ -922,6 +926,7 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
     for (;;) {
       // ---- pop (dual_consensus.rs:340-397) ----
       if (W.heap_n == 0) break;
+      SUB_T0(t_pl);
       const uint32_t plen = uni(E.L.heap[0].len);
       // the processed counts of the top's length, loaded first (HBM, under
       // one wait) while the threshold walks and the sift run
@@ -937,8 +942,12 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
           W.lastc[k] = 0;
         }
       }
+      SUB_T1(45, t_pl);  // (pop-logic: to the heap pop)
+      SUB_T0(t_hp);
       W.heap_n--;
       const HeapEntry top = wheap_pop(E.L.heap, W.heap_n);
+      SUB_T1(46, t_hp);  // (pop-logic: the heap pop)
+      SUB_T0(t_pc);
       const SlotMeta tm = meta_get(E.L.meta[top.slot]);
       const uint32_t dual = uni(tm.flags) & 1u;
       const uint32_t ns0 = uni(tm.nsome[0]), ns1 = uni(tm.nsome[1]);
@@ -948,6 +957,7 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
       const bool imbalanced = dual && (ns0 < am || ns1 < am);
       if (top.len >= W.am_len) W.status = WC_E_INVARIANT_CODE;
       const bool at_cap = uni(dual ? pc_pre1 : pc_pre0) >= cap;
+      SUB_T1(47, t_pc);  // (pop-logic: metadata, tracker, the processed count)
       if (A.trace && lane == 0) {
         const uint32_t act = (top.cost > W.max_err || top.len < W.thr[dual] || at_cap || imbalanced) ? 1u : 0u;
         trace_pop(A, prob, top, dual | (act << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
