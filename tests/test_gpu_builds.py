@@ -6,7 +6,8 @@ bit 1 = dual engine, default 2), the global-state build (WC_GSTATE), the
 1024-thread single engine (engine_cu.hip, the default for batch launches of
 at most one problem per CU; WC_CU=1 forces it, WC_CU=0 keeps it off in the
 other variants), each dual build with dual_hot forced on, and the one-wave
-dual engine (engine_wave.hip, WC_WAVE=1). The build is picked per launch from
+dual engine (engine_wave.hip, the default for dual problems without offsets;
+WC_WAVE=0 in every other variant). The build is picked per launch from
 the environment (engine_host.cpp plan_caps), so one process exercises all of
 them. The calls take the per-call batch path (WAFFLE_CON_SERVICE=0) on the
 thread's default context, whose wc_engines_used mask must name the build the
@@ -49,6 +50,7 @@ def build(request, monkeypatch):
     for k in KNOBS:
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("WC_CU", "0")
+    monkeypatch.setenv("WC_WAVE", "0")  # (the default for dual problems without offsets)
     monkeypatch.setenv("WAFFLE_CON_SERVICE", "0")
     for k, v in BUILDS[request.param].items():
         monkeypatch.setenv(k, v)

@@ -2537,17 +2537,18 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
 
 #ifdef WC_WAVE_DUAL
 #include "wave_dual.hip.hpp"
-// one kernel per reads-per-lane count (engine_wave.hip): problems of <= 64
-// reads, and of <= 128 (two reads per lane)
+// one kernel per reads-per-lane count (engine_wave.hip): launches whose
+// problems have <= 64 reads, and launches with larger ones (<= 128 reads, two
+// per lane), where each problem of <= 64 reads still runs one read per lane
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_wave1_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
-  dual_main_wave<1>(A, smem, *(Lo<Ctl>*)&ctl_lds);
+  dual_main_wave<1, false>(A, smem, *(Lo<Ctl>*)&ctl_lds);
 }
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_wave2_kernel(EngineArgs A) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WC_WAVE2_WPE))) dual_wave2_kernel(EngineArgs A) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Ctl ctl_lds;
-  dual_main_wave<2>(A, smem, *(Lo<Ctl>*)&ctl_lds);
+  dual_main_wave<2, true>(A, smem, *(Lo<Ctl>*)&ctl_lds);
 }
 #elif !defined(WC_SINGLE_ONLY)  // (engine_cu.hip: the single engine only)
 // two kernels, one per dual_hot: in one kernel the two paths' register

@@ -185,9 +185,11 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   if (c.cu) c.narrow = c.lowlat = false;
   // The dual engine on one wave per problem (engine_wave.hip): dual searches
   // without offsets of at most 128 reads, whose popped node stays in LDS with
-  // its tip bytes in registers. WC_WAVE=1 enables it.
+  // its tip bytes in registers. The default for them: cfg5
+  // locus 5949's critical path 17.2 -> 12.7 s, cfg3 210 -> 212 loci/s.
+  // WC_WAVE=0 keeps them on the block engines.
   const char* wvenv = getenv("WC_WAVE");
-  c.wave = sides == 2 && chain == 0 && !gstate && !any_act && nmax <= 128 && wvenv && atoi(wvenv) == 1 &&
+  c.wave = sides == 2 && chain == 0 && !gstate && !any_act && nmax <= 128 && !(wvenv && atoi(wvenv) == 0) &&
            lds_bytes(sides, pcap, nmax, 0, 1) <= kLdsMax;
   if (c.wave) c.narrow = c.lowlat = c.cu = false;
   c.waves = c.cu ? (uint32_t)std::max(sides == 1 ? wcu::engine_waves() : wcv::engine_waves(), kWaves) : (uint32_t)kWaves;
@@ -859,7 +861,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
       d.max_read_len = s.max_len;
       d.n_active = s.n_active;
       d.max_act = s.max_act;
-      qp[seq % kQcap] = d;
+        qp[seq % kQcap] = d;
       for (size_t r = 0; r < s.gid.size(); ++r) {
         const uint64_t q = (rw + r) % kQslots;
         qroff[q] = b->roff_h[s.gid[r]];

@@ -232,7 +232,9 @@ __device__ inline void wave_select_t0(const DevConfig& cfg, Lo<Ctl>& ctl, const 
   ctl.nchild = nc;
 }
 
-template <int R>
+// (V: the kernel it is called from, so that each kernel's call has a body
+// compiled for that kernel's register budget)
+template <int R, int V>
 __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t op,
                                        uint32_t top, uint32_t tdual_u, uint32_t a0, uint32_t a1, uint32_t a2,
                                        uint32_t a3, uint32_t a4) {
@@ -411,11 +413,14 @@ struct LaneReads {  // (R <= 2)
 // in LDS, thread 0 read and wrote each of them with a full LDS round trip, one
 // after the other. The general path (wave_rare) still reads Ctl, so the
 // fields it uses are synced around each call.
+// Lengths, queue sizes and per-problem pop counts fit 32 bits (fewer SGPRs:
+// the pop loop's uniform state spilled into VGPR lanes); the pop counters go
+// to Ctl before they could wrap, lastc saturates.
 struct WCtl {
   uint32_t heap_n, nfree, hot, hot_dual, am_len, n_ret, status;
   uint64_t max_err;
-  uint64_t far[2], lastc[2], total[2], thr[2];
-  uint64_t pops, explored, ignored, peakq, updates, w_out, compares;
+  uint32_t far[2], lastc[2], total[2], thr[2];
+  uint32_t pops, explored, ignored, peakq;
 };
 __device__ __forceinline__ void wctl_to_ctl(const WCtl& W, Lo<Ctl>& ctl) {
   if (threadIdx.x == 0) {
@@ -433,6 +438,22 @@ __device__ __forceinline__ void wctl_from_ctl(WCtl& W, Lo<Ctl>& ctl) {
   W.max_err = ((uint64_t)uni((uint32_t)(ctl.max_err >> 32)) << 32) | uni((uint32_t)ctl.max_err);
   W.status = uni(ctl.status);
   W.hot = uni(ctl.hot_slot);
+}
+// the pop counters (uniform) and the lanes' work counters into Ctl's u64
+// counters: every 16,384 pops (a lane's w_out grows by at most 2 wcap + 1 per
+// pop) and at the end of the problem
+__device__ __forceinline__ void wave_flush_counters(Lo<Ctl>& ctl, WCtl& W, uint32_t (&lcnt)[3]) {
+  const uint32_t u = wave_sum_u32(lcnt[0]), wo = wave_sum_u32(lcnt[1]), cm = wave_sum_u32(lcnt[2]);
+  if (threadIdx.x == 0) {
+    ctl.cnt[S_POPS] += W.pops;
+    ctl.cnt[S_EXPLORED] += W.explored;
+    ctl.cnt[S_IGNORED] += W.ignored;
+    ctl.cnt[S_UPDATES] += u;
+    ctl.cnt[S_WOUT] += wo;
+    ctl.cnt[S_COMPARES] += cm;
+  }
+  W.pops = W.explored = W.ignored = 0;
+  lcnt[0] = lcnt[1] = lcnt[2] = 0;
 }
 // priority-queue 1.x on the LDS heap with the size in a register: the
 // reference's sift rules (strict comparisons), with the
@@ -540,10 +561,11 @@ __device__ __forceinline__ HeapEntry heap_uni(const HeapEntry& e) {
 // no activate_dual): pushes on the hot state, ED increases through the slot
 // (out of line), prune + cost + Some counts in one lane pass; new tip bytes
 // into tx. Returns the child's cost; its metadata goes to the slot. ----
-template <int R>
+template <int R, int V>
 __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs kp, WCtl& W, uint32_t top,
                                                    const SlotMeta& tm, bool tdual, uint32_t kind, const int (&sy)[2],
-                                                   const LaneReads<R>& lr, Tips (&tx)[R][2], uint32_t (&nl)[2]) {
+                                                   const LaneReads<R>& lr, Tips (&tx)[R][2], uint32_t (&nl)[2],
+                                                   uint32_t (&lcnt)[3]) {
   const int lane = lane_id();
   const DevConfig& cfg = E.cfg;
   const bool early = cfg.early != 0;
@@ -608,9 +630,10 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
       nheavy += (uint32_t)__popcll((unsigned long long)hm);
     }
   }
-  W.updates += wave_sum_u32(upd);
-  W.w_out += wave_sum_u32(wout);
-  W.compares += wave_sum_u32(cmps);
+  // (per-lane work counters, summed over the wave once per problem)
+  lcnt[0] += upd;
+  lcnt[1] += wout;
+  lcnt[2] += cmps;
   SUB_T1(48, t_pl);  // (push: the lane pass and its counters)
   if (nheavy) {
     // the ED-increase loops, out of line; then the rebuilt states and their
@@ -623,7 +646,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
       ctl.ovf = 0;
     }
     __syncthreads();
-    wave_rare<R>(kp, E.P, (Sh<uint8_t>*)E.L.hot, ctl, WR_HEAVY, top, tdual, nl[0], nl[1], (uint32_t)sy[0],
+    wave_rare<R, V>(kp, E.P, (Sh<uint8_t>*)E.L.hot, ctl, WR_HEAVY, top, tdual, nl[0], nl[1], (uint32_t)sy[0],
                  (uint32_t)sy[1], 0);
     SUB_T1(54, t_hv);
     const uint32_t ovf = uni(ctl.ovf);
@@ -675,8 +698,9 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
     c1 += e2 != kInactive;
   }
   cost = wave_sum_u64(cost);
-  m.nsome[0] = wave_sum_u32(c0);
-  m.nsome[1] = wave_sum_u32(c1);
+  const uint32_t cc = wave_sum_u32(c0 | (c1 << 16));  // (<= 128 reads a side)
+  m.nsome[0] = cc & 0xFFFFu;
+  m.nsome[1] = cc >> 16;
   if (lane == 0) meta_put(E.L.meta[top], m);
   SUB_T1(49, t_pc);  // (push: prune, cost, Some counts)
   return cost;
@@ -769,81 +793,97 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
       }
     }
   }
-  // two passes over the distinct keys (single-symbol voters by ballots, then
-  // the symbols of multi-symbol voters not seen yet): sums, then the threshold
+  // the distinct keys one at a time (single-symbol voters first, by ballots;
+  // then the symbols of multi-symbol voters not counted yet, lanes in
+  // parallel), each with its vote in eighths; lane k keeps key k and its vote
+  // for the threshold pass. The order of the keys decides nothing here.
+  uint64_t rem[R];
+  uint32_t mrem[R];  // per lane: its multi-symbol slots not counted yet
+  uint32_t mul[R];   // per lane: 8 / split (eighths per occurrence)
+  bool any_multi = false;
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    SymSet seen = {0, 0, 0, 0};
-    uint64_t rem[R], mrem[R];
+  for (int j = 0; j < R; ++j) {
+    rem[j] = ballot(ys[j] != 0x100u);
+    mrem[j] = 0;
+    mul[j] = 8u >> (__builtin_ctz(mn[j].split | 256u) & 3u);
+    if ((mmask[j] >> lane_id()) & 1ull) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if ((((k < 4 ? mn[j].occ_lo : mn[j].occ_hi) >> (8 * (k & 3))) & 0xFFu) != 0u) mrem[j] |= 1u << k;
+    }
+    any_multi |= mmask[j] != 0;
+  }
+  uint32_t tkey = 0x100u, tc8 = 0;  // lane k: key k and its vote
+  for (;;) {
+    uint32_t key = 0x100u;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (key == 0x100u && rem[j]) key = (uint32_t)__builtin_amdgcn_readlane((int)ys[j], __builtin_ctzll(rem[j]));
+    if (key == 0x100u && any_multi) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const uint64_t lm = ballot(mrem[j] != 0u);
+        if (key == 0x100u && lm) {
+          const int l = __builtin_ctzll(lm);
+          const uint32_t k = (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)mrem[j], l));
+          const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)(k < 4 ? mn[j].lo : mn[j].hi), l);
+          key = (w >> (8 * (k & 3))) & 0xFFu;
+        }
+      }
+    }
+    if (key == 0x100u) break;
+    uint32_t c8 = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      rem[j] = ballot(ys[j] != 0x100u);
-      mrem[j] = mmask[j];
+      const uint64_t m = ballot(ys[j] == key);
+      c8 += 8u * (uint32_t)__popcll((unsigned long long)m);
+      rem[j] &= ~m;
     }
-    uint32_t mk = 0;  // next symbol index within the current multi-symbol lane
-    for (;;) {
-      uint32_t key = 0x100u;
+    if (any_multi) {
+      uint32_t mine = 0;
 #pragma unroll
-      for (int j = 0; j < R; ++j)
-        if (key == 0x100u && rem[j]) key = (uint32_t)__builtin_amdgcn_readlane((int)ys[j], __builtin_ctzll(rem[j]));
-      if (key == 0x100u) {
+      for (int j = 0; j < R; ++j) {
+        uint32_t occ = 0;
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
-          while (key == 0x100u && mrem[j]) {
-            const int l = __builtin_ctzll(mrem[j]);
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].lo, l);
-            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].hi, l);
-            const uint32_t olo = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].occ_lo, l);
-            const uint32_t ohi = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].occ_hi, l);
-            for (; mk < 8 && key == 0x100u; ++mk) {
-              const uint32_t ok = ((mk < 4 ? olo : ohi) >> (8 * (mk & 3))) & 0xFFu;
-              const uint32_t sk = ((mk < 4 ? lo : hi) >> (8 * (mk & 3))) & 0xFFu;
-              if (ok && !seen.has(sk)) key = sk;
-            }
-            if (mk >= 8) {
-              mrem[j] &= mrem[j] - 1;
-              mk = 0;
-            }
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t sk = ((k < 4 ? mn[j].lo : mn[j].hi) >> (8 * (k & 3))) & 0xFFu;
+          if (((mrem[j] >> k) & 1u) && sk == key) {
+            occ += ((k < 4 ? mn[j].occ_lo : mn[j].occ_hi) >> (8 * (k & 3))) & 0xFFu;
+            mrem[j] &= ~(1u << k);
           }
         }
+        mine += occ * mul[j];
       }
-      if (key == 0x100u) break;
-      seen.add(key);
-#pragma unroll
-      for (int j = 0; j < R; ++j) rem[j] &= ~ballot(ys[j] == key);
-      const uint32_t c8 = votes8<R>(key, ys, mmask, mn);
-      const bool is_wc = wc >= 0 && key == (uint32_t)(uint8_t)wc;
-      if (pass == 0) {
-        nk++;
-        total8 += c8;
-        mx_all = max(mx_all, c8);
-        if (is_wc) {
-          wc_in = true;
-          wc8 = c8;
-        } else {
-          mx_nowc = max(mx_nowc, c8);
-        }
-      } else {
-        if (drop && is_wc) continue;
-        if (!((double)c8 * 0.125 < thr)) {
-          np++;
-          pk = (int)key;
-        }
-        if (!is_wc) {
-          ns++;
-          if ((double)c8 * 0.125 >= (double)mc) npmc++;
-        }
-      }
+      c8 += wave_sum_u32(mine);
     }
-    if (pass == 0) {
-      drop = wc_in && nk > 1;
-      nko = drop ? nk - 1 : nk;
-      const uint32_t sum8 = drop ? total8 - wc8 : total8;
-      const uint32_t mx8 = drop ? mx_nowc : mx_all;
-      mc = max(cfg.min_count, ceil_u64(cfg.min_af * ((double)sum8 * 0.125)));
-      thr = nko ? fmin((double)mc, (double)mx8 * 0.125) : (double)mc;
+    if (lane_id() == (int)nk) {
+      tkey = key;
+      tc8 = c8;
+    }
+    nk++;
+    total8 += c8;
+    mx_all = max(mx_all, c8);
+    if (wc >= 0 && key == (uint32_t)(uint8_t)wc) {
+      wc_in = true;
+      wc8 = c8;
+    } else {
+      mx_nowc = max(mx_nowc, c8);
     }
   }
+  drop = wc_in && nk > 1;
+  nko = drop ? nk - 1 : nk;
+  const uint32_t sum8 = drop ? total8 - wc8 : total8;
+  const uint32_t mx8 = drop ? mx_nowc : mx_all;
+  mc = max(cfg.min_count, ceil_u64(cfg.min_af * ((double)sum8 * 0.125)));
+  thr = nko ? fmin((double)mc, (double)mx8 * 0.125) : (double)mc;
+  // the threshold pass (:520-552, :655-679), key k on lane k
+  const bool is_wc = wc >= 0 && tkey == (uint32_t)(uint8_t)wc;
+  const bool valid = lane_id() < (int)nk && !(drop && is_wc);
+  const uint64_t pm = ballot(valid && !((double)tc8 * 0.125 < thr));
+  np = (uint32_t)__popcll((unsigned long long)pm);
+  pk = pm ? (int)__builtin_amdgcn_readlane((int)tkey, __builtin_ctzll(pm)) : -1;
+  ns = (uint32_t)__popcll((unsigned long long)ballot(valid && !is_wc));
+  npmc = (uint32_t)__popcll((unsigned long long)ballot(valid && !is_wc && (double)tc8 * 0.125 >= (double)mc));
   return SideVotes{np, nko, pk, npmc > 1 && ns > 1};
 }
 
@@ -856,20 +896,349 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
 // hashbrown order of the keys decides nothing), the lane push. Anything else
 // goes to wave_rare's WR_GENERAL*, the block engines' code for the rest of
 // the pop.
-template <int R>
-__device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* smem, Lo<Ctl>& ctl) {
-  const int tid = threadIdx.x;
+template <int R, int V>
+__device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl>& ctl, uint32_t prob, uint32_t oslot,
+                                             Gm<uint8_t>* outp) {
   const int lane = lane_id();
   const DevConfig& cfg = A.cfg;
   const bool early = cfg.early != 0;
   const bool weighted = cfg.weighted != 0;
-  Eng E = make_eng(A, state_base(A, smem));
   Sh<RInfo>* R0 = E.L.rinfo;
   Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
   Tips tx[R][2];
 #pragma unroll
   for (int j = 0; j < R; ++j) tx[j][0] = tx[j][1] = Tips{0, 0, 0};
+  const uint64_t full_min = max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.n));
+  // active_min_count (:497-513) without activations: the root's count at
+  // every length below am_len
+  const uint64_t am0 = full_min;
+  bool tips_ok = false;  // tx holds the hot node's tip bytes
+  // (written out: a loop here was not unrolled, which would leave lr in scratch)
+  LaneReads<R> lr;
+  {
+    const uint32_t r0 = (uint32_t)lane;
+    lr.rd[0] = E.rbytes + (r0 < E.n ? E.roff[E.P.read_begin + r0] : 0ull);
+    lr.bl[0] = r0 < E.n ? E.rlenp[E.P.read_begin + r0] : 0u;
+    if constexpr (R > 1) {
+      const uint32_t r1 = (uint32_t)lane + 64u;
+      lr.rd[R - 1] = E.rbytes + (r1 < E.n ? E.roff[E.P.read_begin + r1] : 0ull);
+      lr.bl[R - 1] = r1 < E.n ? E.rlenp[E.P.read_begin + r1] : 0u;
+    }
+  }
+  const KArgs kp = kernel_args();
+  Sh<uint8_t>* const sbase = (Sh<uint8_t>*)E.L.hot;
+  // init_problem left: the root in the heap and tracker 0, slot 0 taken
+  WCtl W;
+  W.heap_n = 1;
+  W.nfree = E.pcap - 1;
+  W.hot = kNoSlot;
+  W.hot_dual = 0;
+  W.am_len = 1;
+  W.n_ret = 0;
+  W.status = ST_OK;
+  W.max_err = ~0ull;
+  W.far[0] = W.far[1] = W.lastc[0] = W.lastc[1] = W.thr[0] = W.thr[1] = 0;
+  W.total[0] = 1;
+  W.total[1] = 0;
+  W.pops = W.explored = W.ignored = W.peakq = 0;
+  uint32_t lcnt[3] = {0, 0, 0};  // this lane's updates, w_out, compares (wave_push_fast)
+  const uint64_t L2 = E.lcap + 2;
+  Gm<uint32_t>* const lc[2] = {E.trk, E.trk + 2 * L2};
+  Gm<uint32_t>* const pc[2] = {E.trk + L2, E.trk + 3 * L2};
+  const uint64_t cap = cfg.max_capacity_per_size;
+  // the tracker limits against 32-bit totals (a total above 2^32 - 1 never exceeds a larger limit)
+  const uint32_t mqs32 = (uint32_t)min(cfg.max_queue_size, (uint64_t)0xFFFFFFFFu);
+  const uint32_t mnc32 = (uint32_t)min(cfg.max_nodes_wo_constraint, (uint64_t)0xFFFFFFFFu);
 
+  for (;;) {
+    // ---- pop (dual_consensus.rs:340-397) ----
+    if (W.heap_n == 0) break;
+    SUB_T0(t_pl);
+    const uint32_t plen = uni(E.L.heap[0].len);
+    // the processed counts of the top's length, loaded first (HBM, under
+    // one wait) while the threshold walks and the sift run
+    const uint32_t pc_pre0 = trk_load(&pc[0][WC_IX(plen, L2)]), pc_pre1 = trk_load(&pc[1][WC_IX(plen, L2)]);
+    const uint64_t am = plen < W.am_len ? am0 : 0;
+    W.peakq = max(W.peakq, W.heap_n);
+    if (W.pops >= 0x4000u) {  // (the 32-bit counters into Ctl, long before they could wrap)
+      wave_flush_counters(ctl, W, lcnt);
+    }
+    W.pops++;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      while ((W.total[k] > mqs32 || W.lastc[k] >= mnc32) && W.thr[k] < W.far[k]) {
+        W.total[k] -= uni(trk_load(&lc[k][WC_IX(W.thr[k], L2)]));  // increment_threshold
+        W.thr[k]++;
+        W.lastc[k] = 0;
+      }
+    }
+    SUB_T1(45, t_pl);  // (pop-logic: to the heap pop)
+    SUB_T0(t_hp);
+    W.heap_n--;
+    const HeapEntry top = wheap_pop(E.L.heap, W.heap_n);
+    SUB_T1(46, t_hp);  // (pop-logic: the heap pop)
+    SUB_T0(t_pc);
+    const SlotMeta tm = meta_get(E.L.meta[top.slot]);
+    const uint32_t dual = uni(tm.flags) & 1u;
+    const uint32_t ns0 = uni(tm.nsome[0]), ns1 = uni(tm.nsome[1]);
+    // tracker(dual).remove(len)
+    if (lane == 0) atomicSub((uint32_t*)&lc[dual][WC_IX(top.len, L2)], 1u);
+    if (top.len >= W.thr[dual]) W.total[dual]--;
+    const bool imbalanced = dual && (ns0 < am || ns1 < am);
+    if (top.len >= W.am_len) W.status = WC_E_INVARIANT_CODE;
+    SUB_T1(47, t_pc);  // (pop-logic: metadata, tracker)
+    // the node is ignored (:372-386) when it costs more than the best result,
+    // lies below its tracker's threshold, is imbalanced, or its length is at
+    // capacity; the capacity check waits for the processed count's load and
+    // comes after the analysis below (nothing before it has an effect that
+    // outlives an ignored node), so that load's latency overlaps it
+    const bool ign = top.cost > W.max_err || top.len < W.thr[dual] || imbalanced;
+    if (ign) {
+      if (A.trace && lane == 0) trace_pop(A, prob, top, dual | (1u << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
+      W.ignored++;
+      if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = top.slot;
+      W.nfree++;
+      if (top.slot == W.hot) W.hot = kNoSlot;  // its state is dropped with the slot
+      continue;
+    }
+    PH_MARK(13);
+
+    const uint32_t topslot = top.slot;
+    const uint32_t tlen = top.len;
+    const bool tdual = dual != 0;
+    const uint32_t tlens[2] = {uni(tm.len[0]), uni(tm.len[1])};
+    const uint32_t tflags = uni(tm.flags);
+    SUB_T0(t_hot);
+    if (topslot != W.hot) {
+      SUB_CNT(33, 1);
+      // the previous hot node, still queued, goes back to its slot first
+      if (W.hot != kNoSlot) hot_writeback<R>(E, W.hot, W.hot_dual != 0);
+      hot_fetch_slot<R>(E, topslot, tdual);
+      tips_ok = false;
+      W.hot = topslot;
+      W.hot_dual = tdual ? 1u : 0u;
+    }
+    SUB_T1(32, t_hot);
+
+    // ---- analysis of both sides from the hot state: thread_analyze on the
+    // prefetched tip bytes; the nominations also go to RInfo (the general
+    // path reads them there) ----
+    SUB_T0(t_an);
+    uint32_t ys[2][R];  // the read's one nominated symbol (0x100: none, several, or not a voter)
+    uint64_t mmask[2][R];  // lanes whose read nominates several symbols
+    MultiNom mn[2][R];
+    bool any_wide = false, any_end = false, any_multi = false, odd_split = false;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t r = (uint32_t)lane + 64u * j;
+      const bool live = r < E.n;
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        ys[sd][j] = 0x100u;
+        mn[sd][j] = MultiNom{0, 0, 0, 0, 1};
+        bool wide = false, end = false, multi = false;
+        if (live && (sd == 0 || tdual)) {
+          Sh<RInfo>* out = (sd ? R1 : R0) + r;
+          const RRaw s = rstate_load(&E.L.hot[sd * E.nmax + r]);
+          if (rraw_e(s) == kInactive) {
+            out->e = kInactive;
+            out->n = 0;
+            out->end = 0;
+          } else if (rraw_flags(s) & kWide) {
+            wide = true;
+          } else {
+            Front f;
+            front_load(s, f);
+            if (!tips_ok) tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], tlens[sd]);
+            uint32_t x[kF];
+            tips_unpack(tx[j][sd], x);
+            const Nom o = nominate_tips(f, x, lr.bl[j]);
+            rinfo_store(out, o, f.e);
+            end = o.end != 0;
+            multi = o.n > 1;
+            if (o.n == 1) ys[sd][j] = byte_at(o.sym, 0);
+            if (multi) {
+              mn[sd][j] = MultiNom{(uint32_t)o.sym, (uint32_t)(o.sym >> 32), (uint32_t)o.occ,
+                                   (uint32_t)(o.occ >> 32), o.split};
+              if (o.split > 8u || (o.split & (o.split - 1u))) odd_split = true;
+            }
+          }
+        }
+        mmask[sd][j] = ballot(multi);
+        any_wide |= ballot(wide) != 0;
+        any_end |= ballot(end) != 0;
+        any_multi |= mmask[sd][j] != 0;
+      }
+    }
+    odd_split = ballot(odd_split) != 0;
+    tips_ok = true;
+    SUB_T1(34, t_an);
+    {
+      const bool at_cap = uni(dual ? pc_pre1 : pc_pre0) >= cap;
+      if (A.trace && lane == 0)
+        trace_pop(A, prob, top, dual | ((at_cap ? 1u : 0u) << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
+      if (at_cap) {
+        W.ignored++;
+        if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = topslot;
+        W.nfree++;
+        W.hot = kNoSlot;  // (the hot node: its state is dropped with the slot)
+        continue;
+      }
+    }
+    W.far[dual] = max(W.far[dual], top.len);
+    W.lastc[dual] += W.lastc[dual] != 0xFFFFFFFFu;
+    if (lane == 0) atomicAdd((uint32_t*)&pc[dual][WC_IX(top.len, L2)], 1u);  // process_unchecked
+    W.explored++;
+    if (W.status != ST_OK) break;
+    // active_min_count growth (:497-513): the count at every new length is
+    // the root's (no activation in this build)
+    if (W.am_len == tlen + 1 && tlen + 1 < E.lcap + 2) W.am_len++;
+    PH_MARK(1);
+
+    uint32_t nchild = 2;  // (0 or 1: decided on the lean path)
+    int child[2] = {-1, -1};
+    uint32_t kind = tdual ? 0u : 1u;
+    uint32_t nc = 1;
+    uint64_t ccost = 0;
+    uint32_t clen = 0;
+    bool general = false;  // children from Ctl (the block engines' passes)
+    if (any_wide || any_end) {
+      // wide frontiers or a read at a consensus end (finalize, reached_*):
+      // the block engines' code for the rest of the pop, from the slot
+      SUB_CNT(35, 1);
+      if (lane == 0) {
+        ctl.n_end[0] = ctl.n_end[1] = 0;
+        ctl.n_either = 0;
+        ctl.nheavy = 0;
+        ctl.ovf = 0;
+        ctl.multi[0] = ctl.multi[1] = 0;
+      }
+      wctl_to_ctl(W, ctl);
+      wave_rare<R, V>(kp, E.P, sbase, ctl, WR_GENERAL_POP, topslot, tdual, (uint32_t)full_min,
+                   (uint32_t)(full_min >> 32), oslot, 0, 0);
+      wctl_from_ctl(W, ctl);
+      W.hot = kNoSlot;
+      if (W.status != ST_OK) break;
+      nc = uni(ctl.nchild);
+      general = true;
+    } else {
+      if (!weighted && !odd_split) {
+        // ---- votes and selection on the lean path ----
+        SUB_T0(t_v);
+        const SideVotes sv0 = wave_side_votes<R>(cfg, ys[0], mmask[0], mn[0]);
+        SideVotes sv1 = {0, 0, -1, false};
+        if (tdual) sv1 = wave_side_votes<R>(cfg, ys[1], mmask[1], mn[1]);
+        uint32_t npass[2] = {sv0.npass, sv1.npass};
+        const uint32_t nkeys[2] = {sv0.nkeys, sv1.nkeys};
+        const int pkey[2] = {sv0.pk, sv1.pk};
+        if (tdual) {
+          // options per side: None first (consensus end, no keys, locked),
+          // then the passing keys; children = pairs but (None, None)
+          // (dual_consensus.rs:554-650)
+          bool has_none[2];
+          uint32_t no[2];
+#pragma unroll
+          for (int sd = 0; sd < 2; ++sd) {
+            const bool lock = (tflags & (sd == 0 ? 2u : 4u)) != 0;
+            const bool fin = early && (sd == 0 ? ns0 : ns1) == 0;  // (no read at its end here)
+            has_none[sd] = fin || nkeys[sd] == 0 || lock;
+            if (lock) npass[sd] = 0;
+            no[sd] = (has_none[sd] ? 1u : 0u) + npass[sd];
+          }
+          nchild = no[0] * no[1] - ((has_none[0] && has_none[1]) ? 1u : 0u);
+          child[0] = npass[0] ? pkey[0] : -1;
+          child[1] = npass[1] ? pkey[1] : -1;
+        } else {
+          // stay-single children, and split children from every pair of
+          // candidates when two pass min_count (:655-734)
+          nchild = npass[0] + (sv0.split ? 2u : 0u);
+          child[0] = pkey[0];
+        }
+        SUB_T1(38, t_v);
+      }
+      if (nchild >= 2) {
+        // weighted votes, splits that round, or several children (their
+        // order): the block engines' votes and selection (from RInfo)
+        SUB_CNT((weighted || odd_split) ? 36 : 39, 1);
+        if (lane == 0) {
+          ctl.ovf = 0;
+          ctl.multi[0] = ctl.multi[1] = any_multi ? 1u : 0u;
+          ctl.fin[0] = early && ns0 == 0;
+          ctl.fin[1] = tdual && early && ns1 == 0;
+          ctl.status = W.status;
+        }
+        __syncthreads();
+        wave_rare<R, V>(kp, E.P, sbase, ctl, WR_VOTES_SELECT, topslot, tdual, 0, 0, 0, 0, 0);
+        W.status = uni(ctl.status);
+        if (W.status != ST_OK) break;
+        nchild = uni(ctl.nchild);
+        if (nchild == 1) {
+          child[0] = uni((int32_t)ctl.ch_s[0][0]);
+          child[1] = uni((int32_t)ctl.ch_s[0][1]);
+          kind = uni((uint32_t)ctl.ch_kind[0]);
+        }
+      }
+      if (nchild == 0) {
+        if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = topslot;
+        W.nfree++;
+        W.hot = kNoSlot;
+        PH_MARK(3);
+        continue;
+      }
+      if (tlens[0] + 1 > E.lcap || tlens[1] + 1 > E.lcap) {
+        W.status = ST_RETRY | ST_RETRY_LCAP;
+        break;
+      }
+      PH_MARK(3);
+      if (nchild == 1 && kind != 2) {
+        SUB_CNT(37, 1);
+        uint32_t nl[2];
+        ccost = wave_push_fast<R, V>(E, ctl, kp, W, topslot, tm, tdual, kind, child, lr, tx, nl, lcnt);
+        clen = max(nl[0], nl[1]);
+        if (W.status != ST_OK) break;
+        PH_MARK(11);
+      } else {
+        // clones, activate_dual: dual_build_children from the slot
+        wctl_to_ctl(W, ctl);
+        wave_rare<R, V>(kp, E.P, sbase, ctl, WR_CHILDREN, topslot, tdual, 0, 0, 0, 0, 0);
+        wctl_from_ctl(W, ctl);
+        W.hot = kNoSlot;
+        if (W.status != ST_OK) break;
+        nc = nchild;
+        general = true;
+      }
+    }
+    // ---- the children into the queue and their trackers ----
+    for (uint32_t c = 0; c < nc; ++c) {
+      uint32_t cslot = topslot;
+      if (general) {
+        cslot = uni(ctl.ch_slot[c]);
+        ccost = ((uint64_t)uni((uint32_t)(ctl.ch_cost[c] >> 32)) << 32) | uni((uint32_t)ctl.ch_cost[c]);
+        clen = uni(ctl.ch_len[c]);
+      }
+      const uint32_t k = !general ? (tdual ? 1u : 0u) : ((uni(E.L.meta[cslot].flags) & 1u) ? 1u : 0u);
+      if (lane == 0) atomicAdd((uint32_t*)&lc[k][WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
+      if (clen >= W.thr[k]) W.total[k]++;
+      wheap_push(E.L.heap, W.heap_n, HeapEntry{ccost, clen, cslot});
+      W.heap_n++;
+    }
+    PH_MARK(7);
+  }
+  wave_flush_counters(ctl, W, lcnt);
+  // the register state back into Ctl for finish_problem
+  if (lane == 0) {
+    ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)W.peakq);
+  }
+  wctl_to_ctl(W, ctl);
+  finish_problem(A, ctl, outp, prob, oslot);
+}
+
+// the claim loop: every problem on the build of its read count (R = 1 for
+// <= 64 reads, 2 for <= 128) when `mixed`, else on R's
+template <int R, bool mixed>
+__device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* smem, Lo<Ctl>& ctl) {
+  const int tid = threadIdx.x;
+  Eng E = make_eng(A, state_base(A, smem));
   if (tid == 0) ctl.obuf = 1;
   for (;;) {
     uint32_t oslot = 0;
@@ -885,313 +1254,8 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
       finish_problem(A, ctl, outp, prob, oslot);
       continue;
     }
-    const uint64_t full_min = max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.n));
-    // active_min_count (:497-513) without activations: the root's count at
-    // every length below am_len
-    const uint64_t am0 = full_min;
-    bool tips_ok = false;  // tx holds the hot node's tip bytes
-    // (written out: a loop here was not unrolled, which would leave lr in scratch)
-    LaneReads<R> lr;
-    {
-      const uint32_t r0 = (uint32_t)lane;
-      lr.rd[0] = E.rbytes + (r0 < E.n ? E.roff[E.P.read_begin + r0] : 0ull);
-      lr.bl[0] = r0 < E.n ? E.rlenp[E.P.read_begin + r0] : 0u;
-      if constexpr (R > 1) {
-        const uint32_t r1 = (uint32_t)lane + 64u;
-        lr.rd[R - 1] = E.rbytes + (r1 < E.n ? E.roff[E.P.read_begin + r1] : 0ull);
-        lr.bl[R - 1] = r1 < E.n ? E.rlenp[E.P.read_begin + r1] : 0u;
-      }
-    }
-    const KArgs kp = kernel_args();
-    Sh<uint8_t>* const sbase = (Sh<uint8_t>*)E.L.hot;
-    // init_problem left: the root in the heap and tracker 0, slot 0 taken
-    WCtl W;
-    W.heap_n = 1;
-    W.nfree = E.pcap - 1;
-    W.hot = kNoSlot;
-    W.hot_dual = 0;
-    W.am_len = 1;
-    W.n_ret = 0;
-    W.status = ST_OK;
-    W.max_err = ~0ull;
-    W.far[0] = W.far[1] = W.lastc[0] = W.lastc[1] = W.thr[0] = W.thr[1] = 0;
-    W.total[0] = 1;
-    W.total[1] = 0;
-    W.pops = W.explored = W.ignored = W.peakq = W.updates = W.w_out = W.compares = 0;
-    const uint64_t L2 = E.lcap + 2;
-    Gm<uint32_t>* const lc[2] = {E.trk, E.trk + 2 * L2};
-    Gm<uint32_t>* const pc[2] = {E.trk + L2, E.trk + 3 * L2};
-    const uint64_t cap = cfg.max_capacity_per_size;
-
-    for (;;) {
-      // ---- pop (dual_consensus.rs:340-397) ----
-      if (W.heap_n == 0) break;
-      SUB_T0(t_pl);
-      const uint32_t plen = uni(E.L.heap[0].len);
-      // the processed counts of the top's length, loaded first (HBM, under
-      // one wait) while the threshold walks and the sift run
-      const uint32_t pc_pre0 = trk_load(&pc[0][WC_IX(plen, L2)]), pc_pre1 = trk_load(&pc[1][WC_IX(plen, L2)]);
-      const uint64_t am = plen < W.am_len ? am0 : 0;
-      W.peakq = max(W.peakq, (uint64_t)W.heap_n);
-      W.pops++;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        while ((W.total[k] > cfg.max_queue_size || W.lastc[k] >= cfg.max_nodes_wo_constraint) && W.thr[k] < W.far[k]) {
-          W.total[k] -= uni(trk_load(&lc[k][WC_IX(W.thr[k], L2)]));  // increment_threshold
-          W.thr[k]++;
-          W.lastc[k] = 0;
-        }
-      }
-      SUB_T1(45, t_pl);  // (pop-logic: to the heap pop)
-      SUB_T0(t_hp);
-      W.heap_n--;
-      const HeapEntry top = wheap_pop(E.L.heap, W.heap_n);
-      SUB_T1(46, t_hp);  // (pop-logic: the heap pop)
-      SUB_T0(t_pc);
-      const SlotMeta tm = meta_get(E.L.meta[top.slot]);
-      const uint32_t dual = uni(tm.flags) & 1u;
-      const uint32_t ns0 = uni(tm.nsome[0]), ns1 = uni(tm.nsome[1]);
-      // tracker(dual).remove(len)
-      if (lane == 0) atomicSub((uint32_t*)&lc[dual][WC_IX(top.len, L2)], 1u);
-      if (top.len >= W.thr[dual]) W.total[dual]--;
-      const bool imbalanced = dual && (ns0 < am || ns1 < am);
-      if (top.len >= W.am_len) W.status = WC_E_INVARIANT_CODE;
-      const bool at_cap = uni(dual ? pc_pre1 : pc_pre0) >= cap;
-      SUB_T1(47, t_pc);  // (pop-logic: metadata, tracker, the processed count)
-      if (A.trace && lane == 0) {
-        const uint32_t act = (top.cost > W.max_err || top.len < W.thr[dual] || at_cap || imbalanced) ? 1u : 0u;
-        trace_pop(A, prob, top, dual | (act << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
-      }
-      if (top.cost > W.max_err || top.len < W.thr[dual] || at_cap || imbalanced) {
-        W.ignored++;
-        if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = top.slot;
-        W.nfree++;
-        if (top.slot == W.hot) W.hot = kNoSlot;  // its state is dropped with the slot
-        continue;
-      }
-      W.far[dual] = max(W.far[dual], (uint64_t)top.len);
-      W.lastc[dual]++;
-      if (lane == 0) atomicAdd((uint32_t*)&pc[dual][WC_IX(top.len, L2)], 1u);  // process_unchecked
-      W.explored++;
-      if (W.status != ST_OK) break;
-      PH_MARK(13);
-
-      const uint32_t topslot = top.slot;
-      const uint32_t tlen = top.len;
-      const bool tdual = dual != 0;
-      const uint32_t tlens[2] = {uni(tm.len[0]), uni(tm.len[1])};
-      const uint32_t tflags = uni(tm.flags);
-      SUB_T0(t_hot);
-      if (topslot != W.hot) {
-        SUB_CNT(33, 1);
-        // the previous hot node, still queued, goes back to its slot first
-        if (W.hot != kNoSlot) hot_writeback<R>(E, W.hot, W.hot_dual != 0);
-        hot_fetch_slot<R>(E, topslot, tdual);
-        tips_ok = false;
-        W.hot = topslot;
-        W.hot_dual = tdual ? 1u : 0u;
-      }
-      SUB_T1(32, t_hot);
-
-      // ---- analysis of both sides from the hot state: thread_analyze on the
-      // prefetched tip bytes; the nominations also go to RInfo (the general
-      // path reads them there) ----
-      SUB_T0(t_an);
-      uint32_t ys[2][R];  // the read's one nominated symbol (0x100: none, several, or not a voter)
-      uint64_t mmask[2][R];  // lanes whose read nominates several symbols
-      MultiNom mn[2][R];
-      bool any_wide = false, any_end = false, any_multi = false, odd_split = false;
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const uint32_t r = (uint32_t)lane + 64u * j;
-        const bool live = r < E.n;
-#pragma unroll
-        for (int sd = 0; sd < 2; ++sd) {
-          ys[sd][j] = 0x100u;
-          mn[sd][j] = MultiNom{0, 0, 0, 0, 1};
-          bool wide = false, end = false, multi = false;
-          if (live && (sd == 0 || tdual)) {
-            Sh<RInfo>* out = (sd ? R1 : R0) + r;
-            const RRaw s = rstate_load(&E.L.hot[sd * E.nmax + r]);
-            if (rraw_e(s) == kInactive) {
-              out->e = kInactive;
-              out->n = 0;
-              out->end = 0;
-            } else if (rraw_flags(s) & kWide) {
-              wide = true;
-            } else {
-              Front f;
-              front_load(s, f);
-              if (!tips_ok) tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], tlens[sd]);
-              uint32_t x[kF];
-              tips_unpack(tx[j][sd], x);
-              const Nom o = nominate_tips(f, x, lr.bl[j]);
-              rinfo_store(out, o, f.e);
-              end = o.end != 0;
-              multi = o.n > 1;
-              if (o.n == 1) ys[sd][j] = byte_at(o.sym, 0);
-              if (multi) {
-                mn[sd][j] = MultiNom{(uint32_t)o.sym, (uint32_t)(o.sym >> 32), (uint32_t)o.occ,
-                                     (uint32_t)(o.occ >> 32), o.split};
-                if (o.split > 8u || (o.split & (o.split - 1u))) odd_split = true;
-              }
-            }
-          }
-          mmask[sd][j] = ballot(multi);
-          any_wide |= ballot(wide) != 0;
-          any_end |= ballot(end) != 0;
-          any_multi |= mmask[sd][j] != 0;
-        }
-      }
-      odd_split = ballot(odd_split) != 0;
-      tips_ok = true;
-      SUB_T1(34, t_an);
-      // active_min_count growth (:497-513): the count at every new length is
-      // the root's (no activation in this build)
-      if (W.am_len == tlen + 1 && tlen + 1 < E.lcap + 2) W.am_len++;
-      PH_MARK(1);
-
-      uint32_t nchild = 2;  // (0 or 1: decided on the lean path)
-      int child[2] = {-1, -1};
-      uint32_t kind = tdual ? 0u : 1u;
-      uint32_t nc = 1;
-      uint64_t ccost = 0;
-      uint32_t clen = 0;
-      bool general = false;  // children from Ctl (the block engines' passes)
-      if (any_wide || any_end) {
-        // wide frontiers or a read at a consensus end (finalize, reached_*):
-        // the block engines' code for the rest of the pop, from the slot
-        SUB_CNT(35, 1);
-        if (lane == 0) {
-          ctl.n_end[0] = ctl.n_end[1] = 0;
-          ctl.n_either = 0;
-          ctl.nheavy = 0;
-          ctl.ovf = 0;
-          ctl.multi[0] = ctl.multi[1] = 0;
-        }
-        wctl_to_ctl(W, ctl);
-        wave_rare<R>(kp, E.P, sbase, ctl, WR_GENERAL_POP, topslot, tdual, (uint32_t)full_min,
-                     (uint32_t)(full_min >> 32), oslot, 0, 0);
-        wctl_from_ctl(W, ctl);
-        W.hot = kNoSlot;
-        if (W.status != ST_OK) break;
-        nc = uni(ctl.nchild);
-        general = true;
-      } else {
-        if (!weighted && !odd_split) {
-          // ---- votes and selection on the lean path ----
-          SUB_T0(t_v);
-          const SideVotes sv0 = wave_side_votes<R>(cfg, ys[0], mmask[0], mn[0]);
-          SideVotes sv1 = {0, 0, -1, false};
-          if (tdual) sv1 = wave_side_votes<R>(cfg, ys[1], mmask[1], mn[1]);
-          uint32_t npass[2] = {sv0.npass, sv1.npass};
-          const uint32_t nkeys[2] = {sv0.nkeys, sv1.nkeys};
-          const int pkey[2] = {sv0.pk, sv1.pk};
-          if (tdual) {
-            // options per side: None first (consensus end, no keys, locked),
-            // then the passing keys; children = pairs but (None, None)
-            // (dual_consensus.rs:554-650)
-            bool has_none[2];
-            uint32_t no[2];
-#pragma unroll
-            for (int sd = 0; sd < 2; ++sd) {
-              const bool lock = (tflags & (sd == 0 ? 2u : 4u)) != 0;
-              const bool fin = early && (sd == 0 ? ns0 : ns1) == 0;  // (no read at its end here)
-              has_none[sd] = fin || nkeys[sd] == 0 || lock;
-              if (lock) npass[sd] = 0;
-              no[sd] = (has_none[sd] ? 1u : 0u) + npass[sd];
-            }
-            nchild = no[0] * no[1] - ((has_none[0] && has_none[1]) ? 1u : 0u);
-            child[0] = npass[0] ? pkey[0] : -1;
-            child[1] = npass[1] ? pkey[1] : -1;
-          } else {
-            // stay-single children, and split children from every pair of
-            // candidates when two pass min_count (:655-734)
-            nchild = npass[0] + (sv0.split ? 2u : 0u);
-            child[0] = pkey[0];
-          }
-          SUB_T1(38, t_v);
-        }
-        if (nchild >= 2) {
-          // weighted votes, splits that round, or several children (their
-          // order): the block engines' votes and selection (from RInfo)
-          SUB_CNT((weighted || odd_split) ? 36 : 39, 1);
-          if (lane == 0) {
-            ctl.ovf = 0;
-            ctl.multi[0] = ctl.multi[1] = any_multi ? 1u : 0u;
-            ctl.fin[0] = early && ns0 == 0;
-            ctl.fin[1] = tdual && early && ns1 == 0;
-            ctl.status = W.status;
-          }
-          __syncthreads();
-          wave_rare<R>(kp, E.P, sbase, ctl, WR_VOTES_SELECT, topslot, tdual, 0, 0, 0, 0, 0);
-          W.status = uni(ctl.status);
-          if (W.status != ST_OK) break;
-          nchild = uni(ctl.nchild);
-          if (nchild == 1) {
-            child[0] = uni((int32_t)ctl.ch_s[0][0]);
-            child[1] = uni((int32_t)ctl.ch_s[0][1]);
-            kind = uni((uint32_t)ctl.ch_kind[0]);
-          }
-        }
-        if (nchild == 0) {
-          if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = topslot;
-          W.nfree++;
-          W.hot = kNoSlot;
-          PH_MARK(3);
-          continue;
-        }
-        if (tlens[0] + 1 > E.lcap || tlens[1] + 1 > E.lcap) {
-          W.status = ST_RETRY | ST_RETRY_LCAP;
-          break;
-        }
-        PH_MARK(3);
-        if (nchild == 1 && kind != 2) {
-          SUB_CNT(37, 1);
-          uint32_t nl[2];
-          ccost = wave_push_fast<R>(E, ctl, kp, W, topslot, tm, tdual, kind, child, lr, tx, nl);
-          clen = max(nl[0], nl[1]);
-          if (W.status != ST_OK) break;
-          PH_MARK(11);
-        } else {
-          // clones, activate_dual: dual_build_children from the slot
-          wctl_to_ctl(W, ctl);
-          wave_rare<R>(kp, E.P, sbase, ctl, WR_CHILDREN, topslot, tdual, 0, 0, 0, 0, 0);
-          wctl_from_ctl(W, ctl);
-          W.hot = kNoSlot;
-          if (W.status != ST_OK) break;
-          nc = nchild;
-          general = true;
-        }
-      }
-      // ---- the children into the queue and their trackers ----
-      for (uint32_t c = 0; c < nc; ++c) {
-        uint32_t cslot = topslot;
-        if (general) {
-          cslot = uni(ctl.ch_slot[c]);
-          ccost = ((uint64_t)uni((uint32_t)(ctl.ch_cost[c] >> 32)) << 32) | uni((uint32_t)ctl.ch_cost[c]);
-          clen = uni(ctl.ch_len[c]);
-        }
-        const uint32_t k = !general ? (tdual ? 1u : 0u) : ((uni(E.L.meta[cslot].flags) & 1u) ? 1u : 0u);
-        if (lane == 0) atomicAdd((uint32_t*)&lc[k][WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
-        if (clen >= W.thr[k]) W.total[k]++;
-        wheap_push(E.L.heap, W.heap_n, HeapEntry{ccost, clen, cslot});
-        W.heap_n++;
-      }
-      PH_MARK(7);
-    }
-    // the register state back into Ctl for finish_problem
-    if (lane == 0) {
-      ctl.cnt[S_POPS] += W.pops;
-      ctl.cnt[S_EXPLORED] += W.explored;
-      ctl.cnt[S_IGNORED] += W.ignored;
-      ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], W.peakq);
-      ctl.cnt[S_UPDATES] += W.updates;
-      ctl.cnt[S_WOUT] += W.w_out;
-      ctl.cnt[S_COMPARES] += W.compares;
-    }
-    wctl_to_ctl(W, ctl);
-    finish_problem(A, ctl, outp, prob, oslot);
+    if (mixed && E.n <= 64u) wave_problem<1, mixed ? 1 : 0>(A, E, ctl, prob, oslot, outp);
+    else wave_problem<R, mixed ? 1 : 0>(A, E, ctl, prob, oslot, outp);
   }
   stream_exit(A);
 }
