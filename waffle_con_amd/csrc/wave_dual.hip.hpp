@@ -64,8 +64,18 @@ __device__ __forceinline__ void tips_unpack(const Tips& t, uint32_t (&x)[kF]) {
 }
 
 // thread_nominate on prefetched tip bytes (same arithmetic: every live slot
-// counts for reached_baseline_end, the tips give the nominations)
-__device__ inline Nom nominate_tips(const Front& f, const uint32_t (&x)[kF], uint32_t blen) {
+// counts for reached_baseline_end, the tips give the nominations), without
+// the hashbrown order of several symbols (the lean path's votes do not depend
+// on it): the distinct tip symbols in first-seen
+// order (klo/khi bytes), their counts (nibbles of cnt), and in meta the
+// number of symbols, reached_baseline_end (bit 8) and the split (bits 16+);
+// e = the read's edit distance (kInactive: no DWFA). The order, and RInfo,
+// are made only for the pops whose votes take the block engines' code
+// (wave_fill_rinfo).
+struct NomRaw {
+  uint32_t klo, khi, cnt, meta, e;
+};
+__device__ inline NomRaw nominate_raw(const Front& f, const uint32_t (&x)[kF], uint32_t blen) {
   uint32_t mb = f.maxb;
   const uint32_t hi = f.mask ? 32u - (uint32_t)__builtin_clz(f.mask) : 0u;
 #pragma unroll
@@ -74,7 +84,7 @@ __device__ inline Nom nominate_tips(const Front& f, const uint32_t (&x)[kF], uin
     if (f.mask & (1u << k)) mb = max(mb, f.fd[k] + f.e - f.fi[k]);
   }
   uint64_t keys = 0;
-  uint32_t cnts = 0, nk = 0;
+  uint32_t cnts = 0, nk = 0, split = 0;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
     if ((uint32_t)k >= hi) break;
@@ -87,30 +97,44 @@ __device__ inline Nom nominate_tips(const Front& f, const uint32_t (&x)[kF], uin
       nk++;
     }
     cnts += 1u << (4 * j);
+    split++;
   }
+  return NomRaw{(uint32_t)keys, (uint32_t)(keys >> 32), cnts, nk | ((mb == blen) ? 256u : 0u) | (split << 16), f.e};
+}
+// RInfo (thread_nominate's record, the order of several symbols included) of
+// one read from its NomRaw, for the block engines' votes (WR_VOTES_SELECT)
+__device__ inline void rinfo_from_raw(Sh<RInfo>* out, const NomRaw& r) {
+  if (r.e == kInactive) {
+    out->e = kInactive;
+    out->n = 0;
+    out->end = 0;
+    return;
+  }
+  const uint32_t nk = r.meta & 0xFFu;
+  const uint64_t keys = (uint64_t)r.klo | ((uint64_t)r.khi << 32);
   Nom o;
   o.n = nk;
-  o.end = mb == blen;
+  o.end = (r.meta >> 8) & 1u;
   if (nk <= 1) {
     o.sym = keys;
-    o.occ = cnts;
-    o.split = cnts;
-    return o;
+    o.occ = r.cnt;
+    o.split = r.cnt;
+  } else {
+    const uint64_t ord = fx_order_packed(nk, [&](uint32_t j) { return byte_at(keys, j); });
+    uint64_t sym = 0, occ = 0;
+    uint32_t split = 0;
+    for (uint32_t k = 0; k < nk; ++k) {
+      const uint32_t j = nib(ord, k);
+      const uint32_t c = (r.cnt >> (4 * j)) & 15u;
+      sym |= (uint64_t)byte_at(keys, j) << (8 * k);
+      occ |= (uint64_t)c << (8 * k);
+      split += c;
+    }
+    o.sym = sym;
+    o.occ = occ;
+    o.split = split;
   }
-  const uint64_t ord = fx_order_packed(nk, [&](uint32_t j) { return byte_at(keys, j); });
-  uint64_t sym = 0, occ = 0;
-  uint32_t split = 0;
-  for (uint32_t k = 0; k < nk; ++k) {
-    const uint32_t j = nib(ord, k);
-    const uint32_t c = (cnts >> (4 * j)) & 15u;
-    sym |= (uint64_t)byte_at(keys, j) << (8 * k);
-    occ |= (uint64_t)c << (8 * k);
-    split += c;
-  }
-  o.sym = sym;
-  o.occ = occ;
-  o.split = split;
-  return o;
+  rinfo_store(out, o, r.e);
 }
 
 // the hot node (both sides when `dual`) back into slot `slot`
@@ -650,25 +674,30 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
                  (uint32_t)sy[1], 0);
     SUB_T1(54, t_hv);
     const uint32_t ovf = uni(ctl.ovf);
-    if (ovf & 16u) W.status = WC_E_INVARIANT_CODE;
-    else if (ovf & 4u) W.status = ST_RETRY | ST_RETRY_WCAP;
-    else if (ovf) W.status = limit_status(ovf);
+    // (per-lane branches without continue, and the uniform status after
+    // them: a join of lanes' paths that also carries search control makes
+    // the compiler treat the whole pop loop's control state as divergent)
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t r = (uint32_t)lane + 64u * j;
-      if (r >= n) continue;
 #pragma unroll
       for (int sd = 0; sd < 2; ++sd) {
-        if ((sd == 1 && !tdual) || sy[sd] < 0) continue;
-        const RRaw s = rstate_load(&E.L.hot[sd * E.nmax + r]);
-        if (ee[j][sd] == rraw_e(s) && ee[j][sd] != kInactive && !(rraw_flags(s) & kWide)) continue;
-        ee[j][sd] = rraw_e(s);
-        if (rraw_e(s) == kInactive || (rraw_flags(s) & kWide)) continue;
-        Front f;
-        front_load(s, f);
-        tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], nl[sd]);
+        if (r < n && !(sd == 1 && !tdual) && sy[sd] >= 0) {
+          const RRaw s = rstate_load(&E.L.hot[sd * E.nmax + r]);
+          if (!(ee[j][sd] == rraw_e(s) && ee[j][sd] != kInactive && !(rraw_flags(s) & kWide))) {
+            ee[j][sd] = rraw_e(s);
+            if (rraw_e(s) != kInactive && !(rraw_flags(s) & kWide)) {
+              Front f;
+              front_load(s, f);
+              tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], nl[sd]);
+            }
+          }
+        }
       }
     }
+    if (ovf & 16u) W.status = WC_E_INVARIANT_CODE;
+    else if (ovf & 4u) W.status = ST_RETRY | ST_RETRY_WCAP;
+    else if (ovf) W.status = limit_status(ovf);
   }
   // prune_dwfa (:1030-1045) of a dual child, then per read the cheaper side's
   // cost (strict <: ties keep consensus 1, :1092-1131) and the Some counts
@@ -706,41 +735,6 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   return cost;
 }
 
-// per-lane multi-symbol nominations (read lane + 64 j) for the exact votes
-struct MultiNom {
-  uint32_t lo, hi;  // symbols (bytes, iteration order)
-  uint32_t occ_lo, occ_hi;  // their occurrences (bytes)
-  uint32_t split;
-};
-
-// the vote of key `key` on one side in eighths: 8 per single-symbol voter,
-// occ * 8 / split per multi-symbol voter (split in {1, 2, 4, 8})
-template <int R>
-__device__ __forceinline__ uint32_t votes8(uint32_t key, const uint32_t (&ys)[R], const uint64_t (&mmask)[R],
-                                           const MultiNom (&mn)[R]) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    c += 8u * (uint32_t)__popcll((unsigned long long)ballot(ys[j] == key));
-    uint64_t mm = mmask[j];
-    while (mm) {
-      const int l = __builtin_ctzll(mm);
-      mm &= mm - 1;
-      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].lo, l);
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].hi, l);
-      const uint32_t olo = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].occ_lo, l);
-      const uint32_t ohi = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].occ_hi, l);
-      const uint32_t split = (uint32_t)__builtin_amdgcn_readlane((int)mn[j].split, l);
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t sk = ((k < 4 ? lo : hi) >> (8 * (k & 3))) & 0xFFu;
-        const uint32_t ok = ((k < 4 ? olo : ohi) >> (8 * (k & 3))) & 0xFFu;
-        if (ok && sk == key) c += ok * (8u / split);
-      }
-    }
-  }
-  return c;
-}
-
 // ---- the votes of one node side on the lean path (consensus.rs:540-564,
 // dual_consensus.rs:1242-1290): the keys (the wildcard dropped when it is not
 // the only one, :556-561) with their votes in exact eighths, their sum and
@@ -754,7 +748,7 @@ struct SideVotes {
 };
 template <int R>
 __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const uint32_t (&ys)[R],
-                                                     const uint64_t (&mmask)[R], const MultiNom (&mn)[R]) {
+                                                     const uint64_t (&mmask)[R], const NomRaw (&mn)[R]) {
   const int wc = cfg.wildcard;
   uint32_t nk = 0, total8 = 0, mx_all = 0, mx_nowc = 0, wc8 = 0;
   bool wc_in = false, drop = false;
@@ -805,12 +799,8 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
   for (int j = 0; j < R; ++j) {
     rem[j] = ballot(ys[j] != 0x100u);
     mrem[j] = 0;
-    mul[j] = 8u >> (__builtin_ctz(mn[j].split | 256u) & 3u);
-    if ((mmask[j] >> lane_id()) & 1ull) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if ((((k < 4 ? mn[j].occ_lo : mn[j].occ_hi) >> (8 * (k & 3))) & 0xFFu) != 0u) mrem[j] |= 1u << k;
-    }
+    mul[j] = 8u >> (__builtin_ctz((mn[j].meta >> 16) | 256u) & 3u);
+    if ((mmask[j] >> lane_id()) & 1ull) mrem[j] = (1u << (mn[j].meta & 0xFFu)) - 1u;  // (slots < nk hold a symbol)
     any_multi |= mmask[j] != 0;
   }
   uint32_t tkey = 0x100u, tc8 = 0;  // lane k: key k and its vote
@@ -826,7 +816,7 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
         if (key == 0x100u && lm) {
           const int l = __builtin_ctzll(lm);
           const uint32_t k = (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)mrem[j], l));
-          const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)(k < 4 ? mn[j].lo : mn[j].hi), l);
+          const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)(k < 4 ? mn[j].klo : mn[j].khi), l);
           key = (w >> (8 * (k & 3))) & 0xFFu;
         }
       }
@@ -846,9 +836,9 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
         uint32_t occ = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const uint32_t sk = ((k < 4 ? mn[j].lo : mn[j].hi) >> (8 * (k & 3))) & 0xFFu;
+          const uint32_t sk = ((k < 4 ? mn[j].klo : mn[j].khi) >> (8 * (k & 3))) & 0xFFu;
           if (((mrem[j] >> k) & 1u) && sk == key) {
-            occ += ((k < 4 ? mn[j].occ_lo : mn[j].occ_hi) >> (8 * (k & 3))) & 0xFFu;
+            occ += (mn[j].cnt >> (4 * k)) & 15u;
             mrem[j] &= ~(1u << k);
           }
         }
@@ -982,8 +972,14 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     const uint32_t dual = uni(tm.flags) & 1u;
     const uint32_t ns0 = uni(tm.nsome[0]), ns1 = uni(tm.nsome[1]);
     // tracker(dual).remove(len)
-    if (lane == 0) atomicSub((uint32_t*)&lc[dual][WC_IX(top.len, L2)], 1u);
-    if (top.len >= W.thr[dual]) W.total[dual]--;
+    // (the per-tracker fields by constant index only: a runtime index into
+    // WCtl's arrays keeps the whole struct in scratch memory)
+    const uint32_t thr_d = dual ? W.thr[1] : W.thr[0];
+    if (lane == 0) atomicSub((uint32_t*)&(dual ? lc[1] : lc[0])[WC_IX(top.len, L2)], 1u);
+    if (top.len >= thr_d) {
+      if (dual) W.total[1]--;
+      else W.total[0]--;
+    }
     const bool imbalanced = dual && (ns0 < am || ns1 < am);
     if (top.len >= W.am_len) W.status = WC_E_INVARIANT_CODE;
     SUB_T1(47, t_pc);  // (pop-logic: metadata, tracker)
@@ -992,7 +988,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     // capacity; the capacity check waits for the processed count's load and
     // comes after the analysis below (nothing before it has an effect that
     // outlives an ignored node), so that load's latency overlaps it
-    const bool ign = top.cost > W.max_err || top.len < W.thr[dual] || imbalanced;
+    const bool ign = top.cost > W.max_err || top.len < thr_d || imbalanced;
     if (ign) {
       if (A.trace && lane == 0) trace_pop(A, prob, top, dual | (1u << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
       W.ignored++;
@@ -1026,7 +1022,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     SUB_T0(t_an);
     uint32_t ys[2][R];  // the read's one nominated symbol (0x100: none, several, or not a voter)
     uint64_t mmask[2][R];  // lanes whose read nominates several symbols
-    MultiNom mn[2][R];
+    NomRaw mn[2][R];  // every read's nominations (RInfo is made from them only when needed)
     bool any_wide = false, any_end = false, any_multi = false, odd_split = false;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -1035,15 +1031,12 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
 #pragma unroll
       for (int sd = 0; sd < 2; ++sd) {
         ys[sd][j] = 0x100u;
-        mn[sd][j] = MultiNom{0, 0, 0, 0, 1};
+        mn[sd][j] = NomRaw{0, 0, 0, 1u << 16, kInactive};
         bool wide = false, end = false, multi = false;
         if (live && (sd == 0 || tdual)) {
-          Sh<RInfo>* out = (sd ? R1 : R0) + r;
           const RRaw s = rstate_load(&E.L.hot[sd * E.nmax + r]);
           if (rraw_e(s) == kInactive) {
-            out->e = kInactive;
-            out->n = 0;
-            out->end = 0;
+            // (mn: no DWFA)
           } else if (rraw_flags(s) & kWide) {
             wide = true;
           } else {
@@ -1052,16 +1045,13 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
             if (!tips_ok) tx[j][sd] = tips_fetch(f, lr.rd[j], lr.bl[j], tlens[sd]);
             uint32_t x[kF];
             tips_unpack(tx[j][sd], x);
-            const Nom o = nominate_tips(f, x, lr.bl[j]);
-            rinfo_store(out, o, f.e);
-            end = o.end != 0;
-            multi = o.n > 1;
-            if (o.n == 1) ys[sd][j] = byte_at(o.sym, 0);
-            if (multi) {
-              mn[sd][j] = MultiNom{(uint32_t)o.sym, (uint32_t)(o.sym >> 32), (uint32_t)o.occ,
-                                   (uint32_t)(o.occ >> 32), o.split};
-              if (o.split > 8u || (o.split & (o.split - 1u))) odd_split = true;
-            }
+            const NomRaw o = nominate_raw(f, x, lr.bl[j]);
+            mn[sd][j] = o;
+            const uint32_t nk = o.meta & 0xFFu, split = o.meta >> 16;
+            end = (o.meta & 256u) != 0;
+            multi = nk > 1;
+            if (nk == 1) ys[sd][j] = o.klo & 0xFFu;
+            if (multi && (split > 8u || (split & (split - 1u)))) odd_split = true;
           }
         }
         mmask[sd][j] = ballot(multi);
@@ -1085,9 +1075,14 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
         continue;
       }
     }
-    W.far[dual] = max(W.far[dual], top.len);
-    W.lastc[dual] += W.lastc[dual] != 0xFFFFFFFFu;
-    if (lane == 0) atomicAdd((uint32_t*)&pc[dual][WC_IX(top.len, L2)], 1u);  // process_unchecked
+    if (dual) {
+      W.far[1] = max(W.far[1], top.len);
+      W.lastc[1] += W.lastc[1] != 0xFFFFFFFFu;
+    } else {
+      W.far[0] = max(W.far[0], top.len);
+      W.lastc[0] += W.lastc[0] != 0xFFFFFFFFu;
+    }
+    if (lane == 0) atomicAdd((uint32_t*)&(dual ? pc[1] : pc[0])[WC_IX(top.len, L2)], 1u);  // process_unchecked
     W.explored++;
     if (W.status != ST_OK) break;
     // active_min_count growth (:497-513): the count at every new length is
@@ -1167,6 +1162,16 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
           ctl.fin[1] = tdual && early && ns1 == 0;
           ctl.status = W.status;
         }
+        // the block engines' votes read RInfo: made here, with the order of
+        // several symbols, only for these pops
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const uint32_t r = (uint32_t)lane + 64u * j;
+          if (r < E.n) {
+            rinfo_from_raw(R0 + r, mn[0][j]);
+            if (tdual) rinfo_from_raw(R1 + r, mn[1][j]);
+          }
+        }
         __syncthreads();
         wave_rare<R, V>(kp, E.P, sbase, ctl, WR_VOTES_SELECT, topslot, tdual, 0, 0, 0, 0, 0);
         W.status = uni(ctl.status);
@@ -1217,8 +1222,9 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
         clen = uni(ctl.ch_len[c]);
       }
       const uint32_t k = !general ? (tdual ? 1u : 0u) : ((uni(E.L.meta[cslot].flags) & 1u) ? 1u : 0u);
-      if (lane == 0) atomicAdd((uint32_t*)&lc[k][WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
-      if (clen >= W.thr[k]) W.total[k]++;
+      if (lane == 0) atomicAdd((uint32_t*)&(k ? lc[1] : lc[0])[WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
+      if (k) W.total[1] += clen >= W.thr[1];
+      else W.total[0] += clen >= W.thr[0];
       wheap_push(E.L.heap, W.heap_n, HeapEntry{ccost, clen, cslot});
       W.heap_n++;
     }
