@@ -22,7 +22,7 @@ PHASES = {0: "pop-broadcast", 1: "analyze", 2: "finalize", 3: "votes+select", 4:
           11: "chain-accept", 12: "votes-wave", 13: "pop-logic", 14: "chain-total"}
 # the one-wave dual engine's own counters (wave_dual.hip.hpp; 32..39 and 53..55)
 WAVE_SUB = {32: "hot-load-block", 33: "hot-loads", 34: "analysis-lanes", 35: "general-end-or-wide",
-            36: "general-weighted-or-odd-split", 37: "fast-pushes", 38: "votes", 39: "general-children",
+            36: "general-weighted-or-f64-tie", 37: "fast-pushes", 38: "votes", 39: "general-children",
             53: "heavy-calls", 54: "heavy-cycles", 55: "heavy-items",
             45: "pop-to-heap", 46: "pop-heap", 47: "pop-meta-pc",
             48: "push-lanes", 49: "push-prune-cost"}

@@ -737,26 +737,26 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
 
 // ---- the votes of one node side on the lean path (consensus.rs:540-564,
 // dual_consensus.rs:1242-1290): the keys (the wildcard dropped when it is not
-// the only one, :556-561) with their votes in exact eighths, their sum and
-// maximum, the threshold min(max(min_count, ceil(min_af * sum)), max)
-// (:520-552), and the keys passing it. With one child the order of the keys
-// (hashbrown) decides nothing, so none is computed. ----
+// the only one, :556-561) with their votes, their sum and maximum, the
+// threshold min(max(min_count, ceil(min_af * sum)), max) (:520-552), and the
+// keys passing it. Votes are exact integers in units of 1/U of a read: U = 8
+// when every split is 1, 2, 4 or 8 (the reference's f64 sums are then exact
+// too), U = 840 = lcm(1..8) otherwise. With other splits the reference's f64
+// sums round; they decide the same as the exact values unless two of the
+// compared quantities are exactly equal (a tie at the maximum, or a vote equal
+// to min_count), so those sides are left to the block engines' f64 votes
+// (exact = false), as are min_af > 0 with other splits. With one child the
+// order of the keys (hashbrown) decides nothing, so none is computed. ----
 struct SideVotes {
   uint32_t npass, nkeys;  // keys passing the threshold, keys
   int pk;                 // a passing key (the one, when npass == 1)
   bool split;             // single-consensus node: two candidates pass min_count (split children)
+  bool exact;             // false: decide with the block engines' f64 votes
 };
 template <int R>
 __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const uint32_t (&ys)[R],
-                                                     const uint64_t (&mmask)[R], const NomRaw (&mn)[R]) {
+                                                     const uint64_t (&mmask)[R], const NomRaw (&mn)[R], bool odd) {
   const int wc = cfg.wildcard;
-  uint32_t nk = 0, total8 = 0, mx_all = 0, mx_nowc = 0, wc8 = 0;
-  bool wc_in = false, drop = false;
-  uint32_t np = 0, ns = 0, npmc = 0;
-  int pk = -1;
-  uint64_t mc = 0;
-  double thr = 0.0;
-  uint32_t nko = 0;
   // the common case: every voter nominates one symbol, the same one
   {
     uint64_t vm[R], any = 0, mm = 0;
@@ -768,42 +768,47 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
     }
     if (!mm) {
       if (!any) {  // no key: no option but None; thr (unused) from min_count
-        return SideVotes{0, 0, -1, false};
+        return SideVotes{0, 0, -1, false, true};
       }
       uint32_t first = 0x100u;
 #pragma unroll
       for (int j = 0; j < R; ++j)
         if (first == 0x100u && vm[j]) first = (uint32_t)__builtin_amdgcn_readlane((int)ys[j], __builtin_ctzll(vm[j]));
       bool same = true;
-      uint32_t cnt = 0;
 #pragma unroll
-      for (int j = 0; j < R; ++j) {
-        same = same && ballot(ys[j] == first) == vm[j];
-        cnt += (uint32_t)__popcll((unsigned long long)vm[j]);
-      }
+      for (int j = 0; j < R; ++j) same = same && ballot(ys[j] == first) == vm[j];
       if (same) {
         // one key, not dropped (it is the only one); it passes min(mc, its own count)
-        return SideVotes{1, 1, (int)first, false};
+        return SideVotes{1, 1, (int)first, false, true};
       }
     }
   }
+  if (odd && cfg.min_af != 0.0) return SideVotes{0, 0, -1, false, false};
+  const uint32_t U = odd ? 840u : 8u;
   // the distinct keys one at a time (single-symbol voters first, by ballots;
   // then the symbols of multi-symbol voters not counted yet, lanes in
-  // parallel), each with its vote in eighths; lane k keeps key k and its vote
-  // for the threshold pass. The order of the keys decides nothing here.
+  // parallel), each with its vote in units of 1/U; lane k keeps key k and its
+  // vote for the threshold pass
   uint64_t rem[R];
   uint32_t mrem[R];  // per lane: its multi-symbol slots not counted yet
-  uint32_t mul[R];   // per lane: 8 / split (eighths per occurrence)
-  bool any_multi = false;
+  uint32_t mul[R];   // per lane: U / split (units per occurrence)
+  bool any_multi = false, big = false;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     rem[j] = ballot(ys[j] != 0x100u);
     mrem[j] = 0;
-    mul[j] = 8u >> (__builtin_ctz((mn[j].meta >> 16) | 256u) & 3u);
-    if ((mmask[j] >> lane_id()) & 1ull) mrem[j] = (1u << (mn[j].meta & 0xFFu)) - 1u;  // (slots < nk hold a symbol)
+    const uint32_t split = max(mn[j].meta >> 16, 1u);
+    mul[j] = U / split;
+    if ((mmask[j] >> lane_id()) & 1ull) {
+      mrem[j] = (1u << (mn[j].meta & 0xFFu)) - 1u;  // (slots < nk hold a symbol)
+      big |= split > 8u;                            // (never: at most kF = 8 tips)
+    }
     any_multi |= mmask[j] != 0;
   }
-  uint32_t tkey = 0x100u, tc8 = 0;  // lane k: key k and its vote
+  if (ballot(big)) return SideVotes{0, 0, -1, false, false};
+  uint32_t nk = 0, total = 0, mx_all = 0, mx_nowc = 0, wcv = 0;
+  bool wc_in = false;
+  uint32_t tkey = 0x100u, tc = 0;  // lane k: key k and its vote
   for (;;) {
     uint32_t key = 0x100u;
 #pragma unroll
@@ -822,11 +827,11 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
       }
     }
     if (key == 0x100u) break;
-    uint32_t c8 = 0;
+    uint32_t c = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint64_t m = ballot(ys[j] == key);
-      c8 += 8u * (uint32_t)__popcll((unsigned long long)m);
+      c += U * (uint32_t)__popcll((unsigned long long)m);
       rem[j] &= ~m;
     }
     if (any_multi) {
@@ -844,37 +849,42 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
         }
         mine += occ * mul[j];
       }
-      c8 += wave_sum_u32(mine);
+      c += wave_sum_u32(mine);
     }
     if (lane_id() == (int)nk) {
       tkey = key;
-      tc8 = c8;
+      tc = c;
     }
     nk++;
-    total8 += c8;
-    mx_all = max(mx_all, c8);
+    total += c;
+    mx_all = max(mx_all, c);
     if (wc >= 0 && key == (uint32_t)(uint8_t)wc) {
       wc_in = true;
-      wc8 = c8;
+      wcv = c;
     } else {
-      mx_nowc = max(mx_nowc, c8);
+      mx_nowc = max(mx_nowc, c);
     }
   }
-  drop = wc_in && nk > 1;
-  nko = drop ? nk - 1 : nk;
-  const uint32_t sum8 = drop ? total8 - wc8 : total8;
-  const uint32_t mx8 = drop ? mx_nowc : mx_all;
-  mc = max(cfg.min_count, ceil_u64(cfg.min_af * ((double)sum8 * 0.125)));
-  thr = nko ? fmin((double)mc, (double)mx8 * 0.125) : (double)mc;
+  const bool drop = wc_in && nk > 1;
+  const uint32_t nko = drop ? nk - 1 : nk;
+  const uint32_t sum = drop ? total - wcv : total;
+  const uint32_t mx = drop ? mx_nowc : mx_all;
+  // min_count (and min_af * sum, exact for U = 8) in units; saturated far
+  // above any vote (<= 128 reads)
+  const uint64_t mc = max(cfg.min_count, odd ? 0ull : ceil_u64(cfg.min_af * ((double)sum * 0.125)));
+  const uint64_t mcu = mc > (1ull << 32) ? (1ull << 48) : mc * U;
+  const uint64_t thr = nko ? min(mcu, (uint64_t)mx) : mcu;
   // the threshold pass (:520-552, :655-679), key k on lane k
   const bool is_wc = wc >= 0 && tkey == (uint32_t)(uint8_t)wc;
   const bool valid = lane_id() < (int)nk && !(drop && is_wc);
-  const uint64_t pm = ballot(valid && !((double)tc8 * 0.125 < thr));
-  np = (uint32_t)__popcll((unsigned long long)pm);
-  pk = pm ? (int)__builtin_amdgcn_readlane((int)tkey, __builtin_ctzll(pm)) : -1;
-  ns = (uint32_t)__popcll((unsigned long long)ballot(valid && !is_wc));
-  npmc = (uint32_t)__popcll((unsigned long long)ballot(valid && !is_wc && (double)tc8 * 0.125 >= (double)mc));
-  return SideVotes{np, nko, pk, npmc > 1 && ns > 1};
+  if (odd && (__popcll((unsigned long long)ballot(valid && tc == mx)) > 1 || ballot(valid && (uint64_t)tc == mcu) != 0))
+    return SideVotes{0, 0, -1, false, false};
+  const uint64_t pm = ballot(valid && (uint64_t)tc >= thr);
+  const uint32_t np = (uint32_t)__popcll((unsigned long long)pm);
+  const int pk = pm ? (int)__builtin_amdgcn_readlane((int)tkey, __builtin_ctzll(pm)) : -1;
+  const uint32_t ns = (uint32_t)__popcll((unsigned long long)ballot(valid && !is_wc));
+  const uint32_t npmc = (uint32_t)__popcll((unsigned long long)ballot(valid && !is_wc && (uint64_t)tc >= mcu));
+  return SideVotes{np, nko, pk, npmc > 1 && ns > 1, true};
 }
 
 // ---- the search: dual_main's pop, with a lean path for the common pop ----
@@ -1117,12 +1127,14 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
       nc = uni(ctl.nchild);
       general = true;
     } else {
-      if (!weighted && !odd_split) {
+      SideVotes sv0 = {0, 0, -1, false, false}, sv1 = {0, 0, -1, false, true};
+      if (!weighted) {
+        sv0 = wave_side_votes<R>(cfg, ys[0], mmask[0], mn[0], odd_split);
+        if (tdual && sv0.exact) sv1 = wave_side_votes<R>(cfg, ys[1], mmask[1], mn[1], odd_split);
+      }
+      if (sv0.exact && sv1.exact) {
         // ---- votes and selection on the lean path ----
         SUB_T0(t_v);
-        const SideVotes sv0 = wave_side_votes<R>(cfg, ys[0], mmask[0], mn[0]);
-        SideVotes sv1 = {0, 0, -1, false};
-        if (tdual) sv1 = wave_side_votes<R>(cfg, ys[1], mmask[1], mn[1]);
         uint32_t npass[2] = {sv0.npass, sv1.npass};
         const uint32_t nkeys[2] = {sv0.nkeys, sv1.nkeys};
         const int pkey[2] = {sv0.pk, sv1.pk};
@@ -1152,9 +1164,9 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
         SUB_T1(38, t_v);
       }
       if (nchild >= 2) {
-        // weighted votes, splits that round, or several children (their
-        // order): the block engines' votes and selection (from RInfo)
-        SUB_CNT((weighted || odd_split) ? 36 : 39, 1);
+        // weighted votes, rounding f64 votes at a tie, or several children
+        // (their order): the block engines' votes and selection (from RInfo)
+        SUB_CNT((!sv0.exact || !sv1.exact) ? 36 : 39, 1);
         if (lane == 0) {
           ctl.ovf = 0;
           ctl.multi[0] = ctl.multi[1] = any_multi ? 1u : 0u;
