@@ -815,9 +815,11 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   // WC_LAUNCH_LOG): how far it got and how many workgroups are still in
   auto t_fin = t_log, t_warn = t_log;
   // what is ready but not yet published, in publication order: continuations
-  // first, then the largest (reads x bases)
+  // first (those of the problems that have taken the most pops so far first),
+  // then the largest (reads x bases)
   auto later = [&](uint32_t x, uint32_t y) {
     if (items[x].cont != items[y].cont) return items[y].cont;
+    if (items[x].crit != items[y].crit) return items[x].crit < items[y].crit;
     const double kx = (double)items[x].work * (double)items[x].gid.size();
     const double ky = (double)items[y].work * (double)items[y].gid.size();
     return kx != ky ? kx < ky : x > y;
@@ -1077,6 +1079,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
   std::vector<std::vector<std::vector<ConsRec>>> cons(n);
   std::vector<std::vector<std::vector<uint8_t>>> assigns(n);
   std::vector<bool> alive(n, true);
+  std::vector<uint64_t> owner_pops(n, 0);  // pops of each problem's finished sub-problems (SubProb::crit)
   std::deque<uint32_t> ready, retry_ready;
 
   bool roots_made = false;  // sub-problems made after the roots are continuations
@@ -1094,6 +1097,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     outs.emplace_back();
     SubProb& s = subs.back();
     s.cont = roots_made;
+    s.crit = owner_pops[i];
     std::vector<int64_t> offs;
     for (uint32_t c = 0; c < q.n_chains; ++c) {
       if (!w.inc[c]) continue;
@@ -1302,6 +1306,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
       build_dual(o, (uint32_t)subs[id].gid.size(), cfg.consensus_cost, *w.res);
       w.state = 2;
       o.recs.clear();
+      owner_pops[w.owner] += w.res->stats[S_POPS];
       expand(id);
       if (sublog) {
         // diagnostics: one line per finished sub-problem (the critical path of a locus)

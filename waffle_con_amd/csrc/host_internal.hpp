@@ -227,6 +227,10 @@ struct SubProb {
   // capacity growth earned by ST_RETRY outcomes (log2 multipliers)
   uint8_t wcap_x = 0, pcap_x = 0, lcap_x = 0, rmax_x = 0;
   uint32_t attempts = 0;
+  // PriorityConsensusDWFA: pops its problem's finished sub-problems took before
+  // this one was made (the stream publishes the continuations of the loci that
+  // have run longest first: a deep locus's next sub-problem is on its critical path)
+  uint64_t crit = 0;
 };
 // auto_shift_offsets + activation points (consensus.rs:151-202) of one
 // problem; fills sp.act / n_active / max_act or returns an error code.

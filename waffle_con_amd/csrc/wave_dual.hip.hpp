@@ -168,7 +168,7 @@ __device__ __forceinline__ void hot_fetch_slot(Eng& E, uint32_t slot, bool dual)
 // register allocation does not carry theirs. The callee rebuilds the engine
 // context from the kernel arguments (callee_eng); the hot area is the carve's
 // start, so sbase = Lds::hot. ----
-enum : uint32_t { WR_GENERAL_POP = 0, WR_VOTES_SELECT = 1, WR_HEAVY = 2, WR_CHILDREN = 3 };
+enum : uint32_t { WR_GENERAL_POP = 0, WR_VOTES_SELECT = 1, WR_CHILDREN = 3 };
 
 // dual_main's thread-0 selection (dual_consensus.rs:520-734): thresholds from
 // the votes in ctl.keys/vals, then the children in the reference's order
@@ -256,8 +256,37 @@ __device__ inline void wave_select_t0(const DevConfig& cfg, Lo<Ctl>& ctl, const 
   ctl.nchild = nc;
 }
 
+// the ED-increase loops (and wide frontiers) of the in-place push: one read
+// per wave, on the hot copy (the rows are the slot's). A call of its own: the
+// registers it saves and restores are its own few, not the general paths'.
 // (V: the kernel it is called from, so that each kernel's call has a body
 // compiled for that kernel's register budget)
+template <int R, int V>
+__device__ __noinline__ void wave_heavy_call(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top,
+                                             uint32_t nl0, uint32_t nl1, uint32_t sy0, uint32_t sy1) {
+  Eng E = callee_eng(kp, P, sbase);
+  const int lane = lane_id();
+  const DevConfig& cfg = E.cfg;
+  const bool early = cfg.early != 0;
+  const uint32_t n = E.n;
+  const uint32_t nl[2] = {nl0, nl1};
+  const int sy[2] = {(int32_t)sy0, (int32_t)sy1};
+  const uint32_t nh = uni(ctl.nheavy);
+  WaveCounters cnt = {0, 0, 0, 0, 0, 0};
+  for (uint32_t k = 0; k < nh; ++k) {
+    const uint32_t it = uni(E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))]);
+    const uint32_t sd = it >= n ? 1u : 0u, r = it - sd * n;
+    SideView v = E.sv(top, sd);
+    uint32_t e = 0;
+    const bool ok = wave_heavy(&E.L.hot[sd * E.nmax + r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
+                               nl[sd], (uint8_t)sy[sd], cfg.wildcard, early, E.wcap, cnt, e);
+    __builtin_amdgcn_wave_barrier();
+    if (!ok && lane == 0) atomicOr(&ctl.ovf, 4u);
+  }
+  flush_counters(ctl, cnt);
+  __syncthreads();
+}
+
 template <int R, int V>
 __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t op,
                                        uint32_t top, uint32_t tdual_u, uint32_t a0, uint32_t a1, uint32_t a2,
@@ -269,27 +298,6 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
   const bool weighted = cfg.weighted != 0;
   const bool tdual = tdual_u != 0;
   const uint32_t n = E.n;
-  if (op == WR_HEAVY) {
-    // the ED-increase loops (and wide frontiers) of the in-place push: one
-    // read per wave, on the hot copy (the rows are the slot's)
-    const uint32_t nl[2] = {a0, a1};
-    const int sy[2] = {(int32_t)a2, (int32_t)a3};
-    const uint32_t nh = uni(ctl.nheavy);
-    WaveCounters cnt = {0, 0, 0, 0, 0, 0};
-    for (uint32_t k = 0; k < nh; ++k) {
-      const uint32_t it = uni(E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))]);
-      const uint32_t sd = it >= n ? 1u : 0u, r = it - sd * n;
-      SideView v = E.sv(top, sd);
-      uint32_t e = 0;
-      const bool ok = wave_heavy(&E.L.hot[sd * E.nmax + r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
-                                 nl[sd], (uint8_t)sy[sd], cfg.wildcard, early, E.wcap, cnt, e);
-      __builtin_amdgcn_wave_barrier();
-      if (!ok && lane == 0) atomicOr(&ctl.ovf, 4u);
-    }
-    flush_counters(ctl, cnt);
-    __syncthreads();
-    return;
-  }
   const SlotMeta tm = meta_get(E.L.meta[top]);
   Sh<RInfo>* R0 = E.L.rinfo;
   Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
@@ -670,8 +678,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
       ctl.ovf = 0;
     }
     __syncthreads();
-    wave_rare<R, V>(kp, E.P, (Sh<uint8_t>*)E.L.hot, ctl, WR_HEAVY, top, tdual, nl[0], nl[1], (uint32_t)sy[0],
-                 (uint32_t)sy[1], 0);
+    wave_heavy_call<R, V>(kp, E.P, (Sh<uint8_t>*)E.L.hot, ctl, top, nl[0], nl[1], (uint32_t)sy[0], (uint32_t)sy[1]);
     SUB_T1(54, t_hv);
     const uint32_t ovf = uni(ctl.ovf);
     // (per-lane branches without continue, and the uniform status after
