@@ -267,7 +267,10 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
     b->valid = true;
     return (int)WC_OK;
   };
-  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  // staging threads: up to 16, or WC_UPLOAD_THREADS (a caller that computes
+  // on another context while this one uploads may want to leave it cores)
+  unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (const char* ut = getenv("WC_UPLOAD_THREADS")) hw = std::max(1, std::min(64, atoi(ut)));
   // reads split into contiguous ranges of about equal bytes, one per thread
   auto split_run = [&](uint64_t r_begin, uint64_t r_end, uint64_t nt, auto fn) {
     const uint64_t b0 = r_begin < nr ? roff[r_begin] : pos, b1 = r_end < nr ? roff[r_end] : pos;
