@@ -13,3 +13,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 echo "cfg5 kt done"
 timeout -k 10 900 python3 -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+for v in 2 1; do
+  WC_WAVE=$v timeout -k 10 400 python3 -u bench.py --workload cfg4 --steps 1 --warmup 0 --no-cpu > $O/c4_$v.json 2> $O/c4_$v.err || { tail -5 $O/c4_$v.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/c4_$v.json'));print('cfg4 WC_WAVE=$v', d['value'], d['ms_per_step'], d['kernel_ms_per_step'])"
+done

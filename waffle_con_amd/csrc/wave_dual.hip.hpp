@@ -434,7 +434,7 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
 
 // per-lane read pointers and lengths of the claimed problem (read lane + 64 j)
 template <int R>
-struct LaneReads {  // (R <= 2)
+struct LaneReads {  // (R = 1, 2 or 4)
   const Gm<uint8_t>* rd[R];
   uint32_t bl[R];
 };
@@ -813,6 +813,11 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
     any_multi |= mmask[j] != 0;
   }
   if (ballot(big)) return SideVotes{0, 0, -1, false, false};
+  // symbols per multi-symbol voter, at most (the slot loops below stop there)
+  uint32_t kmax = 0;
+#pragma unroll
+  for (int j = 0; j < R; ++j) kmax = max(kmax, mrem[j] ? 32u - (uint32_t)__builtin_clz(mrem[j]) : 0u);
+  kmax = any_multi ? wave_max_u32(kmax) : 0u;
   uint32_t nk = 0, total = 0, mx_all = 0, mx_nowc = 0, wcv = 0;
   bool wc_in = false;
   uint32_t tkey = 0x100u, tc = 0;  // lane k: key k and its vote
@@ -848,6 +853,7 @@ __device__ __forceinline__ SideVotes wave_side_votes(const DevConfig& cfg, const
         uint32_t occ = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
+          if ((uint32_t)k >= kmax) break;
           const uint32_t sk = ((k < 4 ? mn[j].klo : mn[j].khi) >> (8 * (k & 3))) & 0xFFu;
           if (((mrem[j] >> k) & 1u) && sk == key) {
             occ += (mn[j].cnt >> (4 * k)) & 15u;
@@ -928,8 +934,15 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     lr.bl[0] = r0 < E.n ? E.rlenp[E.P.read_begin + r0] : 0u;
     if constexpr (R > 1) {
       const uint32_t r1 = (uint32_t)lane + 64u;
-      lr.rd[R - 1] = E.rbytes + (r1 < E.n ? E.roff[E.P.read_begin + r1] : 0ull);
-      lr.bl[R - 1] = r1 < E.n ? E.rlenp[E.P.read_begin + r1] : 0u;
+      lr.rd[1] = E.rbytes + (r1 < E.n ? E.roff[E.P.read_begin + r1] : 0ull);
+      lr.bl[1] = r1 < E.n ? E.rlenp[E.P.read_begin + r1] : 0u;
+    }
+    if constexpr (R > 2) {
+      const uint32_t r2 = (uint32_t)lane + 128u, r3 = (uint32_t)lane + 192u;
+      lr.rd[2] = E.rbytes + (r2 < E.n ? E.roff[E.P.read_begin + r2] : 0ull);
+      lr.bl[2] = r2 < E.n ? E.rlenp[E.P.read_begin + r2] : 0u;
+      lr.rd[3] = E.rbytes + (r3 < E.n ? E.roff[E.P.read_begin + r3] : 0ull);
+      lr.bl[3] = r3 < E.n ? E.rlenp[E.P.read_begin + r3] : 0u;
     }
   }
   const KArgs kp = kernel_args();
@@ -1259,7 +1272,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
 }
 
 // the claim loop: every problem on the build of its read count (R = 1 for
-// <= 64 reads, 2 for <= 128) when `mixed`, else on R's
+// <= 64 reads, 2 for <= 128, 4 for <= 256) when `mixed`, else on R's
 template <int R, bool mixed>
 __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* smem, Lo<Ctl>& ctl) {
   const int tid = threadIdx.x;
@@ -1279,8 +1292,10 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
       finish_problem(A, ctl, outp, prob, oslot);
       continue;
     }
-    if (mixed && E.n <= 64u) wave_problem<1, mixed ? 1 : 0>(A, E, ctl, prob, oslot, outp);
-    else wave_problem<R, mixed ? 1 : 0>(A, E, ctl, prob, oslot, outp);
+    constexpr int V = mixed ? R : 0;
+    if (mixed && E.n <= 64u) wave_problem<1, V>(A, E, ctl, prob, oslot, outp);
+    else if (mixed && R > 2 && E.n <= 128u) wave_problem<(R > 2 ? 2 : R), V>(A, E, ctl, prob, oslot, outp);
+    else wave_problem<R, V>(A, E, ctl, prob, oslot, outp);
   }
   stream_exit(A);
 }
