@@ -512,7 +512,7 @@ class Cfg5:
     (shard.prefix_tail_plan / SharedQueue; no collective on the data path)."""
     name = "cfg5"
     scaling = "strong"
-    kernel = "wcn::dual_engine_kernel"
+    kernel = "wcw::dual_wave2_kernel"
 
     @staticmethod
     def pregen(a, rank, world, total=None):
@@ -552,7 +552,7 @@ class Cfg5:
         else:
             self.store = shard.LocalStore()
         self.last, self.mine, self.busy_s, self.static_s = {}, [], 0.0, 0.0
-        self.t0, self.done, self.lat = 0.0, {}, {}
+        self.t0, self.done, self.lat, self.dlat = 0.0, {}, {}, {}
 
     def _run(self, ids):
         """One priority_consensus_batch call over loci `ids`; records each
@@ -568,6 +568,9 @@ class Cfg5:
         self.last.update(zip(ids, res))
         for i, pp in zip(ids, st.pop("per_problem")):
             self.lat[i] = pp["wall_ms"] / 1e3
+            # on the device: from its first sub-problem's publication (a
+            # locus that waited to be published is not slow for that)
+            self.dlat[i] = (pp["wall_ms"] - pp.get("start_ms", 0.0)) / 1e3
             self.done[i] = t_call - self.t0 + self.lat[i]
         return st
 
@@ -578,7 +581,7 @@ class Cfg5:
         from waffle_con_amd import shard
         self.k += 1
         q = shard.SharedQueue(self.store, len(self.tail), self.chunk, key="wc_cfg5_%d" % self.k)
-        self.last, self.mine, self.done, self.lat = {}, list(self.static), {}, {}
+        self.last, self.mine, self.done, self.lat, self.dlat = {}, list(self.static), {}, {}, {}
         t0 = self.t0 = time.perf_counter()
         tot = self._run(self.static)
         self.static_s = time.perf_counter() - t0
@@ -634,7 +637,8 @@ class Cfg5:
         import math
         h = max(range(self.total), key=lambda i: (self.costs[i], -i))
         mine = {"done": [self.done[i] for i in self.mine],
-                "slowest": max(((self.lat[i], i) for i in self.mine), default=(0.0, -1)),
+                "slowest": max(((self.dlat.get(i, self.lat[i]), i) for i in self.mine), default=(0.0, -1)),
+                "slow2": sorted(((self.dlat.get(i, self.lat[i]), i) for i in self.mine), reverse=True)[:2],
                 "heaviest": (self.lat[h], self.done[h]) if h in self.lat else None}
         if dist is None:
             rows = [mine]
@@ -647,10 +651,14 @@ class Cfg5:
             return done[min(len(done) - 1, max(0, int(math.ceil(f * len(done))) - 1))] if done else None
         hv = next((r["heaviest"] for r in rows if r["heaviest"] is not None), (None, None))
         slow = max(r["slowest"] for r in rows)
+        slow2 = sorted((x for r in rows for x in r["slow2"]), reverse=True)[:2]
         return {"t50_s": q(0.50), "t95_s": q(0.95), "t100_s": q(1.0),
                 "heaviest_locus": h, "heaviest_cost": self.costs[h],
                 "heaviest_latency_under_load_s": hv[0], "heaviest_done_s": hv[1],
-                "slowest_latency_under_load_s": slow[0], "slowest_locus": slow[1]}
+                "slowest_latency_under_load_s": slow[0], "slowest_locus": slow[1],
+                "slowest_two_loci": [x[1] for x in slow2],
+                "slowest_note": "latency on the device: from the publication of the locus's first sub-problem "
+                                "to its result (wc_stats start_ms / wall_ms)"}
 
     def heaviest_alone(self, h):
         """The heaviest locus alone on the GPU (one call, nothing else queued): s."""
@@ -749,7 +757,7 @@ class Cfg5Api:
     the same loci; every API result is checked against the batch path's."""
     name = "cfg5-api"
     scaling = "weak"
-    kernel = "wcn::dual_engine_kernel"
+    kernel = "wcw::dual_wave2_kernel"
 
     @staticmethod
     def pregen(a, rank, world, total=None):
@@ -886,13 +894,15 @@ WORKLOADS = {"cfg2": Cfg2, "cfg2-api": Cfg2Api, "cfg2-latency": Cfg2Latency, "cf
 # ---------------------------------------------------------------------------
 # roofline / profile records committed under profiles/
 # ---------------------------------------------------------------------------
-def profile_record(kind, workload_cfg):
-    """Latest committed PMC summary (profiles/r*_<kind>.json) recorded on this workload."""
+def profile_record(kind, workload_cfg, kernel=None):
+    """Latest committed PMC summary (profiles/r*_<kind>.json) recorded on this
+    workload (and, when given, on this kernel: a record of another build's
+    kernel does not describe this one)."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s.json" % kind)), reverse=True):
         with open(path) as f:
             rec = json.load(f)
-        if rec.get("workload") == workload_cfg:
+        if rec.get("workload") == workload_cfg and (kernel is None or rec.get("kernel") in (None, kernel)):
             rec["_file"] = os.path.relpath(path, ROOT)
             return rec
     return None
@@ -1014,7 +1024,7 @@ def main():
                "note": "rank 0's launches; kernel_ms sums the stream epochs' HIP-event times"}
         if rl5["achieved"] is not None:
             rl5["frac"] = rl5["achieved"] / HBM_PEAK_GBS
-        pmc5 = profile_record("pmc_traffic", C5.config()["workload"]) if world == 1 else None
+        pmc5 = profile_record("pmc_traffic", C5.config()["workload"], Cfg5.kernel) if world == 1 else None
         if pmc5:
             rl5["pmc_traffic_bytes_per_launch"] = pmc5["traffic_bytes_per_launch"]
             rl5["pmc_kernel_ms_per_launch"] = pmc5.get("kernel_ms_per_launch_bench_events")
@@ -1029,9 +1039,13 @@ def main():
             # the critical path a larger GPU count cannot shorten: the slowest
             # locus of the batch, alone; 8 GPUs cannot finish the batch before
             # it, so t_1gpu / (8 x that) bounds the 8-GPU efficiency
-            alone = C5.heaviest_alone(tail["slowest_locus"])
+            # (the two slowest on the device, each alone: the slowest under
+            # load need not be the slowest alone)
+            alones = {i: C5.heaviest_alone(i) for i in tail.get("slowest_two_loci") or [tail["slowest_locus"]]}
+            alone = alones.get(tail["slowest_locus"], max(alones.values()))
             cfg5_leg["tail"]["slowest_latency_alone_s"] = alone
-            crit = max(alone, cfg5_leg["tail"].get("heaviest_latency_alone_s") or 0.0)
+            cfg5_leg["tail"]["slowest_two_alone_s"] = {str(k): v for k, v in alones.items()}
+            crit = max(max(alones.values()), cfg5_leg["tail"].get("heaviest_latency_alone_s") or 0.0)
             cfg5_leg["tail"]["projected_8gpu_eff"] = min(1.0, el5 / (8.0 * crit)) if crit > 0 else None
         if rank == 0 and not a.no_cpu:
             # bounded oracle check of sampled loci (and, at N=1, the CPU baseline)
@@ -1057,7 +1071,7 @@ def main():
     cfgd = W.config()
     avg_kernel_s = kernel_ms / a.steps / 1e3
     ref_bytes = (8.0 * wout + 2.0 * cmp) / a.steps  # SURVEY §8(d) B_upd summed, per step
-    pmc = profile_record("pmc_traffic", cfgd["workload"])
+    pmc = profile_record("pmc_traffic", cfgd["workload"], W.kernel)
     traffic = pmc.get("traffic_bytes_per_launch") if pmc else None
     launches_per_step = launches / a.steps
     per_launch_s = avg_kernel_s / max(launches_per_step, 1)
@@ -1091,7 +1105,7 @@ def main():
         roofline["pmc_frac"] = roofline["pmc_achieved"] / HBM_PEAK_GBS
         roofline["pmc_source"] = pmc["_file"]
         roofline["traffic_over_model"] = traffic / model_bytes if model_bytes else None
-    issue = profile_record("issue_view", cfgd["workload"])
+    issue = profile_record("issue_view", cfgd["workload"], W.kernel)
     if issue:
         roofline["issue_view"] = {k: v for k, v in issue.items() if not k.startswith("_") and k != "workload"}
         roofline["issue_view"]["source"] = issue["_file"]

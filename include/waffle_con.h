@@ -238,6 +238,9 @@ typedef struct wc_stats {
   uint64_t launches;        /* engine kernel launches (incl. capacity retries) */
   double kernel_ms;         /* device time of the engine launches (HIP events) */
   double wall_ms;           /* host wall time of the whole call */
+  double start_ms;          /* per problem (wc_results_problem_stats): when its first engine work was
+                             * published to the device, from the start of the call (PriorityConsensusDWFA
+                             * batches; 0 elsewhere): wall_ms - start_ms is its latency on the device */
 } wc_stats;
 int wc_results_stats(const wc_results* r, wc_stats* out);
 /* per-problem counters (same fields; kernel_ms and launches zero; wall_ms =

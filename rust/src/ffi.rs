@@ -126,6 +126,7 @@ pub struct wc_stats {
     pub launches: u64,
     pub kernel_ms: f64,
     pub wall_ms: f64,
+    pub start_ms: f64,
 }
 
 #[repr(C)]

@@ -22,7 +22,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ENGINE = "engine_kernel"
+ENGINES = ("engine_kernel", "dual_wave")  # block engines, wave engine (engine_wave.hip)
 
 
 def counters(path):
@@ -32,7 +32,7 @@ def counters(path):
         return out
     with open(path) as f:
         for row in csv.DictReader(f):
-            if ENGINE in row["Kernel_Name"]:
+            if any(k in row["Kernel_Name"] for k in ENGINES):
                 out.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     return out
 
@@ -55,7 +55,7 @@ def main():
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, tag + "_kernel_stats.csv"))
     with open(os.path.join(src, "kt", "run_kernel_trace.csv")) as f:
         rows = [r for r in csv.reader(f)]
-    hdr, body = rows[0], [r for r in rows[1:] if any(ENGINE in c for c in r)]
+    hdr, body = rows[0], [r for r in rows[1:] if any(k in c for c in r for k in ENGINES)]
     with open(os.path.join(dst, tag + "_kernel_trace_engine.csv"), "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(hdr)

@@ -91,7 +91,8 @@ class WcStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "updates", "w_out", "compares", "ed_increases", "finalizes", "pops", "nodes_explored",
         "nodes_ignored", "peak_queue_size", "row_bytes", "launches")] + [("kernel_ms", ctypes.c_double),
-                                                            ("wall_ms", ctypes.c_double)]
+                                                            ("wall_ms", ctypes.c_double),
+                                                            ("start_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

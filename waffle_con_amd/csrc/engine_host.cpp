@@ -873,6 +873,7 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
         qrlen[q] = b->rlen_h[s.gid[r]];
       }
       seq_item.push_back(id);
+      items[id].t_pub = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
       seq_rw.push_back(rw);
       seq_done.push_back(0);
       rw += s.gid.size();
@@ -1082,6 +1083,9 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
   std::vector<std::vector<std::vector<uint8_t>>> assigns(n);
   std::vector<bool> alive(n, true);
   std::vector<uint64_t> owner_pops(n, 0);  // pops of each problem's finished sub-problems (SubProb::crit)
+  // when each problem's first sub-problem was published (ProbRes::start_ms)
+  std::vector<double> owner_start(n, -1.0);
+  const double t_call_ms = std::chrono::duration<double, std::milli>(t_call.time_since_epoch()).count();
   std::deque<uint32_t> ready, retry_ready;
 
   bool roots_made = false;  // sub-problems made after the roots are continuations
@@ -1309,6 +1313,10 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
       w.state = 2;
       o.recs.clear();
       owner_pops[w.owner] += w.res->stats[S_POPS];
+      if (subs[id].t_pub >= 0) {
+        const double st0 = subs[id].t_pub - t_call_ms;
+        if (owner_start[w.owner] < 0 || st0 < owner_start[w.owner]) owner_start[w.owner] = st0;
+      }
       expand(id);
       if (sublog) {
         // diagnostics: one line per finished sub-problem (the critical path of a locus)
@@ -1329,6 +1337,7 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
 
   for (uint32_t i = 0; i < n; ++i) {
     ProbRes& pr = R->probs[i];
+    pr.start_ms = std::max(0.0, owner_start[i]);
     if (pr.status != WC_OK) continue;
     priority_assemble(problems[i].n_chains, cons[i], assigns[i], pr);
   }

@@ -742,6 +742,7 @@ int wc_results_problem_stats(const wc_results* r, uint32_t p, wc_stats* o) {
   o->peak_queue_size = s[S_PEAKQ];
   o->row_bytes = s[S_ROWB];
   o->wall_ms = r->probs[p].done_ms;
+  o->start_ms = r->probs[p].start_ms;
   return WC_OK;
 }
 

@@ -180,6 +180,7 @@ struct ProbRes {
   std::vector<uint64_t> indices;
   uint64_t stats[wc::S_NSTAT] = {0};
   double done_ms = 0;  // from the start of the call until this problem's result was final
+  double start_ms = 0;  // from the start of the call until its first engine work was published (priority stream)
 };
 struct wc_results {
   int kind = 0;  // 0 single, 1 dual, 2 priority
@@ -231,6 +232,7 @@ struct SubProb {
   // this one was made (the stream publishes the continuations of the loci that
   // have run longest first: a deep locus's next sub-problem is on its critical path)
   uint64_t crit = 0;
+  double t_pub = -1;  // steady-clock ms when the stream published it (-1: not yet)
 };
 // auto_shift_offsets + activation points (consensus.rs:151-202) of one
 // problem; fills sp.act / n_active / max_act or returns an error code.

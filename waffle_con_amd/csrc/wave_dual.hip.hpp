@@ -257,29 +257,50 @@ __device__ inline void wave_select_t0(const DevConfig& cfg, Lo<Ctl>& ctl, const 
 }
 
 // the ED-increase loops (and wide frontiers) of the in-place push: one read
-// per wave, on the hot copy (the rows are the slot's). A call of its own: the
-// registers it saves and restores are its own few, not the general paths'.
+// per wave, on the hot copy (the rows are the slot's). A call of its own, with
+// what it needs as arguments: the general paths' call saved and restored 42
+// registers, and rebuilding the engine context from the kernel arguments
+// (callee_eng) cost most of a call.
 // (V: the kernel it is called from, so that each kernel's call has a body
 // compiled for that kernel's register budget)
+template <int R>
+struct HeavyArgs {
+  Sh<RState>* hot;
+  const Sh<uint32_t>* list;
+  Gm<uint32_t>* wf[2];
+  const Gm<uint8_t>* con[2];
+  const Gm<uint8_t>* rd[R];  // per lane: read lane + 64 j
+  uint32_t bl[R];
+  uint32_t list_cap, nmax, n, wcap, nl[2], sy[2];
+  int wc;
+  uint32_t early;
+};
 template <int R, int V>
-__device__ __noinline__ void wave_heavy_call(KArgs kp, DevProblem P, Sh<uint8_t>* sbase, Lo<Ctl>& ctl, uint32_t top,
-                                             uint32_t nl0, uint32_t nl1, uint32_t sy0, uint32_t sy1) {
-  Eng E = callee_eng(kp, P, sbase);
+__device__ __noinline__ void wave_heavy_call(HeavyArgs<R> h, Lo<Ctl>& ctl) {
   const int lane = lane_id();
-  const DevConfig& cfg = E.cfg;
-  const bool early = cfg.early != 0;
-  const uint32_t n = E.n;
-  const uint32_t nl[2] = {nl0, nl1};
-  const int sy[2] = {(int32_t)sy0, (int32_t)sy1};
   const uint32_t nh = uni(ctl.nheavy);
   WaveCounters cnt = {0, 0, 0, 0, 0, 0};
   for (uint32_t k = 0; k < nh; ++k) {
-    const uint32_t it = uni(E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))]);
-    const uint32_t sd = it >= n ? 1u : 0u, r = it - sd * n;
-    SideView v = E.sv(top, sd);
+    const uint32_t it = uni(h.list[WC_IX(k, h.list_cap)]);
+    const uint32_t sd = it >= h.n ? 1u : 0u, r = it - sd * h.n;
+    // read r's bytes and length from the lane that holds it
+    const uint32_t j = r >> 6, l = r & 63u;
+    const Gm<uint8_t>* rp = h.rd[0];
+    uint32_t bl = h.bl[0];
+#pragma unroll
+    for (int q = 1; q < R; ++q)
+      if (j == (uint32_t)q) {
+        rp = h.rd[q];
+        bl = h.bl[q];
+      }
+    const uint64_t pv = (uint64_t)rp;
+    const Gm<uint8_t>* rd = (const Gm<uint8_t>*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pv >> 32), l) << 32) |
+                                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pv, l));
+    bl = (uint32_t)__builtin_amdgcn_readlane((int)bl, l);
     uint32_t e = 0;
-    const bool ok = wave_heavy(&E.L.hot[sd * E.nmax + r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
-                               nl[sd], (uint8_t)sy[sd], cfg.wildcard, early, E.wcap, cnt, e);
+    const bool ok = wave_heavy(&h.hot[sd * h.nmax + r], (sd ? h.wf[1] : h.wf[0]) + (uint64_t)r * h.wcap, rd, bl,
+                               sd ? h.con[1] : h.con[0], sd ? h.nl[1] : h.nl[0], (uint8_t)(sd ? h.sy[1] : h.sy[0]), h.wc,
+                               h.early != 0, h.wcap, cnt, e);
     __builtin_amdgcn_wave_barrier();
     if (!ok && lane == 0) atomicOr(&ctl.ovf, 4u);
   }
@@ -678,7 +699,32 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
       ctl.ovf = 0;
     }
     __syncthreads();
-    wave_heavy_call<R, V>(kp, E.P, (Sh<uint8_t>*)E.L.hot, ctl, top, nl[0], nl[1], (uint32_t)sy[0], (uint32_t)sy[1]);
+    {
+      HeavyArgs<R> h;
+      h.hot = E.L.hot;
+      h.list = E.L.list;
+      const SideView v0 = E.sv(top, 0), v1 = E.sv(top, tdual ? 1 : 0);
+      h.wf[0] = v0.wf;
+      h.wf[1] = v1.wf;
+      h.con[0] = v0.con;
+      h.con[1] = v1.con;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        h.rd[j] = lr.rd[j];
+        h.bl[j] = lr.bl[j];
+      }
+      h.list_cap = list_entries(E.sides, E.nmax);
+      h.nmax = E.nmax;
+      h.n = n;
+      h.wcap = E.wcap;
+      h.nl[0] = nl[0];
+      h.nl[1] = nl[1];
+      h.sy[0] = (uint32_t)sy[0];
+      h.sy[1] = (uint32_t)sy[1];
+      h.wc = cfg.wildcard;
+      h.early = early ? 1u : 0u;
+      wave_heavy_call<R, V>(h, ctl);
+    }
     SUB_T1(54, t_hv);
     const uint32_t ovf = uni(ctl.ovf);
     // (per-lane branches without continue, and the uniform status after
