@@ -2550,12 +2550,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WC_WAVE
   __shared__ Ctl ctl_lds;
   dual_main_wave<2, true>(A, smem, *(Lo<Ctl>*)&ctl_lds);
 }
-// launches with problems of 129-256 reads (four per lane; cfg3)
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WC_WAVE2_WPE))) dual_wave4_kernel(EngineArgs A) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ Ctl ctl_lds;
-  dual_main_wave<4, true>(A, smem, *(Lo<Ctl>*)&ctl_lds);
-}
 #elif !defined(WC_SINGLE_ONLY)  // (engine_cu.hip: the single engine only)
 // two kernels, one per dual_hot: in one kernel the two paths' register
 // allocations merge (the 4-wave build spilled 236 VGPRs instead of 84)
@@ -2640,16 +2634,13 @@ int engine_waves() { return kEW; }
 #ifdef WC_WAVE_DUAL
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
   if (a.nmax <= 64) hipLaunchKernelGGL(dual_wave1_kernel, dim3(grid), dim3(64), lds, s, a);
-  else if (a.nmax <= 128) hipLaunchKernelGGL(dual_wave2_kernel, dim3(grid), dim3(64), lds, s, a);
-  else hipLaunchKernelGGL(dual_wave4_kernel, dim3(grid), dim3(64), lds, s, a);
+  else hipLaunchKernelGGL(dual_wave2_kernel, dim3(grid), dim3(64), lds, s, a);
 }
 // workgroups per CU of the build that runs problems of nmax reads
 int wave_blocks_per_cu(uint32_t nmax, size_t lds) {
   int nb = 0;
-  const hipError_t e =
-      nmax <= 64    ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave1_kernel, 64, lds)
-      : nmax <= 128 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave2_kernel, 64, lds)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave4_kernel, 64, lds);
+  const hipError_t e = nmax <= 64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave1_kernel, 64, lds)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave2_kernel, 64, lds);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
 #elif !defined(WC_SINGLE_ONLY)

@@ -189,9 +189,7 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   // locus 5949's critical path 17.2 -> 12.7 s, cfg3 210 -> 212 loci/s.
   // WC_WAVE=0 keeps them on the block engines.
   const char* wvenv = getenv("WC_WAVE");
-  // (WC_WAVE=2: also problems of 129-256 reads, four per lane)
-  const uint32_t wmax = (wvenv && atoi(wvenv) == 2) ? 256u : 128u;
-  c.wave = sides == 2 && chain == 0 && !gstate && !any_act && nmax <= wmax && !(wvenv && atoi(wvenv) == 0) &&
+  c.wave = sides == 2 && chain == 0 && !gstate && !any_act && nmax <= 128 && !(wvenv && atoi(wvenv) == 0) &&
            lds_bytes(sides, pcap, nmax, 0, 1) <= kLdsMax;
   if (c.wave) c.narrow = c.lowlat = c.cu = false;
   c.waves = c.cu ? (uint32_t)std::max(sides == 1 ? wcu::engine_waves() : wcv::engine_waves(), kWaves) : (uint32_t)kWaves;

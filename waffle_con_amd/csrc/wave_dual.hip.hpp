@@ -1318,7 +1318,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
 }
 
 // the claim loop: every problem on the build of its read count (R = 1 for
-// <= 64 reads, 2 for <= 128, 4 for <= 256) when `mixed`, else on R's
+// <= 64 reads, 2 for <= 128) when `mixed`, else on R's
 template <int R, bool mixed>
 __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* smem, Lo<Ctl>& ctl) {
   const int tid = threadIdx.x;
@@ -1340,7 +1340,6 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
     }
     constexpr int V = mixed ? R : 0;
     if (mixed && E.n <= 64u) wave_problem<1, V>(A, E, ctl, prob, oslot, outp);
-    else if (mixed && R > 2 && E.n <= 128u) wave_problem<(R > 2 ? 2 : R), V>(A, E, ctl, prob, oslot, outp);
     else wave_problem<R, V>(A, E, ctl, prob, oslot, outp);
   }
   stream_exit(A);
