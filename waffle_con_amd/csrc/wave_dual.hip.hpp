@@ -36,32 +36,22 @@
 struct Tips {
   uint32_t lo, hi, valid;
 };
-// Branch-free over the slots below the wave's highest live slot (a uniform
-// bound): the per-slot conditions select, the loads are unconditional (read
-// byte 0 for a slot without a tip), so no exec-mask branch per slot.
-// the highest live slot + 1 over the active lanes: ballots (exact under any
-// exec mask, unlike a DPP reduction, whose disabled lanes keep stale values)
-__device__ __forceinline__ uint32_t front_hi(const Front& f) {
-  uint32_t m = 0;
-#pragma unroll
-  for (int k = 0; k < kF; ++k) m |= ballot(((f.mask >> k) & 1u) != 0u) ? (1u << k) : 0u;
-  return m ? 32u - (uint32_t)__builtin_clz(m) : 0u;
-}
 __device__ __forceinline__ Tips tips_fetch(const Front& f, const Gm<uint8_t>* rd, uint32_t blen, uint32_t len) {
   Tips t = {0, 0, 0};
-  const uint32_t hmax = front_hi(f);
+  uint32_t rank = 0;
+  const uint32_t hi = f.mask ? 32u - (uint32_t)__builtin_clz(f.mask) : 0u;
 #pragma unroll
   for (int k = 0; k < kF; ++k) {
-    if ((uint32_t)k >= hmax) break;
-    const bool live = (f.mask >> k) & 1u;
+    if ((uint32_t)k >= hi) break;
+    if (!(f.mask & (1u << k))) continue;
     const uint32_t bo = f.fd[k] + f.e - f.fi[k];
-    const bool v = live && f.fd[k] + f.off == len && bo < blen;
-    const uint32_t b = rd[v ? bo : 0u];
-    const uint32_t rank = (uint32_t)__builtin_popcount(f.mask & ((1u << k) - 1u));
-    const uint32_t sh = 8u * (rank & 3u);
-    t.valid |= v ? (1u << rank) : 0u;
-    t.lo |= (v && rank < 4) ? (b << sh) : 0u;
-    t.hi |= (v && rank >= 4) ? (b << sh) : 0u;
+    if (f.fd[k] + f.off == len && bo < blen) {
+      const uint32_t b = rd[bo];
+      t.valid |= 1u << rank;
+      if (rank < 4) t.lo |= b << (8 * rank);
+      else t.hi |= b << (8 * (rank - 4));
+    }
+    rank++;
   }
   return t;
 }
@@ -71,41 +61,6 @@ __device__ __forceinline__ void tips_unpack(const Tips& t, uint32_t (&x)[kF]) {
     const uint32_t b = ((k < 4 ? t.lo : t.hi) >> (8 * (k & 3))) & 0xFFu;
     x[k] = (t.valid >> k) & 1u ? b : 0x100u;
   }
-}
-
-// thread_apply (engine_common.hip.hpp: the extend step of DWFALite::update
-// for one appended symbol on the frontier) without a branch per slot: the
-// conditions select, only the row store of an advancing tip is predicated.
-__device__ __forceinline__ bool wave_thread_apply(Front& f, const uint32_t (&x)[kF], uint32_t blen, uint32_t old_len,
-                                                  uint8_t sym, int wc, bool early, Gm<uint32_t>* wf_row,
-                                                  uint32_t& cmp) {
-  const uint32_t hmax = front_hi(f);
-  const uint32_t wcs = wc >= 0 ? (uint32_t)(uint8_t)wc : 0x200u;
-  uint32_t c = f.nscmp, mb = 0, ns = f.nscmp, maxb = f.maxb, mask = f.mask;
-#pragma unroll
-  for (int k = 0; k < kF; ++k) {
-    if ((uint32_t)k >= hmax) break;
-    const bool live = (f.mask >> k) & 1u;
-    const uint32_t d = f.fd[k];
-    const uint32_t bo = d + f.e - f.fi[k];
-    const bool tip = live && d + f.off == old_len;
-    const bool inr = tip && bo < blen;
-    const bool adv = inr && (x[k] == sym || x[k] == wcs);
-    c += inr ? 1u : 0u;
-    ns += (inr && !adv) ? 1u : 0u;  // stuck on a mismatch: compared on every later push
-    if (adv) wf_row[f.fi[k]] = d + 1;
-    f.fd[k] = adv ? d + 1 : d;
-    mb = max(mb, adv ? bo + 1 : ((live && !tip) ? bo : 0u));
-    const bool stuck = tip && !adv;
-    maxb = stuck ? max(maxb, bo) : maxb;
-    mask &= stuck ? ~(1u << k) : ~0u;
-  }
-  f.nscmp = ns;
-  f.maxb = maxb;
-  f.mask = mask;
-  mb = max(mb, maxb);
-  cmp = c;
-  return mask == 0 && !(early && mb == blen);
 }
 
 // thread_nominate on prefetched tip bytes (same arithmetic: every live slot
@@ -706,7 +661,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
             uint32_t x[kF];
             tips_unpack(tx[j][sd], x);
             uint32_t cmp = 0;
-            heavy = wave_thread_apply(f, x, lr.bl[j], nl[sd] - 1, (uint8_t)sy[sd], cfg.wildcard, early,
+            heavy = thread_apply(f, x, lr.bl[j], nl[sd] - 1, (uint8_t)sy[sd], cfg.wildcard, early,
                                  E.sv(top, sd).wf + (uint64_t)r * E.wcap, cmp);
             cmps += cmp;
             front_store(hp, f);  // (a heavy read's ED-increase loop goes on from it)
