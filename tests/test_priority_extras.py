@@ -144,3 +144,26 @@ def test_gpu_priority_error_mid_stack_vs_oracle(priority_path):
     chains = _chains(800, n_hap=2, per=5, L=150)
     offsets = [[None, 5 + (i % 4)] for i in range(len(chains))]
     _cmp_priority(hip, chains, offsets=offsets, min_count=2, wildcard=ord("*"), auto_shift_offsets=False)
+
+
+@pytest.mark.gpu
+def test_gpu_priority_batch_per_problem_start_times():
+    """wc_stats.start_ms (per problem of a PriorityConsensusDWFA batch): when
+    its first sub-problem was published to the device, from the start of the
+    call; never after its result (wall_ms), and the results and counters are
+    the oracle's for every locus."""
+    import waffle_con_amd as w
+    from waffle_con_amd.cdwfa_config import CdwfaConfig
+    from waffle_con_amd import synth
+    loci = [synth.cfg5_locus(s) for s in range(6)]
+    res, st = w.priority_consensus_batch([(ch, None, None) for ch in loci], CdwfaConfig(wildcard=ord("*")),
+                                         per_problem=True)
+    pp = st["per_problem"]
+    assert len(pp) == len(loci)
+    for chains, r, p in zip(loci, res, pp):
+        assert 0.0 <= p["start_ms"] <= p["wall_ms"]
+        exp, ec = orc.priority_consensus(chains, counters=True, wildcard=ord("*"))
+        assert [[c.sequence() for c in ch] for ch in r.consensuses()] == \
+            [[c["sequence"] for c in ch] for ch in exp["consensuses"]]
+        for k in ("pops", "updates", "w_out", "compares", "ed_increases"):
+            assert p[k] == ec[k], k
