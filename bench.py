@@ -711,10 +711,10 @@ class Cfg4(Cfg5):
         self.gen_s = time.perf_counter() - t0
         self.upload_s = 0.0
         self.last, self.mine, self.busy_s, self.static_s = {}, [], 0.0, 0.0
-        self.t0, self.done, self.lat = 0.0, {}, {}
+        self.t0, self.done, self.lat, self.dlat = 0.0, {}, {}, {}
 
     def step(self):
-        self.last, self.mine, self.done, self.lat = {}, [0], {}, {}
+        self.last, self.mine, self.done, self.lat, self.dlat = {}, [0], {}, {}, {}
         t0 = self.t0 = time.perf_counter()
         st = self._run([0])
         self.busy_s = self.static_s = time.perf_counter() - t0

@@ -534,7 +534,7 @@ __device__ __noinline__ GHOut chain_group_heavy(Lo<Ctl>& ctl, uint32_t j, uint32
       if ((fm >> (16 * q)) & 1ull) bak |= 1ull << ls[q];
     __builtin_amdgcn_wave_barrier();
   }
-  const GroupOut go = group_edinc(gact, gtmp, gwf, rd, blen, con, L0 + jl, wc, early, wcap);
+  const GroupOut go = group_edinc<16>(gact, gtmp, gwf, rd, blen, con, L0 + jl, wc, early, wcap);
   uint32_t st = go.st, e_out = go.e;
   uint32_t t_ed = go.edinc, t_up = go.updates, t_wo = go.w_out, t_rb = go.rowb, t_cm = go.cmp;
   // rows that outgrew the group's registers (rare): the wave goes on with each

@@ -1535,6 +1535,15 @@ __device__ inline void finish_problem(const EngineArgs& A, Lo<Ctl>& ctl, uint8_t
 // block-wide pass, and a group of children costs the latency of one.
 // kDH (dual_hot): the popped node's RStates are the LDS copy (Lds::hot); the
 // clones copy them into their slots, the in-place child is pushed there.
+// the dual pushes' grouped ED increases (group_edinc): 8-lane groups, eight
+// reads per wave, for rows of at most 64 entries; longer rows one read per
+// wave (wave_heavy). Measured on cfg3 (200 reads, one box): 16-lane groups
+// (four reads per wave, rows to 128) 214 loci/s, 8-lane groups 233; on
+// another box 8-lane groups 216 against 212-215 for spreading each round's
+// items evenly over the waves, 16-lane groups for the rows of 65-128 entries,
+// or both, and 4-lane groups (16 reads per wave, rows to 32) 220 vs 233.
+constexpr uint32_t kRowPush = 8u * kQ16;
+
 template <bool kDH>
 __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, const SlotMeta& tm, bool tdual,
                                            uint32_t nc) {
@@ -1602,8 +1611,8 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     PH_MARK(4);
     // pushes: every (child, side) that appends a symbol, thread per read.
     // Reads that need the ED-increase loop go to the group list (rows that fit
-    // kRow16, four reads per wave) or, for wide frontiers and long rows, to
-    // the wave list (filled from the top of E.L.list)
+    // kRow16, eight or four reads per wave) or, for wide frontiers and long
+    // rows, to the wave list (filled from the top of E.L.list)
     const uint32_t lend = (uint32_t)list_entries(2, E.nmax) - 1;
     WaveCounters tc = {0, 0, 0, 0, 0, 0};
     for (uint32_t q = 0; q < 2 * cn; ++q) {
@@ -1641,7 +1650,8 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
               tc.compares += cmp;
               front_store(&rsb[r], f);
               if (heavy) {
-                kind = 2 * f.e + 3 <= kRow16 ? 1u : 2u;
+                const uint32_t w2 = 2 * f.e + 3;
+                kind = w2 <= kRowPush ? 1u : 2u;
               } else {
                 tc.updates++;
                 tc.w_out += 2 * f.e + 1;
@@ -1662,7 +1672,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     flush_thread_counters(ctl, tc);
     __syncthreads();
     PH_MARK(5);
-    // the ED-increase loops: four reads per wave in 16-lane groups ...
+    // the ED-increase loops: eight reads per wave in 8-lane groups ...
     const uint32_t nh = uni(ctl.nheavy), nw = uni(ctl.nwide);
     SUB_CNT(16, nh);
     SUB_CNT(17, nw);
@@ -1671,8 +1681,10 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     GroupCnt gc = {0, 0, 0, 0, 0};
     // (up to one item per wave the 64-lane path is quicker: it goes to the wave loop)
     const uint32_t ng = nh > (uint32_t)kEW ? nh : 0u;
-    for (uint32_t b0 = wave_id() * 4u; b0 < ng; b0 += kEW * 4u) {
-      const uint32_t k = b0 + ((uint32_t)lane >> 4);
+    // (8-lane groups: eight reads per wave, rows of at most kRowPush entries)
+    constexpr uint32_t G = 8u;
+    for (uint32_t b0 = wave_id() * (64u / G); b0 < ng; b0 += kEW * (64u / G)) {
+      const uint32_t k = b0 + ((uint32_t)lane / G);
       const bool act = k < ng;
       const uint32_t it = act ? E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))] : 0u;
       const uint32_t q = it / n, r = it - q * n;
@@ -1682,22 +1694,22 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       GroupOut go;
       if constexpr (kDH) {
         const RSg rp = slot == top ? rs_generic(E.L.hot + sd * E.nmax + r) : rs_generic(&v.rs[r]);
-        go = group_edinc(act, rp, v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con, E.L.meta[slot].len[sd],
+        go = group_edinc<G>(act, rp, v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con, E.L.meta[slot].len[sd],
                          cfg.wildcard, early, E.wcap);
       } else {
-        go = group_edinc(act, &v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
+        go = group_edinc<G>(act, &v.rs[r], v.wf + (uint64_t)r * E.wcap, E.read(r), E.rlen(r), v.con,
                          E.L.meta[slot].len[sd], cfg.wildcard, early, E.wcap);
       }
       const uint32_t g = go.st, e = go.e;
-      if (act && (lane & 15) == 0 && g == kG_DONE) E.L.ce[WC_IX((uint64_t)q * E.nmax + r, (uint64_t)2 * kNCB * E.nmax)] = ce16(e);
+      if (act && (lane & (G - 1)) == 0 && g == kG_DONE) E.L.ce[WC_IX((uint64_t)q * E.nmax + r, (uint64_t)2 * kNCB * E.nmax)] = ce16(e);
       gc.edinc += go.edinc;
       gc.updates += go.updates;
       gc.w_out += go.w_out;
       gc.cmp += go.cmp;
       gc.rowb += go.rowb;
-      if (act && (lane & 15) == 0 && g == kG_WCAP) atomicOr(&ctl.ovf, 4u);
+      if (act && (lane & (G - 1)) == 0 && g == kG_WCAP) atomicOr(&ctl.ovf, 4u);
       // ... a row that outgrew the group finishes with the whole wave
-      uint64_t mem = ballot(act && (lane & 15) == 0 && g == kG_MEM);
+      uint64_t mem = ballot(act && (lane & (G - 1)) == 0 && g == kG_MEM);
       while (mem) {
         const int src = __builtin_ctzll(mem);
         mem &= mem - 1;

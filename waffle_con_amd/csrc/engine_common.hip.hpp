@@ -997,18 +997,30 @@ __device__ inline bool wave_heavy(P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd
   return true;
 }
 
-// ---- the ED-increase loop for four reads per wave (16-lane groups) ----
+// ---- the ED-increase loop for four (eight) reads per wave, 16-lane (8-lane) groups ----
 // A push's ED-increase work (dynamic_wfa.rs:84-91) is a short chain of
 // dependent memory round trips per read (RState, row, the extend's read and
 // consensus bytes), so one read per wave leaves the wave waiting on one chain
-// at a time. Here each 16-lane group of a wave runs its own read's loop, the
-// row held lane-strided (entry 16 q + gl in v[q]) for W <= kRow16, so four
+// at a time. Here each G-lane group of a wave runs its own read's loop, the
+// row held lane-strided (entry G q + gl in v[q]) for W <= G kQ16, so 64 / G
 // reads' chains overlap. Same arithmetic as wave_heavy's register path.
 constexpr int kQ16 = 8;
 constexpr uint32_t kRow16 = 16u * kQ16;
 
-__device__ __forceinline__ uint32_t grp_max(uint32_t v) { return row_max_u32(v); }
-__device__ __forceinline__ uint32_t grp_sum(uint32_t v) { return row_sum_u32(v); }
+template <int G>
+__device__ __forceinline__ uint32_t grp_max(uint32_t v) {
+  if constexpr (G == 16) return row_max_u32(v);
+  v = max(v, dpp_u32<0xb1>(v));  // quad_perm [1,0,3,2]
+  v = max(v, dpp_u32<0x4e>(v));  // quad_perm [2,3,0,1]
+  return max(v, dpp_u32<0x141>(v));  // row_half_mirror (within 8 lanes)
+}
+template <int G>
+__device__ __forceinline__ uint32_t grp_sum(uint32_t v) {
+  if constexpr (G == 16) return row_sum_u32(v);
+  v += dpp_u32<0xb1>(v);
+  v += dpp_u32<0x4e>(v);
+  return v + dpp_u32<0x141>(v);
+}
 
 // Outcome per group: kG_DONE (RState rebuilt), kG_WCAP (wavefront capacity),
 // kG_MEM (the row outgrew kRow16: stored back with e = `e_out`, the loop goes
@@ -1023,13 +1035,15 @@ struct GroupOut {
 };
 // (P: the RState pointer, an HBM slot or, dual_hot, a generic pointer that
 // may point into the LDS copy of the popped node)
-template <class P>
+template <int G, class P>
 __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, const Gm<uint8_t>* rd,
                                              uint32_t blen, const Gm<uint8_t>* con, uint32_t olen, int wc,
                                              bool early, uint32_t wcap) {
+  static_assert(G == 16 || G == 8, "group width");
+  constexpr uint32_t kRowG = (uint32_t)G * kQ16;
   GroupOut go_ = {kG_DONE, 0, 0, 0, 0, 0, 0};
   const int lane = lane_id();
-  const uint32_t gl = (uint32_t)lane & 15u, gb = (uint32_t)lane & ~15u;
+  const uint32_t gl = (uint32_t)lane & (G - 1u), gb = (uint32_t)lane & ~(G - 1u);
   uint32_t e = 0, off = 0;
   if (act) {
     e = rsp->e;
@@ -1047,15 +1061,15 @@ __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, 
   uint32_t v[kQ16];
 #pragma unroll
   for (int q = 0; q < kQ16; ++q) {
-    const uint32_t j = 16u * q + gl;
+    const uint32_t j = (uint32_t)G * q + gl;
     v[q] = 0u;
-    if (16u * q < wlim && act && j < W) v[q] = wf[j];
+    if ((uint32_t)G * q < wlim && act && j < W) v[q] = wf[j];
   }
   uint32_t st = act ? kG_RUN : kG_DONE;
   uint32_t mb = 0, cmp = 0;
   while (ballot(st == kG_RUN)) {
     if (st == kG_RUN && W + 2 > wcap) st = kG_WCAP;
-    else if (st == kG_RUN && W + 2 > kRow16) st = kG_MEM;
+    else if (st == kG_RUN && W + 2 > kRowG) st = kG_MEM;
     const bool go = st == kG_RUN;  // group-uniform
     wlim += 2;
     // increase_edit_distance: W -> W + 2 (lane moves run on every lane).
@@ -1063,11 +1077,21 @@ __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, 
     // rotations of per-lane selections of v[q] and v[q - 1] (row_ror).
 #pragma unroll
     for (int q = kQ16 - 1; q >= 0; --q) {
-      if (16u * q >= wlim) continue;
-      const uint32_t j = 16u * q + gl;
+      if ((uint32_t)G * q >= wlim) continue;
+      const uint32_t j = (uint32_t)G * q + gl;
       const uint32_t prev = q > 0 ? v[q > 0 ? q - 1 : 0] : 0u;
-      const uint32_t m1 = row_ror1(gl == 15 ? prev : v[q]);
-      const uint32_t m2 = row_ror2(gl >= 14 ? prev : v[q]);
+      uint32_t m1, m2;
+      if constexpr (G == 16) {
+        m1 = row_ror1(gl == 15 ? prev : v[q]);
+        m2 = row_ror2(gl >= 14 ? prev : v[q]);
+      } else {
+        // two groups per 16-lane row: a group's first lanes take their
+        // group's last lanes of the previous block (row_ror 9 / 10)
+        const uint32_t p1 = dpp_u32<0x129>(prev), p2 = dpp_u32<0x12a>(prev);
+        const uint32_t r1 = row_ror1(v[q]), r2 = row_ror2(v[q]);
+        m1 = gl == 0 ? p1 : r1;
+        m2 = gl <= 1 ? p2 : r2;
+      }
       uint32_t x = 0;
       if (j < W) x = v[q];
       if (j >= 1 && j <= W) x = max(x, m1 + 1);
@@ -1085,10 +1109,10 @@ __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, 
     uint64_t xa[kQ16], ya[kQ16];
 #pragma unroll
     for (int q = 0; q < kQ16; ++q) {
-      const uint32_t j = 16u * q + gl;
+      const uint32_t j = (uint32_t)G * q + gl;
       const uint32_t bo = v[q] + e - j, oo = v[q] + off;
       xa[q] = ya[q] = 0;
-      if (16u * q >= wlim) continue;
+      if ((uint32_t)G * q >= wlim) continue;
       if (go && j < W && bo < blen && oo < olen) {
         xa[q] = load8(rd, bo);
         ya[q] = load8(con, oo);
@@ -1097,8 +1121,8 @@ __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, 
     uint32_t lmo = 0, lmb = 0;
 #pragma unroll
     for (int q = 0; q < kQ16; ++q) {
-      const uint32_t j = 16u * q + gl;
-      if (16u * q >= wlim) continue;
+      const uint32_t j = (uint32_t)G * q + gl;
+      if ((uint32_t)G * q >= wlim) continue;
       if (!(go && j < W)) continue;
       uint32_t d = v[q];
       const uint32_t bo = d + e - j, oo = d + off;
@@ -1122,8 +1146,8 @@ __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, 
       lmo = max(lmo, d);
       lmb = max(lmb, d + e - j);
     }
-    lmo = grp_max(lmo);
-    lmb = grp_max(lmb);
+    lmo = grp_max<G>(lmo);
+    lmb = grp_max<G>(lmb);
     if (go) {
       mb = lmb;
       if (!(lmo + off < olen && !(early && lmb == blen))) st = kG_DONE;
@@ -1136,8 +1160,8 @@ __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, 
   // the row back to memory
 #pragma unroll
   for (int q = 0; q < kQ16; ++q) {
-    const uint32_t j = 16u * q + gl;
-    if (16u * q < wlim && j < W) wf[j] = v[q];
+    const uint32_t j = (uint32_t)G * q + gl;
+    if ((uint32_t)G * q < wlim && j < W) wf[j] = v[q];
   }
   // row traffic: the load now; the store when the update ends here (a row
   // that outgrew the group is stored by wave_edinc_mem)
@@ -1149,13 +1173,13 @@ __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, 
   uint32_t nf = 0, mbx = 0, nsc = 0;
 #pragma unroll
   for (int q = 0; q < kQ16; ++q) {
-    if (16u * q >= wlim) continue;
-    const uint32_t j = 16u * q + gl;
+    if ((uint32_t)G * q >= wlim) continue;
+    const uint32_t j = (uint32_t)G * q + gl;
     const bool valid = j < W;
     const uint32_t d = v[q];
     const uint32_t bo = d + e - j;
     const bool inF = valid && d + off >= olen;
-    const uint32_t m = (uint32_t)(ballot(inF) >> gb) & 0xFFFFu;
+    const uint32_t m = (uint32_t)(ballot(inF) >> gb) & ((1u << G) - 1u);
     const uint32_t pos = nf + (uint32_t)__popc(m & ((1u << gl) - 1u));
     if (inF && pos < (uint32_t)kF) {
       rsp->fi[pos] = (uint16_t)j;
@@ -1168,8 +1192,8 @@ __device__ __noinline__ GroupOut group_edinc(bool act, P rsp, Gm<uint32_t>* wf, 
     }
   }
   (void)mb;
-  mbx = grp_max(mbx);
-  nsc = grp_sum(nsc);
+  mbx = grp_max<G>(mbx);
+  nsc = grp_sum<G>(nsc);
   if (gl == 0) {
     rsp->e = e;
     rsp->maxb = mbx;
