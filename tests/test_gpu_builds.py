@@ -5,7 +5,8 @@ the 128-thread build (engine_narrow.hip; WC_NARROW bit 0 = single engine,
 bit 1 = dual engine, default 2), the global-state build (WC_GSTATE), the
 1024-thread single engine (engine_cu.hip, the default for batch launches of
 at most one problem per CU; WC_CU=1 forces it, WC_CU=0 keeps it off in the
-other variants), each dual build with dual_hot forced on, and the one-wave
+other variants; dual problems keep their 4-wave build there: the dual engine
+has no whole-CU build), each dual build with dual_hot forced on, and the one-wave
 dual engine (engine_wave.hip, the default for dual problems without offsets;
 WC_WAVE=0 in every other variant). The build is picked per launch from
 the environment (engine_host.cpp plan_caps), so one process exercises all of
@@ -39,7 +40,7 @@ BUILDS = {"wide": {"WC_NARROW": "0", "WC_LOWLAT": "0"}, "lowlat": {"WC_NARROW": 
 ENGINES = {"wide": ("lds.single", "lds.dual"), "lowlat": ("lowlat.single", "lowlat.dual"),
            "narrow-single": ("narrow.single", "lowlat.dual"), "narrow-dual": ("lowlat.single", "narrow.dual"),
            "narrow": ("narrow.single", "narrow.dual"), "gstate": ("gstate.single", "gstate.dual"),
-           "cu": ("cu.single", "cu.dual"), "wide-hot": ("lds.single", "lds.dual"),
+           "cu": ("cu.single", "narrow.dual"), "wide-hot": ("lds.single", "lds.dual"),
            "lowlat-hot": ("lowlat.single", "lowlat.dual"), "narrow-hot": ("lowlat.single", "narrow.dual"),
            "wave": ("lowlat.single", "wave.dual")}
 KNOBS = ("WC_NARROW", "WC_GSTATE", "WC_LOWLAT", "WC_DUAL_HOT", "WC_CU", "WC_WAVE", "WC_CHAIN", "WC_DUAL_CHAIN")

@@ -984,7 +984,8 @@ __device__ inline void chain_votes(Eng& E, Lo<Ctl>& ctl, uint32_t Keff, uint32_t
     uint32_t m = 0, key = 0;
     double val = 0.0;
     bool ok = wave_votes_core([&](uint32_t r) { return nom_decode(E.L.cnom[r * (K + 1) + j], E.L.covf, pj); },
-                              [&](uint32_t) { return 1.0; }, E.n, false, multi != 0, cfg.wildcard, m, key, val);
+                              [&](uint32_t) { return 1.0; }, E.n, false, multi != 0, cfg.wildcard, cfg.min_count,
+                              cfg.min_af == 0.0, m, key, val);
     if (ok) {
       const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
       const double thr = fmin((double)cfg.min_count, max_obs);

@@ -407,8 +407,8 @@ __device__ inline void dual_chain_votes(Eng& E, Lo<Ctl>& ctl, const DualChainAre
         uint32_t m = 0, key = 0;
         double val = 0.0;
         bool vok = wave_votes_core([&](uint32_t r) { return nom_load(nom, E.L.covf, r); },
-                                   [&](uint32_t) { return 1.0; }, E.n, false, step_nmulti(ef) != 0, cfg.wildcard, m,
-                                   key, val);
+                                   [&](uint32_t) { return 1.0; }, E.n, false, step_nmulti(ef) != 0, cfg.wildcard,
+                                   cfg.min_count, cfg.min_af == 0.0, m, key, val);
         if (vok) {
           const double max_obs = m ? wave_max_f64((uint32_t)lane < m ? val : 0.0) : (double)cfg.min_count;
           const double thr = fmin((double)cfg.min_count, max_obs);

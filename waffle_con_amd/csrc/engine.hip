@@ -1215,7 +1215,7 @@ struct SymSet {
 // its f64 vote. Returns false when more than kKout distinct symbols occur.
 template <class Load, class Weight>
 __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, bool weighted, bool multi, int wc,
-                                       uint32_t& m_out, uint32_t& key_out, double& val_out,
+                                       uint64_t mc, bool odd_ok, uint32_t& m_out, uint32_t& key_out, double& val_out,
                                        Lo<uint64_t>* ph = nullptr, Lo<FxCache>* fxc = nullptr) {
   const int lane = lane_id();
 #ifdef WC_PHASE_PROF
@@ -1334,13 +1334,19 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
   VOTE_T(29);
   // 3. per-key sums; lane k keeps key k's running sum
   double accv = 0.0;
-  // Unweighted votes: a read adds occ/split (tips) to each of its symbols. A
-  // single-symbol read adds exactly 1.0; a read with split in {1, 2, 4, 8}
-  // adds multiples of 1/8. All partial sums of such terms are exact in f64
-  // (< 2^50), so the sum in read order is the exact sum: a count of eighths,
-  // here ballot counts for single-symbol reads plus a serial pass over the
-  // (few) multi-symbol reads. Any other split (3, 5, 6, 7 or more than 8
-  // tips) can round, and then every key takes the ordered fold below.
+  // Unweighted votes: a read adds occ/split (tips) to each of its symbols.
+  // They are counted exactly, in units of 1/U of a read, lane-parallel per
+  // key (ballot counts where every voter nominates one symbol, else a wave
+  // sum of each lane's units): U = 8 while every split is 1, 2, 4 or 8 (all
+  // partial sums of the reference's f64 fold are then exact too, < 2^50, so
+  // the count is its value), U = 840 = lcm(1..8) from the first split of 3,
+  // 5, 6 or 7 on. The fold of such terms rounds, but every decision taken on
+  // the votes compares two of them, or one with min_count (the
+  // min(min_count, max) thresholds, the order of the split candidates):
+  // distinct counts are at least 1/840 apart and the fold's error is below
+  // 2^-40, so the counts decide alike unless two compared quantities are
+  // exactly equal. Then, and for splits above 8 or min_af > 0 (the ceil of a
+  // rounded sum), every key takes the ordered fold below.
   bool fold = weighted;
   if (single_sym) {
     // output key j (lane j) gets the read count of its insertion index
@@ -1348,41 +1354,51 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
     const uint32_t c = (uint32_t)__shfl((int)cins, (int)src, 64);
     accv = (uint32_t)lane < m ? (double)c : 0.0;
   } else if (!weighted) {
-    uint32_t c8 = 0;
+    uint32_t U = 8u, cu = 0;  // lane k: key k's count in units of 1/U
     for (uint32_t base = 0; base < n && !fold; base += 64) {
       const uint32_t r = base + lane;
       RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
       if (r < n) x = load(r);
       const bool voter = x.e != kInactive;
+      const bool mul = voter && x.n >= 2;
       const uint32_t s0 = voter && x.n == 1 ? byte_at(x.sym, 0) : 0x100u;
-      for (uint32_t k = 0; k < m; ++k) {
-        const uint32_t cnt = (uint32_t)__popcll((unsigned long long)ballot(s0 == key_at(k)));
-        if ((uint32_t)lane == k) c8 += 8u * cnt;
+      if (!ballot(mul)) {
+        for (uint32_t k = 0; k < m; ++k) {
+          const uint32_t cnt = (uint32_t)__popcll((unsigned long long)ballot(s0 == key_at(k)));
+          if ((uint32_t)lane == k) cu += U * cnt;
+        }
+        continue;
       }
-      uint64_t mm = ballot(voter && x.n >= 2);
-      while (mm) {
-        const int l = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        const uint32_t xn = (uint32_t)__builtin_amdgcn_readlane((int)x.n, l);
-        const uint32_t split = (uint32_t)__builtin_amdgcn_readlane((int)x.split, l);
-        if (split > 8u || (split & (split - 1u))) {
+      if (ballot(mul && x.split > 8u)) {
+        fold = true;
+        break;
+      }
+      if (U == 8u && ballot(mul && (x.split & (x.split - 1u)))) {
+        if (!odd_ok) {
           fold = true;
           break;
         }
-        const uint64_t sym = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x.sym >> 32), l) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x.sym, l);
-        const uint4 occ = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)x.occ.x, l),
-                                     (uint32_t)__builtin_amdgcn_readlane((int)x.occ.y, l),
-                                     (uint32_t)__builtin_amdgcn_readlane((int)x.occ.z, l),
-                                     (uint32_t)__builtin_amdgcn_readlane((int)x.occ.w, l));
-        for (uint32_t jj = 0; jj < xn; ++jj) {
-          const uint32_t sj = byte_at(sym, jj);
-          for (uint32_t k = 0; k < m; ++k)  // the dropped wildcard matches no key
-            if (key_at(k) == sj && (uint32_t)lane == k) c8 += occ_at(occ, jj) * (8u / split);
-        }
+        U = 840u;
+        cu *= 105u;
+      }
+      const uint32_t per = mul ? U / x.split : 0u;
+      for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t key = key_at(k);
+        uint32_t u = s0 == key ? U : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j)
+          if (mul && j < x.n && byte_at(x.sym, j) == key) u = occ_at(x.occ, j) * per;
+        const uint32_t t = wave_sum_u32(u);  // (the whole wave runs the votes)
+        if ((uint32_t)lane == k) cu += t;
       }
     }
-    if (!fold) accv = (double)c8 * 0.125;
+    if (!fold && U != 8u) {  // exact ties (two keys, or a key and min_count): the f64 fold decides
+      for (uint32_t k = 0; k < m && !fold; ++k) {
+        const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)cu, (int)k);
+        fold = __popcll((unsigned long long)ballot((uint32_t)lane < m && cu == ck)) > 1 || (uint64_t)ck == 840ull * mc;
+      }
+    }
+    if (!fold) accv = (uint32_t)lane < m ? (double)cu / (double)U : 0.0;
   }
   if (fold) {
     // contributions computed lane-parallel (one read per lane), then folded
@@ -1435,14 +1451,14 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
 
 
 WC_PHASE_FN bool wave_votes(Lo<Ctl>& ctl, uint32_t side, const Sh<RInfo>* ri, const Sh<RInfo>* r0, const Sh<RInfo>* r1,
-                                  uint32_t n, bool weighted, bool is_dual, bool multi, int wc) {
+                                  uint32_t n, bool weighted, bool is_dual, bool multi, int wc, uint64_t mc, bool odd_ok) {
   const int lane = lane_id();
   const bool side1 = side == 0;
   uint32_t m = 0, key = 0;
   double val = 0.0;
   const bool ok = wave_votes_core([&](uint32_t r) { return rinfo_load(&ri[r]); },
                                   [&](uint32_t r) { return vote_weight(r0, r1, r, is_dual, side1); }, n, weighted,
-                                  multi, wc, m, key, val,
+                                  multi, wc, mc, odd_ok, m, key, val,
 #ifdef WC_PHASE_PROF
                                   ctl.ph,
 #else
@@ -1887,8 +1903,8 @@ WC_SINGLE_FN WaveCounters single_finalize(Eng& E, Lo<Ctl>& ctl, uint32_t top, ui
   finalize_side<true>(E, ctl, top, 0, len, E.L.fe, cnt);
   return cnt;
 }
-WC_SINGLE_FN bool single_votes(Lo<Ctl>& ctl, Sh<RInfo>* ri, uint32_t n, bool multi, int wc) {
-  return wave_votes(ctl, 0, ri, ri, ri, n, false, false, multi, wc);
+WC_SINGLE_FN bool single_votes(Lo<Ctl>& ctl, Sh<RInfo>* ri, uint32_t n, bool multi, int wc, uint64_t mc) {
+  return wave_votes(ctl, 0, ri, ri, ri, n, false, false, multi, wc, mc, true);
 }
 WC_SINGLE_FN void single_store(Eng& E, Lo<Ctl>& ctl, Gm<uint8_t>* outp, uint32_t top, uint32_t len) {
   store_record(E, ctl, outp, top, 1, len, 0, false);
@@ -2038,7 +2054,7 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
 
       // ---- votes + child selection (consensus.rs:283-321) ----
       if (wave_id() == 0) {
-        const bool ok = single_votes(ctl, E.L.rinfo, E.n, ctl.multi[0] != 0, cfg.wildcard);
+        const bool ok = single_votes(ctl, E.L.rinfo, E.n, ctl.multi[0] != 0, cfg.wildcard, cfg.min_count);
         if (lane == 0) {
           if (!ok) {
             ctl.status = limit_status(LIM_VOTES);
@@ -2387,7 +2403,7 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
       // other in a one-wave workgroup) ----
       for (uint32_t side = wave_id(); side < (tdual ? 2u : 1u); side += (uint32_t)kEW) {
         const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, E.n, weighted, tdual,
-                                   ctl.multi[side] != 0, cfg.wildcard);
+                                   ctl.multi[side] != 0, cfg.wildcard, cfg.min_count, cfg.min_af == 0.0);
         if (!ok && lane == 0) atomicOr(&ctl.ovf, (uint32_t)LIM_VOTES);
       }
       __syncthreads();

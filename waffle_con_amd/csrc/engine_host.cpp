@@ -176,12 +176,11 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   // instead of 4. WC_CU=0 disables it, WC_CU=1 forces it (test hook)
   const char* wenv = getenv("WC_CU");
   const int wmode = wenv ? atoi(wenv) : 2;
-  // The dual engine's 1024-thread build (engine_cu_dual.hip, no chains) runs
-  // only when forced: it measured slower on one deep locus (cfg4 24.6 vs
-  // 22.8 s), its per-pop serial sections and 110 spilled VGPRs
-  // (77 at 4 waves) outweigh the wider per-read phases.
+  // (The dual engine has no whole-CU build since round 5: measured slower on
+  // one deep locus, cfg4 24.6 vs 22.8 s, and at 16 waves of 128 VGPRs with
+  // 110 spilled it diverged under unrelated changes of shared code)
   const bool cu_fit = !gstate && wmode != 0 && (wmode == 1 || ids.size() <= (uint64_t)ctx->n_cu);
-  c.cu = cu_ok && cu_fit && (sides == 1 ? chain > 0 : chain == 0 && wmode == 1);
+  c.cu = cu_ok && cu_fit && sides == 1 && chain > 0;
   if (c.cu) c.narrow = c.lowlat = false;
   // The dual engine on one wave per problem (engine_wave.hip): dual searches
   // without offsets of at most 128 reads, whose popped node stays in LDS with
@@ -192,11 +191,11 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   c.wave = sides == 2 && chain == 0 && !gstate && !any_act && nmax <= 128 && !(wvenv && atoi(wvenv) == 0) &&
            lds_bytes(sides, pcap, nmax, 0, 1) <= kLdsMax;
   if (c.wave) c.narrow = c.lowlat = c.cu = false;
-  c.waves = c.cu ? (uint32_t)std::max(sides == 1 ? wcu::engine_waves() : wcv::engine_waves(), kWaves) : (uint32_t)kWaves;
+  c.waves = c.cu ? (uint32_t)std::max(wcu::engine_waves(), kWaves) : (uint32_t)kWaves;
   c.dual_hot = false;
   auto occupancy = [&](size_t l) {
     if (c.wave) return wcw::wave_blocks_per_cu(nmax, l);
-    if (c.cu) return sides == 1 ? wcu::engine_blocks_per_cu(sides, l) : wcv::engine_blocks_per_cu(sides, l, c.dual_hot);
+    if (c.cu) return wcu::engine_blocks_per_cu(sides, l);
     if (sides == 2 && chain > 0 && !gstate) return wcd::engine_blocks_per_cu(sides, l);
     return c.narrow ? wcn::engine_blocks_per_cu(sides, l, c.dual_hot)
                     : (c.lowlat ? wcl::engine_blocks_per_cu(sides, l, c.dual_hot)
@@ -337,6 +336,7 @@ void fault_sentinels(EngineArgs& a, const Caps& caps) {
 }  // namespace
 
 // engine builds (wc_engine_name): bit = 2 * build + sides - 1
+// ("cu.dual": the whole-CU dual build, removed in round 5; the bit stays unused)
 const char* const kEngineNames[] = {"lds.single",    "lds.dual",    "narrow.single", "narrow.dual",
                                     "lowlat.single", "lowlat.dual", "cu.single",     "cu.dual",
                                     "chain.single",  "chain.dual",  "wave.single",   "wave.dual",
@@ -376,8 +376,7 @@ int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
   } else if (caps.wave) {
     wcw::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else if (caps.cu) {
-    if (caps.sides == 1) wcu::launch_single_engine(a, L.grid, caps.lds, L.stream);
-    else wcv::launch_dual_engine(a, L.grid, caps.lds, L.stream);
+    wcu::launch_single_engine(a, L.grid, caps.lds, L.stream);  // (single engine only)
   } else if (caps.narrow) {
     if (caps.sides == 1) wcn::launch_single_engine(a, L.grid, caps.lds, L.stream);
     else wcn::launch_dual_engine(a, L.grid, caps.lds, L.stream);

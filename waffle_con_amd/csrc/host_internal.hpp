@@ -44,11 +44,6 @@ void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hi
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 int engine_waves();
 }  // namespace wcu
-namespace wcv {  // engine_cu_dual.hip: the 1024-thread dual engine (launches of <= one problem per CU)
-void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
-int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
-int engine_waves();
-}  // namespace wcv
 namespace wcw {  // engine_wave.hip: the dual engine on one wave per problem (no offsets, <= 128 reads)
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 int wave_blocks_per_cu(uint32_t nmax, size_t lds);

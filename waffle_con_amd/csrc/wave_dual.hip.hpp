@@ -328,7 +328,7 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
     // builds a single in-place child itself
     for (uint32_t side = 0; side < (tdual ? 2u : 1u); ++side) {
       const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, n, weighted, tdual, ctl.multi[side] != 0,
-                                 cfg.wildcard);
+                                 cfg.wildcard, cfg.min_count, cfg.min_af == 0.0);
       if (!ok && lane == 0) atomicOr(&ctl.ovf, (uint32_t)LIM_VOTES);
     }
     __syncthreads();
@@ -432,7 +432,7 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
   // votes on both sides, the selection, the children (dual_main)
   for (uint32_t side = 0; side < (tdual ? 2u : 1u); ++side) {
     const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, n, weighted, tdual, ctl.multi[side] != 0,
-                               cfg.wildcard);
+                               cfg.wildcard, cfg.min_count, cfg.min_af == 0.0);
     if (!ok && lane == 0) atomicOr(&ctl.ovf, (uint32_t)LIM_VOTES);
   }
   __syncthreads();
