@@ -1278,24 +1278,28 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
     bool voter = x.e != kInactive;
     if (voter && weighted) voter = weight(r) > 0.0;
     const uint32_t xn = voter ? x.n : 0u;
+    // per lane, the high bit of byte j stays set while its symbol j (j < xn)
+    // is not a key yet (a read's symbols are distinct); the keys of earlier
+    // chunks are cleared first, eight bytes at a time
+    constexpr uint64_t kHi = 0x8080808080808080ull, kOnes = 0x0101010101010101ull;
+    uint64_t rem = xn >= 8u ? kHi : kHi & ((1ull << (8u * xn)) - 1ull);
+    for (uint32_t k = 0; k < nk; ++k) rem &= nz_bytes(x.sym ^ (kOnes * ins_at(k)));
     for (;;) {
-      uint32_t cand = 0xFFFF;
-      for (uint32_t k = 0; k < xn; ++k) {
-        const uint32_t s = byte_at(x.sym, k);
-        if (!known.has(s)) {
-          cand = s;
-          break;
-        }
-      }
-      const uint64_t m = ballot(cand != 0xFFFF);
+      // the first read (lane) with a symbol not yet a key, and its first one
+      const uint64_t m = ballot(rem != 0);
       if (!m) break;
       const int first = __ffsll((unsigned long long)m) - 1;
-      const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)cand, first);
+      const uint64_t rf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rem >> 32), first) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rem, first);
+      const uint64_t sf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x.sym >> 32), first) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x.sym, first);
+      const uint32_t s = byte_at(sf, (uint32_t)__builtin_ctzll(rf) >> 3);
       if (nk == (uint32_t)kKout) return false;
       if (nk < 8) ins_lo |= (uint64_t)s << (8 * nk);
       else ins_hi |= (uint64_t)s << (8 * (nk - 8));
       nk++;
       known.add(s);
+      rem &= nz_bytes(x.sym ^ (kOnes * s));
     }
   }
   VOTE_T(28);
