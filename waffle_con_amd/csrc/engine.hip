@@ -1386,14 +1386,21 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
         cu *= 105u;
       }
       const uint32_t per = mul ? U / x.split : 0u;
-      for (uint32_t k = 0; k < m; ++k) {
-        const uint32_t key = key_at(k);
-        uint32_t u = s0 == key ? U : 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j)
-          if (mul && j < x.n && byte_at(x.sym, j) == key) u = occ_at(x.occ, j) * per;
+      // this lane's symbol slots j < x.n of a multi-symbol read (byte high bits)
+      constexpr uint64_t kHi = 0x8080808080808080ull, kOnes = 0x0101010101010101ull;
+      const uint64_t slots = !mul ? 0ull : (x.n >= 8u ? kHi : kHi & ((1ull << (8u * x.n)) - 1ull));
+      // units of key k on this lane: U for its one symbol, occ * U / split
+      // for the slot holding it (a read's symbols are distinct)
+      auto units = [&](uint32_t key) -> uint32_t {
+        const uint64_t eq = slots & ~nz_bytes(x.sym ^ (kOnes * key));
+        return s0 == key ? U : (eq ? occ_at(x.occ, (uint32_t)__builtin_ctzll(eq) >> 3) * per : 0u);
+      };
+      // two keys per wave sum: a key's units over 64 lanes stay below 2^16
+      for (uint32_t k = 0; k < m; k += 2) {
+        const uint32_t u = units(key_at(k)) | (k + 1 < m ? units(key_at(k + 1)) << 16 : 0u);
         const uint32_t t = wave_sum_u32(u);  // (the whole wave runs the votes)
-        if ((uint32_t)lane == k) cu += t;
+        if ((uint32_t)lane == k) cu += t & 0xFFFFu;
+        if ((uint32_t)lane == k + 1) cu += t >> 16;
       }
     }
     if (!fold && U != 8u) {  // exact ties (two keys, or a key and min_count): the f64 fold decides
