@@ -15,7 +15,10 @@
 // sub-problem alone 21.4 -> 17.2 us/pop, the 10,000-locus cfg5 batch 323 ->
 // 361 loci/s, the 2,000-locus one 19.0 -> 15.8 s, despite half the
 // workgroups per CU. The one-read-per-lane kernel keeps 2 (5949's full-read
-// level alone: 12.0 us/pop at either). WC_WAVE_WPE=<k> builds both at k.
+// level alone: 12.0 us/pop at either). Re-measured at the end of round 5
+// (133 VGPRs spilled at 2, none at 1): 80-read sub-problem 12.0 (1) vs 15.0
+// (2) us/pop, the 10,000-locus batch 19.8 vs 24.1 s (gpurun_out/r05wpe).
+// WC_WAVE_WPE=<k> builds both at k.
 #ifdef WC_WAVE_WPE
 #define WC_DUAL_WAVES_PER_EU WC_WAVE_WPE
 #define WC_WAVE2_WPE WC_WAVE_WPE
