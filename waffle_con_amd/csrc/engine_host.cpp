@@ -824,6 +824,13 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
     return kx != ky ? kx < ky : x > y;
   };
   std::priority_queue<uint32_t, std::vector<uint32_t>, decltype(later)> waiting(later);
+  // an epoch planned for more reads than the one-wave dual engine takes ends
+  // as soon as no live sub-problem has more (the rest wait for the next
+  // epoch, planned for them): cfg4's 200-read root, then 50-read groups
+  constexpr size_t kWaveReads = 128;
+  const bool can_shrink = !caps.wave && caps.nmax > kWaveReads && !caps.gstate;
+  uint32_t big_live = 0;  // outstanding or waiting sub-problems of more than kWaveReads reads
+  bool shrink = false;
   for (;;) {
     bool progress = false;
     if (log && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_log).count() > 10.0) {
@@ -839,14 +846,17 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
     // largest (reads x bases) first
     const uint32_t backlog = L.grid + L.grid / 4;
     while (!ready.empty()) {  // new arrivals into the host-side order
+      big_live += items[ready.front()].gid.size() > kWaveReads;
       waiting.push(ready.front());
       ready.pop_front();
     }
+    if (can_shrink && big_live == 0 && !waiting.empty()) shrink = true;
     bool published = false;
-    while (!waiting.empty() && outstanding < backlog) {
+    while (!shrink && !waiting.empty() && outstanding < backlog) {
       const uint32_t id = waiting.top();
       if (!live(id)) {
         waiting.pop();
+        big_live -= items[id].gid.size() > kWaveReads;
         on_done(id, ~0u);  // dropped: its problem already failed
         continue;
       }
@@ -892,13 +902,14 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
       __atomic_store_n(&done[slot], 0u, __ATOMIC_RELEASE);  // the slot may be reused
       seq_done[seq] = 1;
       outstanding--;
+      big_live -= items[id].gid.size() > kWaveReads;
       finished++;
       while (oldest < seq_item.size() && seq_done[oldest]) oldest++;
       on_done(id, st);
       progress = true;
       t_fin = std::chrono::steady_clock::now();
     }
-    if (outstanding == 0 && ready.empty() && waiting.empty()) break;
+    if (outstanding == 0 && ready.empty() && (waiting.empty() || shrink)) break;
     {
       const auto now = std::chrono::steady_clock::now();
       const double quiet = std::chrono::duration<double>(now - t_fin).count();
@@ -1236,7 +1247,11 @@ int priority_stream(wc_ctx* ctx, const wc_config& cfg, uint32_t n, const wc_chai
     // capacities for anything this epoch may see: every read of every problem,
     // plus the growth earned by the items carried over from the last epoch
     std::vector<SubProb> env(1);
-    env[0].gid.assign(max_chains, 0);
+    // (a sub-problem's successors never have more reads than it: the ready
+    // ones bound the epoch)
+    size_t max_ready = 1;
+    for (uint32_t id : ready) max_ready = std::max(max_ready, subs[id].gid.size());
+    env[0].gid.assign(std::min<size_t>(max_chains, max_ready), 0);
     env[0].max_len = max_len;
     env[0].max_act = any_offsets ? 1 : 0;
     for (uint32_t id : ready) {
