@@ -408,6 +408,7 @@ __device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
 }
 // (uniform) wave sum of u64 values: DPP row sums, four scalar reads
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  WC_FULL_EXEC();
   v += dpp_u64<0xb1>(v);
   v += dpp_u64<0x4e>(v);
   v += dpp_u64<0x141>(v);
@@ -436,6 +437,7 @@ __device__ __forceinline__ void agg_or(Lo<uint32_t>* p, bool cond, uint32_t bits
 }
 // a slot of the list counted by `counter` for every lane with `take`
 __device__ __forceinline__ uint32_t agg_append(Lo<uint32_t>* counter, bool take) {
+  WC_FULL_EXEC();
   const uint64_t m = ballot(take);
   if (!m) return 0;
   uint32_t base = 0;
@@ -1217,6 +1219,7 @@ template <class Load, class Weight>
 __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, bool weighted, bool multi, int wc,
                                        uint64_t mc, bool odd_ok, uint32_t& m_out, uint32_t& key_out, double& val_out,
                                        Lo<uint64_t>* ph = nullptr, Lo<FxCache>* fxc = nullptr) {
+  WC_FULL_EXEC();  // (ballots over every read lane, the DPP sums below)
   const int lane = lane_id();
 #ifdef WC_PHASE_PROF
   uint64_t vt = __builtin_amdgcn_s_memtime();
@@ -1411,10 +1414,10 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
     }
     if (!fold) accv = (uint32_t)lane < m ? (double)cu / (double)U : 0.0;
   }
-  if (fold) {
-    // contributions computed lane-parallel (one read per lane), then folded
-    // strictly in read order (the reference's f64 summation order); a read
-    // without the key adds nothing (x + 0.0 == x, so skipping it is exact)
+  // contributions computed lane-parallel (one read per lane), then folded
+  // strictly in read order (the reference's f64 summation order); a read
+  // without the key adds nothing (x + 0.0 == x, so skipping it is exact)
+  auto fold_into = [&](double& acc_io) {
     for (uint32_t base = 0; base < n; base += 64) {
       const uint32_t r = base + lane;
       RInfoReg x = {0, 0, kInactive, 0, make_uint4(0, 0, 0, 0)};
@@ -1437,7 +1440,7 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
         // (add_ones); every other contribution is added one at a time
         const uint64_t ones = ballot(occ != 0 && c == 1.0);
         uint64_t frac = ballot(occ != 0 && c != 1.0);
-        double acc = readlane_f64(accv, (int)k);
+        double acc = readlane_f64(acc_io, (int)k);
         uint64_t done = 0;
         while (frac) {
           const int l = __builtin_ctzll(frac);
@@ -1448,10 +1451,26 @@ __device__ inline bool wave_votes_core(Load load, Weight weight, uint32_t n, boo
           acc += readlane_f64(c, l);
         }
         acc = add_ones(acc, (uint32_t)__popcll((unsigned long long)(ones & ~done)));
-        if ((uint32_t)lane == k) accv = acc;
+        if ((uint32_t)lane == k) acc_io = acc;
       }
     }
+  };
+  if (fold) {
+    fold_into(accv);
   }
+#ifdef WC_VOTE_XCHECK
+  // (diagnostic build) the exact counts against the reference's ordered fold:
+  // distinct counts are >= 1/840 apart, the fold's rounding error < 2^-40
+  else if (!weighted) {
+    double accf = 0.0;
+    fold_into(accf);
+    const bool bad = (uint32_t)lane < m && fabs(accf - accv) > 1e-9;
+    const uint64_t bm = ballot(bad);
+    if (bm && lane == __builtin_ctzll(bm))
+      printf("[wc-xcheck] votes: wg %u wave %u n %u m %u key %u exact %.17g fold %.17g single %d\n", blockIdx.x,
+             threadIdx.x >> 6, n, m, key_at((uint32_t)lane), accv, accf, (int)single_sym);
+  }
+#endif
   VOTE_T(30);
 #undef VOTE_T
   m_out = m;

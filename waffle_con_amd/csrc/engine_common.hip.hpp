@@ -77,8 +77,28 @@ __device__ __forceinline__ uint32_t wc_ix(uint64_t i, uint64_t n, uint32_t line)
   return i < n ? (uint32_t)i : wc_chk_fail(line, i, n);
 }
 #define WC_IX(i, n) wc_ix((i), (n), __LINE__)
+// Wave-wide reductions and ballot-driven code (the DPP row sums read lanes 0,
+// 16, 32, 48 and every lane's neighbours) are only correct with all 64 lanes
+// in exec; checked builds report every call site reached with a partial mask.
+__device__ __noinline__ void wc_chk_exec_fail(uint32_t line, uint64_t exec) {
+  if (atomicAdd(&wc_chk_hits, 1u) < 64u)
+    printf("[wc-check] line %u: partial exec 0x%016llx (workgroup %u wave %u)\n", line, (unsigned long long)exec,
+           blockIdx.x, threadIdx.x >> 6);
+}
+#define WC_FULL_EXEC()                                                     \
+  do {                                                                     \
+    const uint64_t _ex = __builtin_amdgcn_read_exec();                     \
+    if (_ex != ~0ull && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(_ex)) \
+      wc_chk_exec_fail(__LINE__, _ex);                                     \
+  } while (0)
+// a per-wave LDS index (wave w of the build's kEW) in range
+#define WC_WAVE_IX(w, n) wc_ix((w), (n), __LINE__)
 #else
 #define WC_IX(i, n) (i)
+#define WC_FULL_EXEC() \
+  do {                 \
+  } while (0)
+#define WC_WAVE_IX(w, n) (w)
 #endif
 
 // Wave64 reductions through DPP lane moves (VALU, no LDS round trips): quad
@@ -104,6 +124,7 @@ __device__ __forceinline__ uint32_t row_sum_u32(uint32_t v) {
   return v;
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  WC_FULL_EXEC();
   v = row_max_u32(v);
   return max(max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
              max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
@@ -113,6 +134,7 @@ __device__ __forceinline__ uint32_t row_ror1(uint32_t v) { return dpp_u32<0x121>
 __device__ __forceinline__ uint32_t row_ror2(uint32_t v) { return dpp_u32<0x122>(v); }
 __device__ __forceinline__ uint32_t wave_ror1(uint32_t v) { return dpp_u32<0x13c>(v); }
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  WC_FULL_EXEC();
   v = row_sum_u32(v);
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
          (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
