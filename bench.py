@@ -504,6 +504,9 @@ class Cfg3(Cfg2):
                 "gpu_matches_cpu_on_sample": ok}
 
 
+CFG5_FAMILY = "PriorityConsensusDWFA cfg5: fixed batch of "
+
+
 class Cfg5:
     """PriorityConsensusDWFA over a fixed batch of cfg5 loci, strong-scaled:
     the heavy prefix of the cost-sorted order (75% of the estimated cost) is
@@ -894,15 +897,21 @@ WORKLOADS = {"cfg2": Cfg2, "cfg2-api": Cfg2Api, "cfg2-latency": Cfg2Latency, "cf
 # ---------------------------------------------------------------------------
 # roofline / profile records committed under profiles/
 # ---------------------------------------------------------------------------
-def profile_record(kind, workload_cfg, kernel=None):
+def profile_record(kind, workload_cfg, kernel, family=None):
     """Latest committed PMC summary (profiles/r*_<kind>.json) recorded on this
-    workload (and, when given, on this kernel: a record of another build's
-    kernel does not describe this one)."""
+    kernel (exact name: a record of another build's kernel, or one that does
+    not name its kernel, does not describe this one) and on this workload, or,
+    with `family`, on any workload whose description starts with it (the same
+    generator at another batch size: only the record's size-independent
+    ratios apply then)."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s.json" % kind)), reverse=True):
         with open(path) as f:
             rec = json.load(f)
-        if rec.get("workload") == workload_cfg and (kernel is None or rec.get("kernel") in (None, kernel)):
+        wl = rec.get("workload") or ""
+        if rec.get("kernel") != kernel:
+            continue
+        if wl == workload_cfg or (family is not None and wl.startswith(family)):
             rec["_file"] = os.path.relpath(path, ROOT)
             return rec
     return None
@@ -1027,14 +1036,25 @@ def main():
                "note": "rank 0's launches; kernel_ms sums the stream epochs' HIP-event times"}
         if rl5["achieved"] is not None:
             rl5["frac"] = rl5["achieved"] / HBM_PEAK_GBS
-        pmc5 = profile_record("pmc_traffic", C5.config()["workload"], Cfg5.kernel) if world == 1 else None
+        # the PMC passes cannot run the whole 10,000-locus batch within the
+        # profiler's limits: the record is of a smaller batch of the same
+        # generator (its workload names the count), so only its intensive
+        # figures (HBM rate, traffic over the compulsory model) are carried
+        pmc5 = profile_record("pmc_traffic", C5.config()["workload"], Cfg5.kernel, family=CFG5_FAMILY)
         if pmc5:
+            rl5["pmc_workload"] = pmc5["workload"]
             rl5["pmc_traffic_bytes_per_launch"] = pmc5["traffic_bytes_per_launch"]
             rl5["pmc_kernel_ms_per_launch"] = pmc5.get("kernel_ms_per_launch_bench_events")
             if rl5["pmc_kernel_ms_per_launch"]:
-                rl5["pmc_frac"] = (pmc5["traffic_bytes_per_launch"] / (rl5["pmc_kernel_ms_per_launch"] / 1e3) / 1e9
-                                   / HBM_PEAK_GBS)
+                rl5["pmc_achieved"] = pmc5["traffic_bytes_per_launch"] / (rl5["pmc_kernel_ms_per_launch"] / 1e3) / 1e9
+                rl5["pmc_frac"] = rl5["pmc_achieved"] / HBM_PEAK_GBS
+            if pmc5.get("model_bytes_per_launch"):
+                rl5["traffic_over_model"] = pmc5["traffic_bytes_per_launch"] / pmc5["model_bytes_per_launch"]
             rl5["pmc_source"] = pmc5["_file"]
+        iv5 = profile_record("issue_view", C5.config()["workload"], Cfg5.kernel, family=CFG5_FAMILY)
+        if iv5:
+            rl5["issue_view"] = {k: v for k, v in iv5.items() if not k.startswith("_")}
+            rl5["issue_view"]["source"] = iv5["_file"]
         cfg5_leg["roofline"] = rl5
         if rank == 0 and tail["heaviest_latency_under_load_s"] is not None:
             cfg5_leg["tail"]["heaviest_latency_alone_s"] = C5.heaviest_alone(tail["heaviest_locus"])
@@ -1074,8 +1094,11 @@ def main():
     cfgd = W.config()
     avg_kernel_s = kernel_ms / a.steps / 1e3
     ref_bytes = (8.0 * wout + 2.0 * cmp) / a.steps  # SURVEY §8(d) B_upd summed, per step
-    pmc = profile_record("pmc_traffic", cfgd["workload"], W.kernel)
-    traffic = pmc.get("traffic_bytes_per_launch") if pmc else None
+    fam = CFG5_FAMILY if W.name in ("cfg5",) else None
+    pmc = profile_record("pmc_traffic", cfgd["workload"], W.kernel, family=fam)
+    pmc_same = pmc is not None and pmc.get("workload") == cfgd["workload"]
+    # (per-launch bytes only from a record of this very workload)
+    traffic = pmc.get("traffic_bytes_per_launch") if pmc_same else None
     launches_per_step = launches / a.steps
     per_launch_s = avg_kernel_s / max(launches_per_step, 1)
     # The roofline model: the HBM bytes this search cannot avoid
@@ -1108,7 +1131,15 @@ def main():
         roofline["pmc_frac"] = roofline["pmc_achieved"] / HBM_PEAK_GBS
         roofline["pmc_source"] = pmc["_file"]
         roofline["traffic_over_model"] = traffic / model_bytes if model_bytes else None
-    issue = profile_record("issue_view", cfgd["workload"], W.kernel)
+    elif pmc and pmc.get("kernel_ms_per_launch_bench_events"):
+        # a smaller batch of the same generator: its own rate and ratio
+        roofline["pmc_workload"] = pmc["workload"]
+        roofline["pmc_achieved"] = pmc["traffic_bytes_per_launch"] / (pmc["kernel_ms_per_launch_bench_events"] / 1e3) / 1e9
+        roofline["pmc_frac"] = roofline["pmc_achieved"] / HBM_PEAK_GBS
+        roofline["pmc_source"] = pmc["_file"]
+        if pmc.get("model_bytes_per_launch"):
+            roofline["traffic_over_model"] = pmc["traffic_bytes_per_launch"] / pmc["model_bytes_per_launch"]
+    issue = profile_record("issue_view", cfgd["workload"], W.kernel, family=fam)
     if issue:
         roofline["issue_view"] = {k: v for k, v in issue.items() if not k.startswith("_") and k != "workload"}
         roofline["issue_view"]["source"] = issue["_file"]

@@ -269,6 +269,12 @@ typedef struct wc_dwfa_job {
   uint64_t cand_counts[16];
   uint32_t n_cand;
   int32_t status;
+  /* op 2 output: the same n_cand symbols in insertion order (first tip in
+   * ascending diagonal index: the order of the reference's entry().or_insert()
+   * calls, dynamic_wfa.rs:244-250). A hashbrown map's layout depends on it when
+   * keys collide (C and G share bucket 3 of 4), so a caller
+   * that rebuilds the map inserts in this order. */
+  uint8_t cand_first[16];
 } wc_dwfa_job;
 int wc_dwfa_batch(wc_ctx* ctx, uint32_t n, wc_dwfa_job* jobs);
 

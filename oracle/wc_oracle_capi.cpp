@@ -245,6 +245,31 @@ int orc_dwfa_candidates(const uint8_t* baseline, uint64_t blen, const uint8_t* o
   return 0;
 }
 
+// The same nomination's keys in insertion order: dynamic_wfa.rs:244-250 calls
+// entry(read[bo]).or_insert(0) tip by tip in ascending diagonal index, so the
+// k-th key is the k-th distinct tip symbol. (Replaying these inserts through
+// FxByteMap gives orc_dwfa_candidates' iteration order.)
+int orc_dwfa_candidate_first(const uint8_t* baseline, uint64_t blen, const uint8_t* other, uint64_t olen,
+                             int32_t wildcard, uint8_t* syms, uint32_t cap, uint32_t* n_out) {
+  Dwfa d;
+  d.wildcard = wildcard;
+  Seq b{baseline, (size_t)blen};
+  for (uint64_t l = 1; l <= olen; ++l) d.update(b, Seq{other, (size_t)l}, nullptr);
+  bool seen[256] = {false};
+  uint32_t k = 0;
+  for (size_t i = 0; i < d.wf.size(); ++i) {
+    const size_t dd = d.wf[i];
+    if (dd + d.offset != (size_t)olen) continue;
+    const size_t bo = dd + d.e - i;
+    if (bo >= (size_t)blen || seen[baseline[bo]]) continue;
+    seen[baseline[bo]] = true;
+    if (k < cap) syms[k] = baseline[bo];
+    k++;
+  }
+  *n_out = k;
+  return 0;
+}
+
 // One DWFALite operation on an explicit state (clone = copy the state on the
 // caller side). op 0 = update(baseline, other), 1 = finalize(baseline, other).
 // State: *e, wf[0..*wf_len] (in/out, capacity wf_cap).

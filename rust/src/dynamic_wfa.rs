@@ -71,6 +71,7 @@ impl DWFALite {
             cand_counts: [0; 16],
             n_cand: 0,
             status: 0,
+            cand_first: [0; 16],
         };
         device::with_ctx(|ctx| {
             let rc = unsafe { ffi::wc_dwfa_batch(ctx, 1, &mut job) };
@@ -128,16 +129,26 @@ impl DWFALite {
     }
 
     /// dynamic_wfa.rs:241-255: the symbols at the wavefront's tips with their
-    /// counts. The device returns them in FxHashMap iteration order; they are
-    /// inserted here in that order (the map's own order does not depend on
-    /// insertion for distinct keys). Infallible in the reference: a device
-    /// failure here panics with the library's message.
+    /// counts. The device returns them in FxHashMap iteration order with their
+    /// counts, and also in insertion order (first tip in ascending diagonal
+    /// index, `cand_first`). The map is rebuilt by inserting in that order, as
+    /// the reference's `entry().or_insert()` calls do: a hashbrown table's
+    /// layout, and so its iteration order, depends on the insertion order when
+    /// keys share a home bucket (C and G in a 4-bucket table, SURVEY Appendix
+    /// B). Infallible in the reference: a device failure here panics with the
+    /// library's message.
     pub fn get_extension_candidates(&self, baseline_seq: &[u8], other_seq: &[u8]) -> HashMap<u8, usize> {
         let (job, _) = self.run(baseline_seq, other_seq, OP_CANDIDATES)
             .unwrap_or_else(|e| panic!("get_extension_candidates on the device failed: {}", e));
+        let n = job.n_cand as usize;
+        let count = |s: u8| -> usize {
+            (0..n).find(|&k| job.cand_syms[k] == s).map(|k| job.cand_counts[k] as usize)
+                .unwrap_or_else(|| panic!("get_extension_candidates: symbol {} missing from the device's map", s))
+        };
         let mut ret: HashMap<u8, usize> = Default::default();
-        for k in 0..job.n_cand as usize {
-            ret.insert(job.cand_syms[k], job.cand_counts[k] as usize);
+        for k in 0..n {
+            let s = job.cand_first[k];
+            ret.insert(s, count(s));
         }
         ret
     }

@@ -149,6 +149,7 @@ pub struct wc_dwfa_job {
     pub cand_counts: [u64; 16],
     pub n_cand: u32,
     pub status: i32,
+    pub cand_first: [u8; 16],
 }
 
 extern "C" {

@@ -29,6 +29,17 @@ service per device (`wc_service_*`: persistent engine launches, one workgroup
 per locus in flight). The device is `WAFFLE_CON_DEVICE` (default 0). Many loci
 at once can also go through [`device::consensus_batch`] and friends (one
 launch over the whole batch).
+
+**Build status.** This crate has not been compiled or type-checked: the build
+image has no `cargo`/`rustc` and no crate registry (`rustc-hash`,
+`priority-queue` and `derive_builder` are crates.io dependencies). What is
+checked, on the CPU, is the text: `tests/test_rust_crate.py` matches every
+`ffi` declaration and `#[repr(C)]` struct against `include/waffle_con.h` and
+the public surface against the reference's. The device paths these modules
+call are parity-tested through the same C ABI from Python (`tests/test_gpu_*`,
+e.g. `test_gpu_dwfa.py` for `DWFALite`'s update / finalize / candidates and
+the insertion order its `get_extension_candidates` replays), but the Rust code
+around those calls is not.
 */
 
 /// Configuration for ConsensusDWFA (cdwfa_config.rs)

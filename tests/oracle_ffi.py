@@ -86,6 +86,9 @@ def lib():
                                           ctypes.c_int32, ctypes.POINTER(ctypes.c_uint8),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32,
                                           ctypes.POINTER(ctypes.c_uint32)]
+        L.orc_dwfa_candidate_first.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
+                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint32,
+                                               ctypes.POINTER(ctypes.c_uint32)]
         L.orc_dwfa_step.restype = ctypes.c_int
         L.orc_dwfa_step.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                                     ctypes.c_int32, ctypes.c_uint8, ctypes.c_uint64, ctypes.c_int,
@@ -228,6 +231,16 @@ def dwfa_candidates(baseline, other, wildcard=None):
     L.orc_dwfa_candidates(bytes(baseline), len(baseline), bytes(other), len(other),
                           -1 if wildcard is None else wildcard, syms, cnts, 256, ctypes.byref(n))
     return [(syms[i], cnts[i]) for i in range(n.value)]
+
+
+def dwfa_candidate_first(baseline, other, wildcard=None):
+    """The keys of dwfa_candidates in insertion (first-appearance) order."""
+    L = lib()
+    syms = (ctypes.c_uint8 * 256)()
+    n = ctypes.c_uint32()
+    L.orc_dwfa_candidate_first(bytes(baseline), len(baseline), bytes(other), len(other),
+                               -1 if wildcard is None else wildcard, syms, 256, ctypes.byref(n))
+    return list(syms[:n.value])
 
 
 def wfa_ed_config(v1, v2, require_both_end, wildcard):

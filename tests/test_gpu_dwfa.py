@@ -69,3 +69,24 @@ def test_dwfa_random_vs_oracle():
         assert eds == ref["eds"] and d.wavefront() == ref["wavefront"]
         cand = d.get_extension_candidates(base, other)
         assert list(cand.items()) == orc.dwfa_candidates(base, other) if not early else True
+
+
+def test_dwfa_candidate_insertion_order_vs_oracle():
+    """wc_dwfa_job.cand_first (the insertion order the Rust crate replays into
+    its FxHashMap) equals the reference's first-appearance order, and replaying
+    it through the hashbrown model gives the device's iteration order;
+    includes the G-then-C collision case."""
+    rng = random.Random(5)
+    cases = [(b"CG", b"G"), (b"ACGT", b"AG")]
+    for _ in range(60):
+        cases.append((bytes(rng.choice(b"ACGT") for _ in range(rng.randint(2, 12))),
+                      bytes(rng.choice(b"ACGT") for _ in range(rng.randint(1, 9)))))
+    for base, other in cases:
+        d = w.DWFALite.default()
+        for l in range(1, len(other) + 1):
+            d.update(base, other[:l])
+        cand = d.get_extension_candidates(base, other)
+        first = d.candidate_insertion_order(base, other)
+        assert list(cand.items()) == orc.dwfa_candidates(base, other)
+        assert first == orc.dwfa_candidate_first(base, other)
+        assert orc.fxmap_order(bytes(first)) == list(cand.keys())

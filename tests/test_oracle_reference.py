@@ -109,3 +109,36 @@ def test_fxmap_orders_appendix_b():
     # <= 3 keys: insertion order decides collisions (C and G share bucket 3 of 4)
     assert orc.fxmap_order(b"CG") == list(b"GC")  # C at 3, G wraps to 0
     assert orc.fxmap_order(b"GC") == list(b"CG")
+
+
+def _insertion_cases():
+    """(baseline, other) pairs: the reference's DWFA test inputs, a G-then-C
+    tip collision, and seeded random pairs."""
+    import random
+    cases = [(rc.b(c["base"]), rc.b(c["other"])) for c in rc.DWFA_CASES.values()]
+    cases.append((b"CG", b"G"))  # tips nominate G (diagonal 0) then C (diagonal 2): C and G share bucket 3 of 4
+    rng = random.Random(5)
+    for _ in range(400):
+        cases.append((bytes(rng.choice(b"ACGT") for _ in range(rng.randint(2, 12))),
+                      bytes(rng.choice(b"ACGT") for _ in range(rng.randint(1, 9)))))
+    return cases
+
+
+def test_candidate_insertion_order_rebuilds_the_map():
+    """dynamic_wfa.rs:241-255 inserts tip symbols in ascending diagonal order.
+    Replaying that insertion order through the hashbrown model (Appendix B)
+    gives the map's iteration order on every case; replaying the iteration
+    order instead (what a shim that only sees the iteration order would do)
+    does not, once keys collide (the Rust crate's get_extension_candidates
+    inserts in wc_dwfa_job.cand_first order for this reason)."""
+    wrong = 0
+    for base, other in _insertion_cases():
+        it = [s for s, _ in orc.dwfa_candidates(base, other)]
+        ins = orc.dwfa_candidate_first(base, other)
+        assert sorted(ins) == sorted(it)
+        assert orc.fxmap_order(bytes(ins)) == it, (base, other)
+        wrong += orc.fxmap_order(bytes(it)) != it
+    assert orc.dwfa_candidate_first(b"CG", b"G") == list(b"GC")
+    assert [s for s, _ in orc.dwfa_candidates(b"CG", b"G")] == list(b"CG")
+    assert orc.fxmap_order(b"CG") == list(b"GC")  # re-inserting the iteration order flips it
+    assert wrong > 0

@@ -79,6 +79,7 @@ def main():
         "traffic_bytes_per_launch_if_wide": 2.0 * fetch_b + write_b,
         "traffic_formula": "FETCH_SIZE + WRITE_SIZE (KiB -> bytes); the gfx950 x2 FETCH correction is calibrated for "
                            "16-B/lane coalesced reads only, so it gives the upper reading (_if_wide)",
+        "model_bytes_per_launch": kt["roofline"].get("model_bytes_per_launch"),
         "reference_equiv_bytes_per_step": kt["roofline"]["reference_equiv_bytes_per_step"],
         "kernel_ms_per_launch_bench_events": kt["roofline"]["kernel_ms_per_launch"],
         "kernel_ms_per_launch_pmc_pass": fb["roofline"]["kernel_ms_per_launch"],
@@ -92,7 +93,7 @@ def main():
         for k, v in counters(os.path.join(src, p, "run_counter_collection.csv")).items():
             sq[k] = mean(v)
     if sq:
-        iv = {"tag": tag, "workload": workload, "counters_per_launch": sq}
+        iv = {"tag": tag, "kernel": kt["roofline"]["kernel"], "workload": workload, "counters_per_launch": sq}
         wc = sq.get("SQ_WAVE_CYCLES")
         if wc:
             iv["wave_cycle_split"] = {k: sq[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",

@@ -114,7 +114,7 @@ class WcDwfaJob(ctypes.Structure):
                 ("e", ctypes.c_uint64), ("wavefront", ctypes.POINTER(ctypes.c_uint64)),
                 ("wf_len", ctypes.c_uint64), ("wf_cap", ctypes.c_uint64),
                 ("cand_syms", ctypes.c_uint8 * 16), ("cand_counts", ctypes.c_uint64 * 16),
-                ("n_cand", ctypes.c_uint32), ("status", ctypes.c_int32)]
+                ("n_cand", ctypes.c_uint32), ("status", ctypes.c_int32), ("cand_first", ctypes.c_uint8 * 16)]
 
 
 # every symbol include/waffle_con.h declares (checked by tests/test_cabi.py)

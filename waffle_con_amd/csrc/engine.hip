@@ -2664,13 +2664,15 @@ __global__ void __launch_bounds__(64) dwfa_jobs_kernel(DwfaDevJob* jobs) {
   } else {
     __shared__ RInfo ri_lds;
     Lo<RInfo>& ri = *(Lo<RInfo>*)&ri_lds;
-    if (!wave_analyze_read(wf, e, j.offset, base, j.blen, j.olen, &ri)) status = WC_E_LIMIT_CODE;
+    uint64_t ins = 0;
+    if (!wave_analyze_read(wf, e, j.offset, base, j.blen, j.olen, &ri, &ins)) status = WC_E_LIMIT_CODE;
     __builtin_amdgcn_wave_barrier();
     if (lane == 0 && status == 0) {
       j.n_cand = ri.n;
       for (uint32_t k = 0; k < ri.n; ++k) {
         j.cand_syms[k] = ri.sym[k];
         j.cand_counts[k] = ri.occ[k];
+        j.cand_first[k] = (uint8_t)byte_at(ins, k);
       }
     }
   }

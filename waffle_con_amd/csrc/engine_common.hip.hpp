@@ -572,8 +572,10 @@ __device__ inline bool wave_finalize_read(const Gm<uint32_t>* wf, uint32_t e, ui
 // first-appearance order (ascending diagonal), then permuted into FxHashMap
 // iteration order. Keys/counts are wave-uniform packed registers. Returns
 // false when more than kKmax distinct symbols sit at the tips.
+// (ins: when given, lane 0 also stores the symbols in insertion order, the
+// order of the reference's entry().or_insert() calls, byte k = k-th key)
 __device__ inline bool wave_analyze_read(const Gm<uint32_t>* wf, uint32_t e, uint32_t off, const Gm<uint8_t>* rd,
-                                         uint32_t blen, uint32_t olen, Sh<RInfo>* out) {
+                                         uint32_t blen, uint32_t olen, Sh<RInfo>* out, uint64_t* ins = nullptr) {
   const int lane = lane_id();
   const uint32_t W = 2 * e + 1;
   uint64_t keys = 0, cnt_lo = 0, cnt_hi = 0;  // 8 keys (bytes), 8 x 16-bit counts
@@ -625,6 +627,7 @@ __device__ inline bool wave_analyze_read(const Gm<uint32_t>* wf, uint32_t e, uin
       out->occ[k] = (uint16_t)c;
       split += c;
     }
+    if (ins) *ins = keys;
     out->n = (uint8_t)nk;
     out->split = (uint16_t)split;
     out->end = (mb == blen);

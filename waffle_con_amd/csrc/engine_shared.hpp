@@ -350,6 +350,7 @@ struct DwfaDevJob {
   uint32_t status, n_cand;
   uint8_t cand_syms[16];
   uint32_t cand_counts[16];
+  uint8_t cand_first[16];  // the same symbols in insertion (first-appearance) order
 };
 // one standalone wfa_ed_config pair (wc_wfa_ed_batch); offsets into the
 // batch's sequence arena and scratch rows (two rows of `cap` u64 entries)

@@ -823,6 +823,7 @@ int wc_dwfa_batch(wc_ctx* ctx, uint32_t n, wc_dwfa_job* jobs) {
       for (uint32_t k = 0; k < d.n_cand && k < 16; ++k) {
         j.cand_syms[k] = d.cand_syms[k];
         j.cand_counts[k] = d.cand_counts[k];
+        j.cand_first[k] = d.cand_first[k];
       }
     }
   } while (0);

@@ -83,6 +83,14 @@ class DWFALite:
         j, _ = self._job(baseline_seq, other_seq, 2)
         return {j.cand_syms[k]: j.cand_counts[k] for k in range(j.n_cand)}
 
+    def candidate_insertion_order(self, baseline_seq, other_seq):
+        """The symbols of get_extension_candidates in the order the reference
+        inserts them into its FxHashMap (first tip in ascending diagonal index,
+        dynamic_wfa.rs:244-250; wc_dwfa_job.cand_first): the order a caller
+        rebuilding the hashbrown map must insert in."""
+        j, _ = self._job(baseline_seq, other_seq, 2)
+        return [j.cand_first[k] for k in range(j.n_cand)]
+
     def maximum_baseline_distance(self):
         return max(d + self._e - i for i, d in enumerate(self._wf))
 
