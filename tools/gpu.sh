@@ -6,6 +6,15 @@
 #   bash tools/gpu.sh profile <tag> [bench.py args]   tools/profile_round.sh (kernel trace + PMC passes)
 #   bash tools/gpu.sh smoke  <tag>                    __graft_entry__.smoke()
 #   bash tools/gpu.sh cmd    <tag> <seconds> <cmd...> any command under its own time limit
+#   bash tools/gpu.sh ab     <tag> <workload> <reps> <v1> <v2> ...
+#                                  library variants (waffle_con_amd/libwaffle_con_<v>.so,
+#                                  "main" = libwaffle_con.so) alternating on one box, one
+#                                  bench line each; AB_ARGS adds bench.py arguments
+#   bash tools/gpu.sh sub    <tag> <variant> [one_sub.py args]   one sub-problem alone
+#                                  (tools/one_sub.py) on a library variant
+#   bash tools/gpu.sh pmc    <tag> <seconds> "<counters>" <cmd...>  one rocprofv3 --pmc pass
+# Environment variables given to gpu.sh (WAFFLE_CON_LIB, WC_*) apply to every job;
+# `cmd <tag> <s> env K=V prog` sets them for one job.
 # Jobs can be chained: bash tools/gpu.sh tests t1 -- bench t1 --workload cfg5
 # Every GPU step has its own timeout; the first failing step ends the call.
 set -o pipefail
@@ -39,6 +48,32 @@ run_job() {
       shift
       timeout -k 10 $lim "$@" > $O/cmd.log 2>&1 || { echo "cmd failed: $*"; tail -30 $O/cmd.log; return 1; }
       tail -5 $O/cmd.log ;;
+    ab)
+      local W=$1 N=$2
+      shift 2
+      for rep in $(seq $N); do
+        for v in "$@"; do
+          local lib=$PWD/waffle_con_amd/libwaffle_con_$v.so
+          [ "$v" = main ] && lib=$PWD/waffle_con_amd/libwaffle_con.so
+          WAFFLE_CON_LIB=$lib timeout -k 10 400 python3 -u bench.py --workload $W --steps 3 --warmup 1 --no-cpu --no-e2e \
+            $AB_ARGS > $O/${W}_${v}_$rep.json 2> $O/${W}_${v}_$rep.err || { echo "ab $v failed"; tail -20 $O/${W}_${v}_$rep.err; return 1; }
+          python3 -c "import json;d=json.load(open('$O/${W}_${v}_$rep.json'));print('$v', $rep, round(d['value']/1e6,1), d.get('loci_per_s'), round(d['ms_per_step'],2), round(d['kernel_ms_per_step'],2))"
+        done
+      done ;;
+    sub)
+      local v=$1
+      shift
+      local lib=$PWD/waffle_con_amd/libwaffle_con_$v.so
+      [ "$v" = main ] && lib=$PWD/waffle_con_amd/libwaffle_con.so
+      WAFFLE_CON_LIB=$lib timeout -k 10 300 python3 -u tools/one_sub.py "$@" > $O/sub_$v.log 2>&1 \
+        || { echo "sub failed"; tail -20 $O/sub_$v.log; return 1; }
+      grep -v amdgpu $O/sub_$v.log | tail -3 ;;
+    pmc)
+      local lim=$1 ctrs=$2
+      shift 2
+      timeout -s KILL $lim rocprofv3 --pmc $ctrs --output-format csv -d $O/pmc -o run -- "$@" > $O/pmc.log 2>&1 \
+        || { echo "pmc pass failed"; tail -20 $O/pmc.log; return 1; }
+      echo "pmc done" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
         || { echo "smoke failed"; tail -30 $O/smoke.log; return 1; }

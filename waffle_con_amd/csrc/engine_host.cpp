@@ -52,10 +52,14 @@ void persistent_end() {
   for (auto& b : g_parked) (void)(b.second ? hipHostFree(b.first) : hipFree(b.first));
   g_parked.clear();
 }
+// Every free of a device or pinned buffer goes through here: parked while a
+// persistent launch runs, else freed at once, under the same lock, so that no
+// persistent_begin (and the launch after it) can start while a free is in
+// flight. Always takes ownership (returns true).
 bool free_deferred(void* p, bool host) {
   std::lock_guard<std::mutex> g(g_persist_mu);
-  if (g_persist_running == 0) return false;
-  g_parked.emplace_back(p, host);
+  if (g_persist_running > 0) g_parked.emplace_back(p, host);
+  else (void)(host ? hipHostFree(p) : hipFree(p));
   return true;
 }
 
@@ -494,9 +498,19 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
     a.phases = (unsigned long long*)L.phases.p;
     HIPCHK(hipMemsetAsync(L.phases.p, 0, kPhases * 8, L.stream));
   }
+  // pop trace of the launch's problem 0 (WC_POP_TRACE=<file>, diagnostics;
+  // the device code is the same with or without it): per pop (cost, len,
+  // flags, extra), engine.hip trace_pop
+  constexpr uint32_t kTraceCap = 1u << 20;
+  if (getenv("WC_POP_TRACE") && L.trace.ensure((4ull + 4ull * kTraceCap) * 4)) {
+    a.trace = (uint32_t*)L.trace.p;
+    a.trace_cap = kTraceCap;
+    HIPCHK(hipMemsetAsync(L.trace.p, 0, 16, L.stream));
+  }
   const int krc = launch_kernel(ctx, L, a, caps);
   if (krc != WC_OK) return krc;
   L.busy = true;
+  L.traced = a.trace != nullptr;
   if (getenv("WC_LAUNCH_LOG"))
     fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d cu=%d wave=%d dual_hot=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
             caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, (int)caps.cu, (int)caps.wave, (int)caps.dual_hot, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
@@ -599,6 +613,21 @@ int launch_finish(wc_ctx* ctx, Launch& L) {
     }
   }
   if (getenv("WC_LAUNCH_LOG")) fprintf(stderr, "[wc] done problems=%u ms=%.3f\n", L.P, ms);
+  if (const char* path = getenv("WC_POP_TRACE")) {
+    if (L.traced) {
+      uint32_t k = 0;
+      HIPCHK(hipMemcpy(&k, L.trace.p, 4, hipMemcpyDeviceToHost));
+      std::vector<uint32_t> rec(4ull * k);
+      if (k) HIPCHK(hipMemcpy(rec.data(), (const uint32_t*)L.trace.p + 4, rec.size() * 4, hipMemcpyDeviceToHost));
+      if (FILE* f = fopen(path, "a")) {
+        fprintf(f, "# launch sides=%u problems=%u pops=%u\n", L.caps.sides, L.P, k);
+        for (uint32_t i = 0; i < k; ++i)
+          fprintf(f, "%u %u %u %u\n", rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+        fclose(f);
+      }
+    }
+    L.traced = false;
+  }
   return WC_OK;
 }
 
@@ -880,7 +909,9 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
         qrlen[q] = b->rlen_h[s.gid[r]];
       }
       seq_item.push_back(id);
-      items[id].t_pub = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+      // first publication only: a retried sub-problem keeps its first start
+      if (items[id].t_pub < 0)
+        items[id].t_pub = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
       seq_rw.push_back(rw);
       seq_done.push_back(0);
       rw += s.gid.size();

@@ -307,7 +307,14 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
       if (!good) ok.store(false, std::memory_order_relaxed);
     }
   };
-  const uint64_t nch = std::max<uint64_t>(1, std::min<uint64_t>(8, total >> 26));
+  // (test hooks: WC_UPLOAD_CHUNK_SHIFT / WC_UPLOAD_THREAD_SHIFT shrink the
+  // 64 MiB chunks and the 8 MiB per staging thread, so small batches run the
+  // multi-chunk, multi-thread path)
+  const char* cse = getenv("WC_UPLOAD_CHUNK_SHIFT");
+  const char* tse = getenv("WC_UPLOAD_THREAD_SHIFT");
+  const int cshift = cse ? std::max(4, std::min(40, atoi(cse))) : 26;
+  const int tshift = tse ? std::max(4, std::min(40, atoi(tse))) : 23;
+  const uint64_t nch = std::max<uint64_t>(1, std::min<uint64_t>(8, total >> cshift));
   for (int pass = packed ? 0 : 1; pass < 2; ++pass) {
     const bool pk = pass == 0;
     if (!pk) {
@@ -327,7 +334,7 @@ int upload_batch(wc_ctx* ctx, uint32_t n, const wc_problem* problems, wc_batch* 
       while (c_r1 < nr && (c + 1 == nch || roff[c_r1] < want_end)) ++c_r1;
       const uint64_t b0 = c_r0 < nr ? roff[c_r0] : pos;
       const uint64_t b1 = c_r1 < nr ? roff[c_r1] : pos;
-      const uint64_t nt = std::max<uint64_t>(1, std::min<uint64_t>(hw, (b1 - b0) >> 23));
+      const uint64_t nt = std::max<uint64_t>(1, std::min<uint64_t>(hw, (b1 - b0) >> tshift));
       const bool last = c + 1 == nch;
       if (pk) {
         split_run(c_r0, c_r1, nt, pack);

@@ -65,7 +65,7 @@ int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 // parked, and released by the thread that ends the last persistent launch.
 void persistent_begin();
 void persistent_end();
-bool free_deferred(void* p, bool host);  // true: parked (a persistent launch is running)
+bool free_deferred(void* p, bool host);  // parks (a persistent launch runs) or frees now, under the lock; always true
 
 // device buffer, grown on demand (never shrinks)
 struct DevBuf {

@@ -43,7 +43,7 @@ struct Caps {
 struct Launch {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  DevBuf probs, sroff, srlen, ract, ws, counter, act, phases, gst;
+  DevBuf probs, sroff, srlen, ract, ws, counter, act, phases, gst, trace;
   HostBuf host;  // mapped: done[P] | status[P] | stats[P][S_NSTAT] | out[P]
   HostBuf ring;  // mapped (stream launches): StreamCtl | problem ring | read-table rings
   Caps caps;
@@ -54,6 +54,7 @@ struct Launch {
   std::vector<uint8_t> taken;
   uint32_t n_taken = 0;
   bool busy = false;
+  bool traced = false;  // this launch writes a pop trace (WC_POP_TRACE)
   double kernel_ms = 0;
   uint64_t reads_bytes = 0;  // WC_FAULT_LOG: bytes of the read arena the launch reads
   uint64_t ws_stride = 0;  // WC_CHECK: workspace bytes per workgroup (guard zone at the end)
@@ -90,7 +91,7 @@ struct Launch {
     return n;
   }
   ~Launch() {
-    for (DevBuf* b : {&probs, &sroff, &srlen, &ract, &ws, &counter, &act, &phases, &gst}) b->release();
+    for (DevBuf* b : {&probs, &sroff, &srlen, &ract, &ws, &counter, &act, &phases, &gst, &trace}) b->release();
     host.release();
     ring.release();
     if (ev0) (void)hipEventDestroy(ev0);
@@ -118,7 +119,7 @@ void bump(SubProb& s, uint32_t st);
 int launch_finish(wc_ctx* ctx, Launch& L);
 // frees the device and pinned buffers a (finished) launch keeps cached
 inline void launch_release_buffers(Launch& L) {
-  for (DevBuf* b : {&L.probs, &L.sroff, &L.srlen, &L.ract, &L.ws, &L.counter, &L.act, &L.phases, &L.gst}) b->release();
+  for (DevBuf* b : {&L.probs, &L.sroff, &L.srlen, &L.ract, &L.ws, &L.counter, &L.act, &L.phases, &L.gst, &L.trace}) b->release();
   L.host.release();
   L.ring.release();
 }
