@@ -642,6 +642,7 @@ class Cfg5:
         mine = {"done": [self.done[i] for i in self.mine],
                 "slowest": max(((self.dlat.get(i, self.lat[i]), i) for i in self.mine), default=(0.0, -1)),
                 "slow2": sorted(((self.dlat.get(i, self.lat[i]), i) for i in self.mine), reverse=True)[:2],
+                "slowest_call": max(((self.lat[i], i) for i in self.mine), default=(0.0, -1)),
                 "heaviest": (self.lat[h], self.done[h]) if h in self.lat else None}
         if dist is None:
             rows = [mine]
@@ -654,14 +655,18 @@ class Cfg5:
             return done[min(len(done) - 1, max(0, int(math.ceil(f * len(done))) - 1))] if done else None
         hv = next((r["heaviest"] for r in rows if r["heaviest"] is not None), (None, None))
         slow = max(r["slowest"] for r in rows)
+        slow_call = max(r["slowest_call"] for r in rows)
         slow2 = sorted((x for r in rows for x in r["slow2"]), reverse=True)[:2]
         return {"t50_s": q(0.50), "t95_s": q(0.95), "t100_s": q(1.0),
                 "heaviest_locus": h, "heaviest_cost": self.costs[h],
                 "heaviest_latency_under_load_s": hv[0], "heaviest_done_s": hv[1],
-                "slowest_latency_under_load_s": slow[0], "slowest_locus": slow[1],
+                "slowest_device_latency_s": slow[0], "slowest_locus": slow[1],
                 "slowest_two_loci": [x[1] for x in slow2],
-                "slowest_note": "latency on the device: from the publication of the locus's first sub-problem "
-                                "to its result (wc_stats start_ms / wall_ms)"}
+                "slowest_note": "slowest_device_latency_s / slowest_locus: latency on the device, from the first "
+                                "publication of the locus's first sub-problem to its result (wc_stats start_ms / "
+                                "wall_ms); slowest_latency_under_load_s: the largest latency inside the call (from "
+                                "the call's start, queueing included: the meaning this key had before round 5)",
+                "slowest_latency_under_load_s": slow_call[0], "slowest_call_locus": slow_call[1]}
 
     def heaviest_alone(self, h):
         """The heaviest locus alone on the GPU (one call, nothing else queued): s."""

@@ -65,3 +65,31 @@ def test_packed_upload_falls_back_outside_alphabet(monkeypatch):
     assert packed == 0
     for p, g in zip(probs, got):
         assert g == orc.consensus(p, min_count=2)
+
+
+@pytest.mark.parametrize("bad_last", [False, True])
+def test_packed_upload_several_chunks_and_threads(bad_last, monkeypatch):
+    """The production shape on a small batch: eight chunks, each packed by
+    several threads while the previous chunks' copies are in flight
+    (WC_UPLOAD_CHUNK_SHIFT / WC_UPLOAD_THREAD_SHIFT shrink the 64 MiB chunks
+    and 8 MiB per thread). With a byte outside the alphabet in the batch's
+    last read, the packed copies already queued are dropped and the batch
+    goes the byte way."""
+    monkeypatch.setenv("WC_UPLOAD_CHUNK_SHIFT", "12")
+    monkeypatch.setenv("WC_UPLOAD_THREAD_SHIFT", "9")
+    probs = _problems(True, n=16)
+    if bad_last:
+        probs[-1] = list(probs[-1])
+        r = bytearray(probs[-1][-1])
+        r[-1] = ord("N")
+        probs[-1][-1] = bytes(r)
+    total = sum((len(r) + 15) // 16 * 16 for p in probs for r in p)
+    assert total >> 12 >= 8  # eight chunks
+    got_p, st_p, packed = _run(probs, monkeypatch, "1")
+    got_b, st_b, _ = _run(probs, monkeypatch, "0")
+    assert packed == (0 if bad_last else total // 4)
+    assert got_p == got_b
+    for k in KEYS:
+        assert st_p[k] == st_b[k], k
+    for p, g in zip(probs[-3:], got_p[-3:]):
+        assert g == orc.consensus(p, min_count=2)
