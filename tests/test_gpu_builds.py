@@ -8,7 +8,8 @@ at most one problem per CU; WC_CU=1 forces it, WC_CU=0 keeps it off in the
 other variants; dual problems keep their 4-wave build there: the dual engine
 has no whole-CU build), each dual build with dual_hot forced on, and the one-wave
 dual engine (engine_wave.hip, the default for dual problems without offsets;
-WC_WAVE=0 in every other variant). The build is picked per launch from
+WC_WAVE=0 in every other variant) and its search on cooperating waves
+(engine_coop.hip, WC_COOP=1; WC_COOP=0 in every other variant). The build is picked per launch from
 the environment (engine_host.cpp plan_caps), so one process exercises all of
 them. The calls take the per-call batch path (WAFFLE_CON_SERVICE=0) on the
 thread's default context, whose wc_engines_used mask must name the build the
@@ -34,7 +35,11 @@ BUILDS = {"wide": {"WC_NARROW": "0", "WC_LOWLAT": "0"}, "lowlat": {"WC_NARROW": 
           # opt-in knob, measured not to pay; forced here in every dual build)
           "wide-hot": {"WC_NARROW": "0", "WC_LOWLAT": "0", "WC_DUAL_HOT": "2"},
           "lowlat-hot": {"WC_NARROW": "0", "WC_DUAL_HOT": "2"}, "narrow-hot": {"WC_NARROW": "2", "WC_DUAL_HOT": "2"},
-          "wave": {"WC_WAVE": "1"}}
+          "wave": {"WC_WAVE": "1"},
+          # the one-wave engine's search on cooperating waves (engine_coop.hip,
+          # the default for 65-256-read problems in launches of at most one per
+          # CU; WC_COOP=1 forces it, WC_COOP=0 keeps it off in the other variants)
+          "coop": {"WC_COOP": "1"}}
 # the engine build (wc_engine_name) each variant runs for one problem of at
 # most 128 reads: (single, dual)
 ENGINES = {"wide": ("lds.single", "lds.dual"), "lowlat": ("lowlat.single", "lowlat.dual"),
@@ -42,8 +47,9 @@ ENGINES = {"wide": ("lds.single", "lds.dual"), "lowlat": ("lowlat.single", "lowl
            "narrow": ("narrow.single", "narrow.dual"), "gstate": ("gstate.single", "gstate.dual"),
            "cu": ("cu.single", "narrow.dual"), "wide-hot": ("lds.single", "lds.dual"),
            "lowlat-hot": ("lowlat.single", "lowlat.dual"), "narrow-hot": ("lowlat.single", "narrow.dual"),
-           "wave": ("lowlat.single", "wave.dual")}
-KNOBS = ("WC_NARROW", "WC_GSTATE", "WC_LOWLAT", "WC_DUAL_HOT", "WC_CU", "WC_WAVE", "WC_CHAIN", "WC_DUAL_CHAIN")
+           "wave": ("lowlat.single", "wave.dual"), "coop": ("lowlat.single", "coop.dual")}
+KNOBS = ("WC_NARROW", "WC_GSTATE", "WC_LOWLAT", "WC_DUAL_HOT", "WC_CU", "WC_WAVE", "WC_COOP", "WC_CHAIN",
+         "WC_DUAL_CHAIN")
 
 
 @pytest.fixture(params=sorted(BUILDS))
@@ -52,6 +58,7 @@ def build(request, monkeypatch):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("WC_CU", "0")
     monkeypatch.setenv("WC_WAVE", "0")  # (the default for dual problems without offsets)
+    monkeypatch.setenv("WC_COOP", "0")  # (the default for 65-256-read dual problems, few per launch)
     monkeypatch.setenv("WAFFLE_CON_SERVICE", "0")
     for k, v in BUILDS[request.param].items():
         monkeypatch.setenv(k, v)

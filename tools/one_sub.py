@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cfg5-hpc", choices=("cfg5-hpc", "cfg5-full", "cfg3"))
+    ap.add_argument("--workload", default="cfg5-hpc",
+                    choices=("cfg5-hpc", "cfg5-full", "cfg3", "cfg4-root", "cfg4-h01", "cfg4-h0"))
     ap.add_argument("--seed", type=int, default=48)
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--phases", default="", help="WC_PHASES file: per-pop phase cycles of the measured runs "
@@ -27,6 +28,13 @@ def main():
     from waffle_con_amd import synth
     if a.workload == "cfg3":
         p, cfg = synth.cfg3_locus(a.seed), CdwfaConfig()
+    elif a.workload.startswith("cfg4"):
+        # the cfg4 locus (synth.cfg4_locus(seed), 4 haplotypes x 50 reads):
+        # all 200 reads (the priority search's root), the first two
+        # haplotypes' 100, or the first one's 50
+        p = synth.cfg4_locus(a.seed)
+        p = p[:{"cfg4-root": 200, "cfg4-h01": 100, "cfg4-h0": 50}[a.workload]]
+        cfg = CdwfaConfig(wildcard=ord("*"))
     else:
         lvl = 1 if a.workload == "cfg5-full" else 0
         p, cfg = [ch[lvl] for ch in synth.cfg5_locus(a.seed)], CdwfaConfig(wildcard=ord("*"))

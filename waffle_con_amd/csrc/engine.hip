@@ -123,6 +123,14 @@ struct Ctl {
   uint64_t chain_tot[5];  // updates, w_out, compares, ed increases, row bytes of one chain pass
 #endif
   uint32_t deal_cnt[kEW];  // chain_prepare: reads per wave expected to need an ED increase
+  // the cooperative wave build's per-wave exchange (wave_dual.hip.hpp; the
+  // other builds never touch it)
+  uint32_t cx_flags[kEW];  // analysis flags of the wave's reads
+  uint32_t cx_nh[kEW];     // heavy (ED-increase) items of the wave's reads
+  uint32_t cx_cc[kEW];     // Some counts of the in-place child (side 1 | side 2 << 16)
+  uint64_t cx_cost[kEW];   // the in-place child's cost over the wave's reads
+  uint64_t cx_top_cost[2];  // the node wave 0 popped for every wave (double-buffered by pop parity)
+  uint32_t cx_top_len[2], cx_top_slot[2];
   // the chain walk's grouped ED increases (chain_group_heavy): the chain's
   // uniform arguments, in LDS rather than in call registers
   Gm<uint32_t>* gh_nwf;  // the node's wavefront rows
@@ -2595,6 +2603,14 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
 
 #ifdef WC_WAVE_DUAL
 #include "wave_dual.hip.hpp"
+#ifdef WC_COOP
+// every problem on kEW cooperating waves, one read per lane (engine_coop.hip)
+__global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_DUAL_WAVES_PER_EU))) dual_coop_kernel(EngineArgs A) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Ctl ctl_lds;
+  dual_main_wave<1, false>(A, smem, *(Lo<Ctl>*)&ctl_lds);
+}
+#else
 // one kernel per reads-per-lane count (engine_wave.hip): launches whose
 // problems have <= 64 reads, and launches with larger ones (<= 128 reads, two
 // per lane), where each problem of <= 64 reads still runs one read per lane
@@ -2608,6 +2624,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WC_WAVE
   __shared__ Ctl ctl_lds;
   dual_main_wave<2, true>(A, smem, *(Lo<Ctl>*)&ctl_lds);
 }
+#endif  // WC_COOP
 #elif !defined(WC_SINGLE_ONLY)  // (engine_cu.hip: the single engine only)
 // two kernels, one per dual_hot: in one kernel the two paths' register
 // allocations merge (the 4-wave build spilled 236 VGPRs instead of 84)
@@ -2691,7 +2708,16 @@ void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStr
 #endif
 // waves per workgroup of this build (the host sizes the per-wave layouts)
 int engine_waves() { return kEW; }
-#ifdef WC_WAVE_DUAL
+#if defined(WC_WAVE_DUAL) && defined(WC_COOP)
+void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL(dual_coop_kernel, dim3(grid), dim3(kEB), lds, s, a);
+}
+int coop_blocks_per_cu(size_t lds) {
+  int nb = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_coop_kernel, kEB, lds);
+  return e == hipSuccess && nb > 0 ? nb : 1;
+}
+#elif defined(WC_WAVE_DUAL)
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
   if (a.nmax <= 64) hipLaunchKernelGGL(dual_wave1_kernel, dim3(grid), dim3(64), lds, s, a);
   else hipLaunchKernelGGL(dual_wave2_kernel, dim3(grid), dim3(64), lds, s, a);

@@ -195,9 +195,23 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   c.wave = sides == 2 && chain == 0 && !gstate && !any_act && nmax <= 128 && !(wvenv && atoi(wvenv) == 0) &&
            lds_bytes(sides, pcap, nmax, 0, 1) <= kLdsMax;
   if (c.wave) c.narrow = c.lowlat = c.cu = false;
+  // The same search on cooperating waves (engine_coop.hip): one read per lane
+  // over wcc::engine_waves() waves, for dual searches without offsets of
+  // 65-256 reads in a launch whose latency is what counts (at most one
+  // problem per CU: a PriorityConsensusDWFA call on one locus, a deep locus
+  // alone). WC_COOP=0 disables it, WC_COOP=1 takes it for every dual launch
+  // without offsets of at most 256 reads (a test hook: 64 reads or fewer run
+  // on wave 0 alone).
+  const char* cenv = getenv("WC_COOP");
+  const int cmode = cenv ? atoi(cenv) : 2;
+  c.coop = sides == 2 && chain == 0 && !gstate && !any_act && (nmax > 64 || cmode == 1) &&
+           nmax <= 64u * (uint32_t)wcc::engine_waves() && cmode != 0 &&
+           (cmode == 1 || ids.size() <= (uint64_t)ctx->n_cu) && lds_bytes(sides, pcap, nmax, 0, 1) <= kLdsMax;
+  if (c.coop) c.wave = c.narrow = c.lowlat = c.cu = false;
   c.waves = c.cu ? (uint32_t)std::max(wcu::engine_waves(), kWaves) : (uint32_t)kWaves;
   c.dual_hot = false;
   auto occupancy = [&](size_t l) {
+    if (c.coop) return nmax <= 64u * (uint32_t)wcc2::engine_waves() ? wcc2::coop_blocks_per_cu(l) : wcc::coop_blocks_per_cu(l);
     if (c.wave) return wcw::wave_blocks_per_cu(nmax, l);
     if (c.cu) return wcu::engine_blocks_per_cu(sides, l);
     if (sides == 2 && chain > 0 && !gstate) return wcd::engine_blocks_per_cu(sides, l);
@@ -213,8 +227,8 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
   // by default: WC_DUAL_HOT=1 turns it on where it costs the launch no
   // workgroups (same occupancy, or room for every problem anyway),
   // WC_DUAL_HOT=2 wherever the LDS allows.
-  if (c.wave) c.dual_hot = true;  // (the LDS carve of its hot node)
-  if (sides == 2 && chain == 0 && !gstate && !c.wave) {
+  if (c.wave || c.coop) c.dual_hot = true;  // (the LDS carve of its hot node)
+  if (sides == 2 && chain == 0 && !gstate && !c.wave && !c.coop) {
     const char* henv = getenv("WC_DUAL_HOT");
     const int hmode = henv ? atoi(henv) : 0;
     const uint64_t lhot = lds_bytes(sides, pcap, nmax, 0, 1);
@@ -344,10 +358,11 @@ void fault_sentinels(EngineArgs& a, const Caps& caps) {
 const char* const kEngineNames[] = {"lds.single",    "lds.dual",    "narrow.single", "narrow.dual",
                                     "lowlat.single", "lowlat.dual", "cu.single",     "cu.dual",
                                     "chain.single",  "chain.dual",  "wave.single",   "wave.dual",
-                                    "gstate.single", "gstate.dual"};
+                                    "gstate.single", "gstate.dual",  "coop.single", "coop.dual"};
 const uint32_t kNumEngineNames = sizeof(kEngineNames) / sizeof(kEngineNames[0]);
 static uint32_t engine_build(const Caps& caps) {
   if (caps.gstate) return 6;
+  if (caps.coop) return 7;
   if (caps.sides == 2 && caps.chain > 0) return 4;
   if (caps.wave) return 5;
   if (caps.cu) return 3;
@@ -377,6 +392,10 @@ int launch_kernel(wc_ctx* ctx, Launch& L, EngineArgs& a, const Caps& caps) {
     else wcg::launch_dual_engine(a, L.grid, 0, L.stream);
   } else if (caps.sides == 2 && caps.chain > 0) {
     wcd::launch_dual_engine(a, L.grid, caps.lds, L.stream);
+  } else if (caps.coop) {
+    // (2 waves for problems of at most 128 reads, else 4)
+    if (caps.nmax <= 64u * (uint32_t)wcc2::engine_waves()) wcc2::launch_dual_engine(a, L.grid, caps.lds, L.stream);
+    else wcc::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else if (caps.wave) {
     wcw::launch_dual_engine(a, L.grid, caps.lds, L.stream);
   } else if (caps.cu) {
@@ -512,8 +531,8 @@ int launch_start(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_config& cfg
   L.busy = true;
   L.traced = a.trace != nullptr;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d cu=%d wave=%d dual_hot=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
-            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, (int)caps.cu, (int)caps.wave, (int)caps.dual_hot, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
+    fprintf(stderr, "[wc] launch sides=%u problems=%u grid=%u per_cu=%d lds=%zu gstate=%d narrow=%d lowlat=%d cu=%d wave=%d coop=%d dual_hot=%d pcap=%u wcap=%u lcap=%u chain=%u rmax=%u\n",
+            caps.sides, P, L.grid, caps.per_cu, caps.lds, (int)caps.gstate, (int)caps.narrow, (int)caps.lowlat, (int)caps.cu, (int)caps.wave, (int)caps.coop, (int)caps.dual_hot, caps.pcap, caps.wcap, caps.lcap, caps.chain, caps.rmax);
   return WC_OK;
 }
 
@@ -823,9 +842,9 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   }
   L.busy = true;
   if (getenv("WC_LAUNCH_LOG"))
-    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u narrow=%d lowlat=%d wave=%d dual_hot=%d\n",
+    fprintf(stderr, "[wc] stream launch grid=%u per_cu=%d lds=%zu pcap=%u wcap=%u lcap=%u nmax=%u rmax=%u narrow=%d lowlat=%d wave=%d coop=%d dual_hot=%d\n",
             L.grid, caps.per_cu, caps.lds, caps.pcap, caps.wcap, caps.lcap, caps.nmax, caps.rmax, (int)caps.narrow,
-            (int)caps.lowlat, (int)caps.wave, (int)caps.dual_hot);
+            (int)caps.lowlat, (int)caps.wave, (int)caps.coop, (int)caps.dual_hot);
 
   // publication state: seq -> item, read-ring position; incomplete seqs in order
   std::vector<uint32_t> seq_item;
@@ -845,18 +864,24 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   // what is ready but not yet published, in publication order: continuations
   // first (those of the problems that have taken the most pops so far first),
   // then the largest (reads x bases)
+  // (WC_PUB_ORDER=bases: new problems by their bases alone, reads x length,
+  // the better predictor of a locus's critical path; default reads x bases)
+  const char* poe = getenv("WC_PUB_ORDER");
+  const bool by_bases = poe && strcmp(poe, "bases") == 0;
   auto later = [&](uint32_t x, uint32_t y) {
     if (items[x].cont != items[y].cont) return items[y].cont;
     if (items[x].crit != items[y].crit) return items[x].crit < items[y].crit;
-    const double kx = (double)items[x].work * (double)items[x].gid.size();
-    const double ky = (double)items[y].work * (double)items[y].gid.size();
+    const double kx = (double)items[x].work * (by_bases ? 1.0 : (double)items[x].gid.size());
+    const double ky = (double)items[y].work * (by_bases ? 1.0 : (double)items[y].gid.size());
     return kx != ky ? kx < ky : x > y;
   };
   std::priority_queue<uint32_t, std::vector<uint32_t>, decltype(later)> waiting(later);
   // an epoch planned for more reads than the one-wave dual engine takes ends
   // as soon as no live sub-problem has more (the rest wait for the next
   // epoch, planned for them): cfg4's 200-read root, then 50-read groups
-  constexpr size_t kWaveReads = 128;
+  // (an epoch on the cooperative build ends once no live sub-problem has
+  // more than 64 reads: the one-wave kernel runs the rest)
+  const size_t kWaveReads = caps.coop ? 64 : 128;
   const bool can_shrink = !caps.wave && caps.nmax > kWaveReads && !caps.gstate;
   uint32_t big_live = 0;  // outstanding or waiting sub-problems of more than kWaveReads reads
   bool shrink = false;

@@ -44,6 +44,16 @@ void launch_single_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hi
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot = false);
 int engine_waves();
 }  // namespace wcu
+namespace wcc {  // engine_coop.hip: the one-wave dual engine on cooperating waves (65-256 reads, few problems)
+void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+int coop_blocks_per_cu(size_t lds);
+int engine_waves();
+}  // namespace wcc
+namespace wcc2 {  // engine_coop2.hip: the same on 2 waves (65-128 reads)
+void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
+int coop_blocks_per_cu(size_t lds);
+int engine_waves();
+}  // namespace wcc2
 namespace wcw {  // engine_wave.hip: the dual engine on one wave per problem (no offsets, <= 128 reads)
 void launch_dual_engine(const wc::EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s);
 int wave_blocks_per_cu(uint32_t nmax, size_t lds);

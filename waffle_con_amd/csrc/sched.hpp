@@ -32,6 +32,7 @@ struct Caps {
   bool lowlat = false;  // 256-thread build at 2 waves/SIMD (engine_lowlat.hip)
   bool cu = false;      // 1024-thread single engine, one workgroup per CU (engine_cu.hip)
   bool wave = false;    // the dual engine on one wave per problem (engine_wave.hip)
+  bool coop = false;    // the same search on cooperating waves, one read per lane (engine_coop.hip)
   uint32_t waves = wc::kWaves;  // waves per workgroup the per-wave layouts are sized for
   bool dual_hot = false;  // dual engine: the popped node's RStates in LDS (EngineArgs::dual_hot)
   uint64_t gsb = 0;     // its bytes per workgroup

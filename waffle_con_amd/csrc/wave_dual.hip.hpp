@@ -26,6 +26,24 @@
 // Problems with offsets (activation) run on the block engines (the host never
 // plans this build for them).
 
+// ---- the cooperative build (engine_coop.hip, kEW > 1 waves per problem) ----
+// Wave w's lane l holds read 64 w + l (one read per lane); every wave runs the
+// search control on the same values (what one wave learns about its reads, the
+// others get through LDS: nominations in the RInfo area, flag words and
+// partial sums in Ctl::cx_*), and wave 0 alone writes the shared state: heap,
+// trackers, free stack, slot metadata and consensus bytes (thread 0).
+constexpr bool kCoop = kEW > 1;
+// the first read of this wave
+__device__ __forceinline__ uint32_t read_base() { return kCoop ? 64u * (uint32_t)wave_id() : 0u; }
+// (coop) between every wave's reads of shared state and wave 0's writes
+__device__ __forceinline__ void coop_sync() {
+  if constexpr (kCoop) __syncthreads();
+}
+// a read's nominations (NomRaw) through the LDS area of its RInfo record
+struct NomRaw;
+__device__ __forceinline__ void nom_put(Sh<RInfo>* p, const NomRaw& o);
+__device__ __forceinline__ NomRaw nom_get(const Sh<RInfo>* p);
+
 // ---- the hot copy: the popped node's RStates (slot format) in LDS ----
 // Lds::hot[side * nmax + r] is authoritative while the node is hot: pushes
 // (front_store) and the ED-increase loops (wave_heavy's rebuild) write it
@@ -101,6 +119,15 @@ __device__ inline NomRaw nominate_raw(const Front& f, const uint32_t (&x)[kF], u
   }
   return NomRaw{(uint32_t)keys, (uint32_t)(keys >> 32), cnts, nk | ((mb == blen) ? 256u : 0u) | (split << 16), f.e};
 }
+__device__ __forceinline__ void nom_put(Sh<RInfo>* p, const NomRaw& o) {
+  static_assert(sizeof(RInfo) >= 20 && sizeof(RInfo) % 16 == 0, "RInfo holds a NomRaw");
+  ((Sh<uint4>*)p)[0] = make_uint4(o.klo, o.khi, o.cnt, o.meta);
+  ((Sh<uint32_t>*)p)[4] = o.e;
+}
+__device__ __forceinline__ NomRaw nom_get(const Sh<RInfo>* p) {
+  const uint4 a = ((const Sh<uint4>*)p)[0];
+  return NomRaw{a.x, a.y, a.z, a.w, ((const Sh<uint32_t>*)p)[4]};
+}
 // RInfo (thread_nominate's record, the order of several symbols included) of
 // one read from its NomRaw, for the block engines' votes (WR_VOTES_SELECT)
 __device__ inline void rinfo_from_raw(Sh<RInfo>* out, const NomRaw& r) {
@@ -143,7 +170,7 @@ __device__ __forceinline__ void hot_writeback(Eng& E, uint32_t slot, bool dual) 
   const int lane = lane_id();
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    const uint32_t r = (uint32_t)lane + 64u * j;
+    const uint32_t r = read_base() + (uint32_t)lane + 64u * j;
     if (r >= E.n) continue;
     rstate_store(&E.sv(slot, 0).rs[r], rstate_load(&E.L.hot[r]));
     if (dual) rstate_store(&E.sv(slot, 1).rs[r], rstate_load(&E.L.hot[E.nmax + r]));
@@ -154,7 +181,7 @@ __device__ __forceinline__ void hot_fetch_slot(Eng& E, uint32_t slot, bool dual)
   const int lane = lane_id();
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    const uint32_t r = (uint32_t)lane + 64u * j;
+    const uint32_t r = read_base() + (uint32_t)lane + 64u * j;
     if (r >= E.n) continue;
     const RRaw a = rstate_load(&E.sv(slot, 0).rs[r]);
     RRaw b = a;
@@ -276,15 +303,18 @@ struct HeavyArgs {
   uint32_t early;
 };
 template <int R, int V>
-__device__ __noinline__ void wave_heavy_call(HeavyArgs<R> h, Lo<Ctl>& ctl) {
+__device__ __noinline__ uint32_t wave_heavy_call(HeavyArgs<R> h, Lo<Ctl>& ctl, uint32_t lbase, uint32_t nh) {
   const int lane = lane_id();
-  const uint32_t nh = uni(ctl.nheavy);
   WaveCounters cnt = {0, 0, 0, 0, 0, 0};
+  uint32_t ovf = 0;  // (coop: returned, the caller exchanges it; else ctl.ovf)
+  // (this wave's items: list entries [lbase, lbase + nh), its own reads; every
+  // wave calls, for the barrier at the end)
   for (uint32_t k = 0; k < nh; ++k) {
-    const uint32_t it = uni(h.list[WC_IX(k, h.list_cap)]);
+    const uint32_t it = uni(h.list[WC_IX(lbase + k, h.list_cap)]);
     const uint32_t sd = it >= h.n ? 1u : 0u, r = it - sd * h.n;
     // read r's bytes and length from the lane that holds it
-    const uint32_t j = r >> 6, l = r & 63u;
+    const uint32_t rr = r - read_base();
+    const uint32_t j = rr >> 6, l = rr & 63u;
     const Gm<uint8_t>* rp = h.rd[0];
     uint32_t bl = h.bl[0];
 #pragma unroll
@@ -302,10 +332,12 @@ __device__ __noinline__ void wave_heavy_call(HeavyArgs<R> h, Lo<Ctl>& ctl) {
                                sd ? h.con[1] : h.con[0], sd ? h.nl[1] : h.nl[0], (uint8_t)(sd ? h.sy[1] : h.sy[0]), h.wc,
                                h.early != 0, h.wcap, cnt, e);
     __builtin_amdgcn_wave_barrier();
-    if (!ok && lane == 0) atomicOr(&ctl.ovf, 4u);
+    if (kCoop) ovf |= ok ? 0u : 4u;
+    else if (!ok && lane == 0) atomicOr(&ctl.ovf, 4u);
   }
   flush_counters(ctl, cnt);
-  __syncthreads();
+  if constexpr (!kCoop) __syncthreads();
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)ovf);
 }
 
 template <int R, int V>
@@ -326,7 +358,7 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
     // the votes from the pop's RInfo (weighted, or splits that round, or
     // several children to order) and dual_main's selection; the caller
     // builds a single in-place child itself
-    for (uint32_t side = 0; side < (tdual ? 2u : 1u); ++side) {
+    for (uint32_t side = wave_id(); side < (tdual ? 2u : 1u); side += (uint32_t)kEW) {
       const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, n, weighted, tdual, ctl.multi[side] != 0,
                                  cfg.wildcard, cfg.min_count, cfg.min_af == 0.0);
       if (!ok && lane == 0) atomicOr(&ctl.ovf, (uint32_t)LIM_VOTES);
@@ -430,7 +462,7 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
     }
   }
   // votes on both sides, the selection, the children (dual_main)
-  for (uint32_t side = 0; side < (tdual ? 2u : 1u); ++side) {
+  for (uint32_t side = wave_id(); side < (tdual ? 2u : 1u); side += (uint32_t)kEW) {
     const bool ok = wave_votes(ctl, side, side == 0 ? R0 : R1, R0, R1, n, weighted, tdual, ctl.multi[side] != 0,
                                cfg.wildcard, cfg.min_count, cfg.min_af == 0.0);
     if (!ok && lane == 0) atomicOr(&ctl.ovf, (uint32_t)LIM_VOTES);
@@ -497,10 +529,18 @@ __device__ __forceinline__ void wctl_from_ctl(WCtl& W, Lo<Ctl>& ctl) {
 // pop) and at the end of the problem
 __device__ __forceinline__ void wave_flush_counters(Lo<Ctl>& ctl, WCtl& W, uint32_t (&lcnt)[3]) {
   const uint32_t u = wave_sum_u32(lcnt[0]), wo = wave_sum_u32(lcnt[1]), cm = wave_sum_u32(lcnt[2]);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // (the pop counters: every wave holds the same)
     ctl.cnt[S_POPS] += W.pops;
     ctl.cnt[S_EXPLORED] += W.explored;
     ctl.cnt[S_IGNORED] += W.ignored;
+  }
+  if (kCoop) {  // (each wave's reads)
+    if (lane_id() == 0) {
+      atomicAdd((unsigned long long*)&ctl.cnt[S_UPDATES], (unsigned long long)u);
+      atomicAdd((unsigned long long*)&ctl.cnt[S_WOUT], (unsigned long long)wo);
+      atomicAdd((unsigned long long*)&ctl.cnt[S_COMPARES], (unsigned long long)cm);
+    }
+  } else if (threadIdx.x == 0) {
     ctl.cnt[S_UPDATES] += u;
     ctl.cnt[S_WOUT] += wo;
     ctl.cnt[S_COMPARES] += cm;
@@ -629,7 +669,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
 #pragma unroll
   for (int sd = 0; sd < 2; ++sd) {
     if (sy[sd] >= 0) {
-      if (lane == 0) E.sv(top, sd).con[WC_IX(m.len[sd], E.lcap)] = (uint8_t)sy[sd];
+      if (threadIdx.x == 0) E.sv(top, sd).con[WC_IX(m.len[sd], E.lcap)] = (uint8_t)sy[sd];
       m.len[sd]++;
     } else if (kind == 0) {
       m.flags |= (sd == 0 ? 2u : 4u);  // lock_sequence
@@ -639,10 +679,12 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   nl[1] = m.len[1];
   uint32_t upd = 0, wout = 0, cmps = 0, nheavy = 0;
   uint32_t ee[R][2];  // the child's edit distances (kInactive = None)
+  // (coop: each wave lists its heavy items in its own part of the list)
+  const uint32_t hbase = kCoop ? (uint32_t)wave_id() * 2u * 64u : 0u;
   SUB_T0(t_pl);
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    const uint32_t r = (uint32_t)lane + 64u * j;
+    const uint32_t r = read_base() + (uint32_t)lane + 64u * j;
     const bool live = r < n;
 #pragma unroll
     for (int sd = 0; sd < 2; ++sd) {
@@ -678,7 +720,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
       const uint64_t hm = ballot(heavy);
       if (heavy) {
         const uint32_t k = nheavy + (uint32_t)__popcll((unsigned long long)(hm & ((1ull << lane) - 1ull)));
-        E.L.list[WC_IX(k, list_entries(E.sides, E.nmax))] = sd * n + r;
+        E.L.list[WC_IX(hbase + k, list_entries(E.sides, E.nmax))] = sd * n + r;
       }
       nheavy += (uint32_t)__popcll((unsigned long long)hm);
     }
@@ -688,17 +730,18 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   lcnt[1] += wout;
   lcnt[2] += cmps;
   SUB_T1(48, t_pl);  // (push: the lane pass and its counters)
+  uint32_t hovf = 0;  // (coop) this wave's ED-increase overflow bits, exchanged with the cost partials
   if (nheavy) {
     // the ED-increase loops, out of line; then the rebuilt states and their
-    // tip bytes from the hot copy
+    // tip bytes from the hot copy (coop: each wave its own reads', with no
+    // barrier)
     SUB_CNT(53, 1);
     SUB_CNT(55, nheavy);
     SUB_T0(t_hv);
-    if (lane == 0) {
-      ctl.nheavy = nheavy;
-      ctl.ovf = 0;
+    if constexpr (!kCoop) {
+      if (lane == 0) ctl.ovf = 0;
+      __syncthreads();
     }
-    __syncthreads();
     {
       HeavyArgs<R> h;
       h.hot = E.L.hot;
@@ -723,16 +766,16 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
       h.sy[1] = (uint32_t)sy[1];
       h.wc = cfg.wildcard;
       h.early = early ? 1u : 0u;
-      wave_heavy_call<R, V>(h, ctl);
+      hovf = wave_heavy_call<R, V>(h, ctl, hbase, nheavy);
     }
     SUB_T1(54, t_hv);
-    const uint32_t ovf = uni(ctl.ovf);
+    const uint32_t ovf = kCoop ? 0u : uni(ctl.ovf);
     // (per-lane branches without continue, and the uniform status after
     // them: a join of lanes' paths that also carries search control makes
     // the compiler treat the whole pop loop's control state as divergent)
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      const uint32_t r = (uint32_t)lane + 64u * j;
+      const uint32_t r = read_base() + (uint32_t)lane + 64u * j;
 #pragma unroll
       for (int sd = 0; sd < 2; ++sd) {
         if (r < n && !(sd == 1 && !tdual) && sy[sd] >= 0) {
@@ -759,7 +802,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   uint32_t c0 = 0, c1 = 0;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    const uint32_t r = (uint32_t)lane + 64u * j;
+    const uint32_t r = read_base() + (uint32_t)lane + 64u * j;
     if (r >= n) continue;
     uint32_t e1 = ee[j][0];
     uint32_t e2 = tdual ? ee[j][1] : kInactive;
@@ -780,10 +823,30 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
     c1 += e2 != kInactive;
   }
   cost = wave_sum_u64(cost);
-  const uint32_t cc = wave_sum_u32(c0 | (c1 << 16));  // (<= 128 reads a side)
+  uint32_t cc = wave_sum_u32(c0 | (c1 << 16));  // (<= 256 reads a side)
+  if constexpr (kCoop) {  // the partial sums and overflow bits of every wave
+    if (lane == 0) {
+      ctl.cx_cost[wave_id()] = cost;
+      ctl.cx_cc[wave_id()] = cc;
+      ctl.cx_nh[wave_id()] = hovf;
+    }
+    __syncthreads();
+    cost = 0;
+    cc = 0;
+    uint32_t ovf = 0;
+#pragma unroll
+    for (int w = 0; w < kEW; ++w) {
+      cost += ((uint64_t)uni((uint32_t)(ctl.cx_cost[w] >> 32)) << 32) | uni((uint32_t)ctl.cx_cost[w]);
+      cc += uni(ctl.cx_cc[w]);
+      ovf |= uni(ctl.cx_nh[w]);
+    }
+    if (ovf & 16u) W.status = WC_E_INVARIANT_CODE;
+    else if (ovf & 4u) W.status = ST_RETRY | ST_RETRY_WCAP;
+    else if (ovf) W.status = limit_status(ovf);
+  }
   m.nsome[0] = cc & 0xFFFFu;
   m.nsome[1] = cc >> 16;
-  if (lane == 0) meta_put(E.L.meta[top], m);
+  if (threadIdx.x == 0) meta_put(E.L.meta[top], m);
   SUB_T1(49, t_pc);  // (push: prune, cost, Some counts)
   return cost;
 }
@@ -975,7 +1038,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
   // (written out: a loop here was not unrolled, which would leave lr in scratch)
   LaneReads<R> lr;
   {
-    const uint32_t r0 = (uint32_t)lane;
+    const uint32_t r0 = read_base() + (uint32_t)lane;
     lr.rd[0] = E.rbytes + (r0 < E.n ? E.roff[E.P.read_begin + r0] : 0ull);
     lr.bl[0] = r0 < E.n ? E.rlenp[E.P.read_begin + r0] : 0u;
     if constexpr (R > 1) {
@@ -1016,11 +1079,26 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
   const uint32_t mqs32 = (uint32_t)min(cfg.max_queue_size, (uint64_t)0xFFFFFFFFu);
   const uint32_t mnc32 = (uint32_t)min(cfg.max_nodes_wo_constraint, (uint64_t)0xFFFFFFFFu);
 
+  uint32_t pb = 0;  // (coop) pop parity: which hand-off buffer of the popped node
   for (;;) {
     // ---- pop (dual_consensus.rs:340-397) ----
     if (W.heap_n == 0) break;
+    if constexpr (kCoop) {
+      // wave 0 pops (after its own writes of the last pop: heap, trackers,
+      // metadata), every wave takes the node from Ctl after the barrier (the
+      // other waves never read the heap)
+      if (wave_id() == 0) {
+        const HeapEntry t = wheap_pop(E.L.heap, W.heap_n - 1);
+        if (lane == 0) {
+          ctl.cx_top_cost[pb] = t.cost;
+          ctl.cx_top_len[pb] = t.len;
+          ctl.cx_top_slot[pb] = t.slot;
+        }
+      }
+      __syncthreads();
+    }
     SUB_T0(t_pl);
-    const uint32_t plen = uni(E.L.heap[0].len);
+    const uint32_t plen = kCoop ? uni(ctl.cx_top_len[pb]) : uni(E.L.heap[0].len);
     // the processed counts of the top's length, loaded first (HBM, under
     // one wait) while the threshold walks and the sift run
     const uint32_t pc_pre0 = trk_load(&pc[0][WC_IX(plen, L2)]), pc_pre1 = trk_load(&pc[1][WC_IX(plen, L2)]);
@@ -1041,7 +1119,15 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     SUB_T1(45, t_pl);  // (pop-logic: to the heap pop)
     SUB_T0(t_hp);
     W.heap_n--;
-    const HeapEntry top = wheap_pop(E.L.heap, W.heap_n);
+    HeapEntry top;
+    if constexpr (kCoop) {
+      top.cost = ((uint64_t)uni((uint32_t)(ctl.cx_top_cost[pb] >> 32)) << 32) | uni((uint32_t)ctl.cx_top_cost[pb]);
+      top.len = uni(ctl.cx_top_len[pb]);
+      top.slot = uni(ctl.cx_top_slot[pb]);
+      pb ^= 1u;
+    } else {
+      top = wheap_pop(E.L.heap, W.heap_n);
+    }
     SUB_T1(46, t_hp);  // (pop-logic: the heap pop)
     SUB_T0(t_pc);
     const SlotMeta tm = meta_get(E.L.meta[top.slot]);
@@ -1051,7 +1137,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     // (the per-tracker fields by constant index only: a runtime index into
     // WCtl's arrays keeps the whole struct in scratch memory)
     const uint32_t thr_d = dual ? W.thr[1] : W.thr[0];
-    if (lane == 0) atomicSub((uint32_t*)&(dual ? lc[1] : lc[0])[WC_IX(top.len, L2)], 1u);
+    if (threadIdx.x == 0) atomicSub((uint32_t*)&(dual ? lc[1] : lc[0])[WC_IX(top.len, L2)], 1u);
     if (top.len >= thr_d) {
       if (dual) W.total[1]--;
       else W.total[0]--;
@@ -1066,9 +1152,9 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     // outlives an ignored node), so that load's latency overlaps it
     const bool ign = top.cost > W.max_err || top.len < thr_d || imbalanced;
     if (ign) {
-      if (A.trace && lane == 0) trace_pop(A, prob, top, dual | (1u << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
+      if (A.trace && threadIdx.x == 0) trace_pop(A, prob, top, dual | (1u << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
       W.ignored++;
-      if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = top.slot;
+      if (threadIdx.x == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = top.slot;
       W.nfree++;
       if (top.slot == W.hot) W.hot = kNoSlot;  // its state is dropped with the slot
       continue;
@@ -1102,7 +1188,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     bool any_wide = false, any_end = false, any_multi = false, odd_split = false;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      const uint32_t r = (uint32_t)lane + 64u * j;
+      const uint32_t r = read_base() + (uint32_t)lane + 64u * j;
       const bool live = r < E.n;
 #pragma unroll
       for (int sd = 0; sd < 2; ++sd) {
@@ -1137,15 +1223,33 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
       }
     }
     odd_split = ballot(odd_split) != 0;
+    if constexpr (kCoop) {
+      // every wave's nominations (the votes read every read's) and flags
+      const uint32_t r = read_base() + (uint32_t)lane;
+      if (r < E.n) {
+        nom_put(R0 + r, mn[0][0]);
+        if (tdual) nom_put(R1 + r, mn[1][0]);
+      }
+      if (lane == 0)
+        ctl.cx_flags[wave_id()] = (any_wide ? 1u : 0u) | (any_end ? 2u : 0u) | (any_multi ? 4u : 0u) | (odd_split ? 8u : 0u);
+      __syncthreads();
+      uint32_t fw = 0;
+#pragma unroll
+      for (int w = 0; w < kEW; ++w) fw |= uni(ctl.cx_flags[w]);
+      any_wide = fw & 1u;
+      any_end = (fw & 2u) != 0;
+      any_multi = (fw & 4u) != 0;
+      odd_split = (fw & 8u) != 0;
+    }
     tips_ok = true;
     SUB_T1(34, t_an);
     {
       const bool at_cap = uni(dual ? pc_pre1 : pc_pre0) >= cap;
-      if (A.trace && lane == 0)
+      if (A.trace && threadIdx.x == 0)
         trace_pop(A, prob, top, dual | ((at_cap ? 1u : 0u) << 1) | (ns0 << 8) | (ns1 << 20), (uint32_t)am);
       if (at_cap) {
         W.ignored++;
-        if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = topslot;
+        if (threadIdx.x == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = topslot;
         W.nfree++;
         W.hot = kNoSlot;  // (the hot node: its state is dropped with the slot)
         continue;
@@ -1158,7 +1262,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
       W.far[0] = max(W.far[0], top.len);
       W.lastc[0] += W.lastc[0] != 0xFFFFFFFFu;
     }
-    if (lane == 0) atomicAdd((uint32_t*)&(dual ? pc[1] : pc[0])[WC_IX(top.len, L2)], 1u);  // process_unchecked
+    if (threadIdx.x == 0) atomicAdd((uint32_t*)&(dual ? pc[1] : pc[0])[WC_IX(top.len, L2)], 1u);  // process_unchecked
     W.explored++;
     if (W.status != ST_OK) break;
     // active_min_count growth (:497-513): the count at every new length is
@@ -1177,7 +1281,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
       // wide frontiers or a read at a consensus end (finalize, reached_*):
       // the block engines' code for the rest of the pop, from the slot
       SUB_CNT(35, 1);
-      if (lane == 0) {
+      if (threadIdx.x == 0) {
         ctl.n_end[0] = ctl.n_end[1] = 0;
         ctl.n_either = 0;
         ctl.nheavy = 0;
@@ -1195,8 +1299,30 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     } else {
       SideVotes sv0 = {0, 0, -1, false, false}, sv1 = {0, 0, -1, false, true};
       if (!weighted) {
-        sv0 = wave_side_votes<R>(cfg, ys[0], mmask[0], mn[0], odd_split);
-        if (tdual && sv0.exact) sv1 = wave_side_votes<R>(cfg, ys[1], mmask[1], mn[1], odd_split);
+        if constexpr (kCoop) {
+          // every read's nominations, read w * 64 + lane as this lane's w-th
+          // (the single-wave build's two-reads-per-lane arrays, kEW of them)
+          auto side_votes = [&](const Sh<RInfo>* Rs) {
+            uint32_t ysA[kEW];
+            uint64_t mmA[kEW];
+            NomRaw mnA[kEW];
+#pragma unroll
+            for (int w = 0; w < kEW; ++w) {
+              const uint32_t r = 64u * (uint32_t)w + (uint32_t)lane;
+              const NomRaw o = r < E.n ? nom_get(Rs + r) : NomRaw{0, 0, 0, 1u << 16, kInactive};
+              const uint32_t nk = o.meta & 0xFFu;
+              ysA[w] = nk == 1 ? (o.klo & 0xFFu) : 0x100u;
+              mmA[w] = ballot(nk > 1);
+              mnA[w] = o;
+            }
+            return wave_side_votes<kEW>(cfg, ysA, mmA, mnA, odd_split);
+          };
+          sv0 = side_votes(R0);
+          if (tdual && sv0.exact) sv1 = side_votes(R1);
+        } else {
+          sv0 = wave_side_votes<R>(cfg, ys[0], mmask[0], mn[0], odd_split);
+          if (tdual && sv0.exact) sv1 = wave_side_votes<R>(cfg, ys[1], mmask[1], mn[1], odd_split);
+        }
       }
       if (sv0.exact && sv1.exact) {
         // ---- votes and selection on the lean path ----
@@ -1233,7 +1359,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
         // weighted votes, rounding f64 votes at a tie, or several children
         // (their order): the block engines' votes and selection (from RInfo)
         SUB_CNT((!sv0.exact || !sv1.exact) ? 36 : 39, 1);
-        if (lane == 0) {
+        if (threadIdx.x == 0) {
           ctl.ovf = 0;
           ctl.multi[0] = ctl.multi[1] = any_multi ? 1u : 0u;
           ctl.fin[0] = early && ns0 == 0;
@@ -1241,10 +1367,12 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
           ctl.status = W.status;
         }
         // the block engines' votes read RInfo: made here, with the order of
-        // several symbols, only for these pops
+        // several symbols, only for these pops (coop: over the nominations the
+        // other waves may still be reading)
+        coop_sync();
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-          const uint32_t r = (uint32_t)lane + 64u * j;
+          const uint32_t r = read_base() + (uint32_t)lane + 64u * j;
           if (r < E.n) {
             rinfo_from_raw(R0 + r, mn[0][j]);
             if (tdual) rinfo_from_raw(R1 + r, mn[1][j]);
@@ -1262,7 +1390,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
         }
       }
       if (nchild == 0) {
-        if (lane == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = topslot;
+        if (threadIdx.x == 0) E.L.freestack[WC_IX(W.nfree, E.pcap)] = topslot;
         W.nfree++;
         W.hot = kNoSlot;
         PH_MARK(3);
@@ -1300,17 +1428,17 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
         clen = uni(ctl.ch_len[c]);
       }
       const uint32_t k = !general ? (tdual ? 1u : 0u) : ((uni(E.L.meta[cslot].flags) & 1u) ? 1u : 0u);
-      if (lane == 0) atomicAdd((uint32_t*)&(k ? lc[1] : lc[0])[WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
+      if (threadIdx.x == 0) atomicAdd((uint32_t*)&(k ? lc[1] : lc[0])[WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
       if (k) W.total[1] += clen >= W.thr[1];
       else W.total[0] += clen >= W.thr[0];
-      wheap_push(E.L.heap, W.heap_n, HeapEntry{ccost, clen, cslot});
+      if (!kCoop || wave_id() == 0) wheap_push(E.L.heap, W.heap_n, HeapEntry{ccost, clen, cslot});
       W.heap_n++;
     }
     PH_MARK(7);
   }
   wave_flush_counters(ctl, W, lcnt);
   // the register state back into Ctl for finish_problem
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)W.peakq);
   }
   wctl_to_ctl(W, ctl);
@@ -1332,7 +1460,7 @@ __device__ __forceinline__ void dual_main_wave(const EngineArgs& A, uint8_t* sme
     Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)oslot * A.out_stride;
     init_problem(E, ctl);
     // what this build runs (the host plans it so): no offsets, <= 64 R reads
-    if (E.n > 64u * R || E.P.max_act != 0 || E.P.n_active != E.n) {
+    if (E.n > 64u * R * (uint32_t)kEW || E.P.max_act != 0 || E.P.n_active != E.n) {
       if (tid == 0) ctl.status = WC_E_INVARIANT_CODE;
       __syncthreads();
       finish_problem(A, ctl, outp, prob, oslot);

@@ -119,9 +119,10 @@ def cfg5_params(seed, len_range=(1000, 6000), reads_range=(15, 40), max_variants
 
 
 def cfg5_cost(seed, **kw):
-    """Estimated search cost of cfg5 locus `seed` (reads x length, both levels)."""
+    """Estimated cost of cfg5 locus `seed`: reads x length, both levels
+    (shard.locus_cost; the better predictor of its critical path)."""
     L, _, n = cfg5_params(seed, **kw)
-    return 2 * n * L * 2 * n
+    return 2 * n * L * 2
 
 
 def cfg5_locus(seed, len_range=(1000, 6000), reads_range=(15, 40), err=0.005, max_variants=15):
