@@ -100,3 +100,36 @@ def test_coop_priority_cfg5_loci(coop):
         assert got == exp
         for k in KEYS:
             assert gc[k] == ec[k], (seed, k, gc[k], ec[k])
+
+
+def test_wave_stream_pool_for_occupancy(monkeypatch, capfd):
+    """A PriorityConsensusDWFA stream with more sub-problems than fit on the
+    chip at once plans the one-wave engine's node pool for occupancy: the
+    smallest pool, down to 256 nodes, that gives another workgroup per CU
+    (engine_host.cpp plan_caps; a pool of 512 gives 3 per CU). One CU
+    (WC_DEVICE_SHARE on a fresh context) makes six loci such a launch.
+    Results and counters must equal the oracle's
+    (priority_consensus.rs:172-341)."""
+    import waffle_con_amd as w
+    from waffle_con_amd import _lib, synth
+    from waffle_con_amd.cdwfa_config import CdwfaConfig
+    for k in ("WC_WAVE", "WC_COOP", "WC_DUAL_LDS_KB", "WC_NARROW", "WC_LOWLAT", "WC_CU", "WC_GSTATE"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("WC_DEVICE_SHARE", "256")
+    monkeypatch.setenv("WC_LAUNCH_LOG", "1")
+    monkeypatch.setenv("WAFFLE_CON_SERVICE", "0")
+    ctx = _lib.Context(0)
+    seeds = (2, 6, 8, 9, 17, 303)
+    loci = [synth.cfg5_locus(s) for s in seeds]
+    cfg = CdwfaConfig(wildcard=ord("*"))
+    res, st = w.priority_consensus_batch([(L, None, None) for L in loci], cfg, context=ctx, per_problem=True)
+    log = capfd.readouterr().err
+    launches = [ln for ln in log.splitlines() if "stream launch" in ln]
+    assert launches and "grid=4 per_cu=4 " in launches[0] and "pcap=256 " in launches[0], launches
+    for L, r, pp in zip(loci, res, st["per_problem"]):
+        exp, ec = orc.priority_consensus(L, counters=True, wildcard=ord("*"))
+        got = {"consensuses": [[hip._cons(c) for c in chain] for chain in r.consensuses()],
+               "sequence_indices": list(r.sequence_indices())}
+        assert got == exp
+        for k in KEYS:
+            assert pp[k] == ec[k], (k, pp[k], ec[k])

@@ -2718,14 +2718,20 @@ int coop_blocks_per_cu(size_t lds) {
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
 #elif defined(WC_WAVE_DUAL)
+// experiment hook: WC_WAVE_KERNEL=2 runs every problem on the two-reads-per-lane
+// kernel (1 wave per SIMD) instead of the one-read kernel for <=64 reads
+static bool wave_force2() {
+  static const bool f = [] { const char* e = getenv("WC_WAVE_KERNEL"); return e && atoi(e) == 2; }();
+  return f;
+}
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
-  if (a.nmax <= 64) hipLaunchKernelGGL(dual_wave1_kernel, dim3(grid), dim3(64), lds, s, a);
+  if (a.nmax <= 64 && !wave_force2()) hipLaunchKernelGGL(dual_wave1_kernel, dim3(grid), dim3(64), lds, s, a);
   else hipLaunchKernelGGL(dual_wave2_kernel, dim3(grid), dim3(64), lds, s, a);
 }
 // workgroups per CU of the build that runs problems of nmax reads
 int wave_blocks_per_cu(uint32_t nmax, size_t lds) {
   int nb = 0;
-  const hipError_t e = nmax <= 64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave1_kernel, 64, lds)
+  const hipError_t e = nmax <= 64 && !wave_force2() ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave1_kernel, 64, lds)
                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave2_kernel, 64, lds);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }

@@ -250,6 +250,21 @@ int plan_caps(wc_ctx* ctx, const wc_config& cfg, uint32_t sides, const std::vect
       chain = k;
     }
   }
+  // A one-wave launch with more problems than fit at once (a cfg5 stream) is
+  // bound by how many run together: its node pool gets the smallest size, down
+  // to 256 nodes, that still gives another workgroup per CU (the kernels' 256
+  // VGPRs allow 4, one per SIMD; a pool of 512 holds the LDS to 3). A problem
+  // that outgrows the pool retries larger, as always. cfg5 10,000 loci: 768 ->
+  // 1,024 workgroups, 19.8 -> 16.3 s, no retries (gpurun_out/occ3).
+  // WC_DUAL_LDS_KB (experiment hook) keeps the pool it plans.
+  if (c.wave && px == 0 && !getenv("WC_DUAL_LDS_KB")) {
+    while (pcap > 256) {
+      const int occ_now = occupancy((size_t)lds_bytes(sides, pcap, nmax, 0, 1));
+      if (ids.size() <= (uint64_t)occ_now * ctx->n_cu) break;
+      if (occupancy((size_t)lds_bytes(sides, pcap / 2, nmax, 0, 1)) <= occ_now) break;
+      pcap /= 2;
+    }
+  }
   c.pcap = pcap;
   c.chain = chain;
   // result records per problem: up to 256 at first; a problem with more tied
@@ -827,6 +842,10 @@ static int stream_epoch(wc_ctx* ctx, Launch& L, const wc_batch* b, const wc_conf
   a.act_m = caps.act_m;
   a.act_scr = caps.act_m ? (uint64_t*)L.act.p : nullptr;
   a.act_stride = caps.act_m ? act_scr_u64(caps.act_m, caps.waves) : 0;
+  if (getenv("WC_PHASES") && L.phases.ensure(kPhases * 8)) {  // (WC_PHASE_PROF builds only)
+    a.phases = (unsigned long long*)L.phases.p;
+    HIPCHK(hipMemsetAsync(L.phases.p, 0, kPhases * 8, L.stream));
+  }
   a.stream = 1;
   a.qcap = kQcap;
   a.qslots = kQslots;
