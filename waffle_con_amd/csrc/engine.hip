@@ -123,14 +123,6 @@ struct Ctl {
   uint64_t chain_tot[5];  // updates, w_out, compares, ed increases, row bytes of one chain pass
 #endif
   uint32_t deal_cnt[kEW];  // chain_prepare: reads per wave expected to need an ED increase
-  // the cooperative wave build's per-wave exchange (wave_dual.hip.hpp; the
-  // other builds never touch it)
-  uint32_t cx_flags[kEW];  // analysis flags of the wave's reads
-  uint32_t cx_nh[kEW];     // heavy (ED-increase) items of the wave's reads
-  uint32_t cx_cc[kEW];     // Some counts of the in-place child (side 1 | side 2 << 16)
-  uint64_t cx_cost[kEW];   // the in-place child's cost over the wave's reads
-  uint64_t cx_top_cost[2];  // the node wave 0 popped for every wave (double-buffered by pop parity)
-  uint32_t cx_top_len[2], cx_top_slot[2];
   // the chain walk's grouped ED increases (chain_group_heavy): the chain's
   // uniform arguments, in LDS rather than in call registers
   Gm<uint32_t>* gh_nwf;  // the node's wavefront rows
@@ -2708,15 +2700,28 @@ void launch_single_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStr
 #endif
 // waves per workgroup of this build (the host sizes the per-wave layouts)
 int engine_waves() { return kEW; }
+// Workgroups per CU of `kernel` at `lds` bytes of dynamic LDS. The runtime's
+// occupancy query counts LDS more finely than gfx950 allocates it: a CU's
+// 160 KB go out in granules of 1,280 bytes (tools/lds_occupancy.hip: 53,760
+// bytes ran 3 per CU, 53,761 only 2, where the query answers 3 up to 54,613),
+// so its answer is capped by the granule count of static + dynamic LDS.
+template <class K>
+static int blocks_per_cu(K kernel, int threads, size_t lds) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess || nb <= 0) return 1;
+  hipFuncAttributes at;
+  if (hipFuncGetAttributes(&at, (const void*)kernel) == hipSuccess) {
+    constexpr size_t kGranule = 1280, kLdsPerCu = 160 * 1024;
+    const size_t per_wg = (at.sharedSizeBytes + lds + kGranule - 1) / kGranule * kGranule;
+    if (per_wg) nb = std::min<int>(nb, (int)(kLdsPerCu / per_wg));
+  }
+  return std::max(nb, 1);
+}
 #if defined(WC_WAVE_DUAL) && defined(WC_COOP)
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(dual_coop_kernel, dim3(grid), dim3(kEB), lds, s, a);
 }
-int coop_blocks_per_cu(size_t lds) {
-  int nb = 0;
-  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_coop_kernel, kEB, lds);
-  return e == hipSuccess && nb > 0 ? nb : 1;
-}
+int coop_blocks_per_cu(size_t lds) { return blocks_per_cu(dual_coop_kernel, kEB, lds); }
 #elif defined(WC_WAVE_DUAL)
 // experiment hook: WC_WAVE_KERNEL=2 runs every problem on the two-reads-per-lane
 // kernel (1 wave per SIMD) instead of the one-read kernel for <=64 reads
@@ -2730,10 +2735,7 @@ void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStrea
 }
 // workgroups per CU of the build that runs problems of nmax reads
 int wave_blocks_per_cu(uint32_t nmax, size_t lds) {
-  int nb = 0;
-  const hipError_t e = nmax <= 64 && !wave_force2() ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave1_kernel, 64, lds)
-                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_wave2_kernel, 64, lds);
-  return e == hipSuccess && nb > 0 ? nb : 1;
+  return nmax <= 64 && !wave_force2() ? blocks_per_cu(dual_wave1_kernel, 64, lds) : blocks_per_cu(dual_wave2_kernel, 64, lds);
 }
 #elif !defined(WC_SINGLE_ONLY)
 void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
@@ -2748,20 +2750,18 @@ void launch_dual_engine(const EngineArgs& a, uint32_t grid, size_t lds, hipStrea
 #endif
 #ifndef WC_WAVE_DUAL
 int engine_blocks_per_cu(uint32_t sides, size_t lds, bool dual_hot) {
-  int nb = 0;
-  hipError_t e = hipSuccess;
 #ifndef WC_DUAL_ONLY
-  if (sides == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, single_engine_kernel, kEB, lds);
+  if (sides == 1) return blocks_per_cu(single_engine_kernel, kEB, lds);
 #else
   if (sides == 1) return 1;
 #endif
 #ifndef WC_SINGLE_ONLY
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_DUAL_CHAIN_CALL)
-  else if (dual_hot) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_hot_engine_kernel, kEB, lds);
+  if (dual_hot) return blocks_per_cu(dual_hot_engine_kernel, kEB, lds);
 #endif
-  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dual_engine_kernel, kEB, lds);
+  return blocks_per_cu(dual_engine_kernel, kEB, lds);
 #endif
-  return e == hipSuccess && nb > 0 ? nb : 1;
+  return 1;
 }
 #endif
 #if !defined(WC_GLOBAL_STATE) && !defined(WC_NARROW) && !defined(WC_LOWLAT) && !defined(WC_CU) && !defined(WC_WAVE_DUAL)

@@ -30,7 +30,7 @@
 // Wave w's lane l holds read 64 w + l (one read per lane); every wave runs the
 // search control on the same values (what one wave learns about its reads, the
 // others get through LDS: nominations in the RInfo area, flag words and
-// partial sums in Ctl::cx_*), and wave 0 alone writes the shared state: heap,
+// partial sums in coopx()), and wave 0 alone writes the shared state: heap,
 // trackers, free stack, slot metadata and consensus bytes (thread 0).
 constexpr bool kCoop = kEW > 1;
 // the first read of this wave
@@ -38,6 +38,22 @@ __device__ __forceinline__ uint32_t read_base() { return kCoop ? 64u * (uint32_t
 // (coop) between every wave's reads of shared state and wave 0's writes
 __device__ __forceinline__ void coop_sync() {
   if constexpr (kCoop) __syncthreads();
+}
+// (coop) the waves' exchange area, a static LDS variable of its own that only
+// the cooperative build references: Ctl keeps its size in every other build,
+// whose LDS budgets sit at 1,280-byte allocation granules (§2.6 of DESIGN.md:
+// 112 bytes more in Ctl cost cfg3's dual build a workgroup per CU)
+struct CoopX {
+  uint32_t flags[kEW];  // analysis flags of the wave's reads
+  uint32_t nh[kEW];     // ED-increase overflow bits of the wave's reads
+  uint32_t cc[kEW];     // Some counts of the in-place child (side 1 | side 2 << 16)
+  uint64_t cost[kEW];   // the in-place child's cost over the wave's reads
+  uint64_t top_cost[2];  // the node wave 0 popped for every wave (double-buffered by pop parity)
+  uint32_t top_len[2], top_slot[2];
+};
+__device__ __forceinline__ CoopX& coopx() {
+  __shared__ CoopX x;
+  return x;
 }
 // a read's nominations (NomRaw) through the LDS area of its RInfo record
 struct NomRaw;
@@ -826,9 +842,9 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   uint32_t cc = wave_sum_u32(c0 | (c1 << 16));  // (<= 256 reads a side)
   if constexpr (kCoop) {  // the partial sums and overflow bits of every wave
     if (lane == 0) {
-      ctl.cx_cost[wave_id()] = cost;
-      ctl.cx_cc[wave_id()] = cc;
-      ctl.cx_nh[wave_id()] = hovf;
+      coopx().cost[wave_id()] = cost;
+      coopx().cc[wave_id()] = cc;
+      coopx().nh[wave_id()] = hovf;
     }
     __syncthreads();
     cost = 0;
@@ -836,9 +852,9 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
     uint32_t ovf = 0;
 #pragma unroll
     for (int w = 0; w < kEW; ++w) {
-      cost += ((uint64_t)uni((uint32_t)(ctl.cx_cost[w] >> 32)) << 32) | uni((uint32_t)ctl.cx_cost[w]);
-      cc += uni(ctl.cx_cc[w]);
-      ovf |= uni(ctl.cx_nh[w]);
+      cost += ((uint64_t)uni((uint32_t)(coopx().cost[w] >> 32)) << 32) | uni((uint32_t)coopx().cost[w]);
+      cc += uni(coopx().cc[w]);
+      ovf |= uni(coopx().nh[w]);
     }
     if (ovf & 16u) W.status = WC_E_INVARIANT_CODE;
     else if (ovf & 4u) W.status = ST_RETRY | ST_RETRY_WCAP;
@@ -1090,15 +1106,17 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
       if (wave_id() == 0) {
         const HeapEntry t = wheap_pop(E.L.heap, W.heap_n - 1);
         if (lane == 0) {
-          ctl.cx_top_cost[pb] = t.cost;
-          ctl.cx_top_len[pb] = t.len;
-          ctl.cx_top_slot[pb] = t.slot;
+          coopx().top_cost[pb] = t.cost;
+          coopx().top_len[pb] = t.len;
+          coopx().top_slot[pb] = t.slot;
         }
       }
       __syncthreads();
     }
     SUB_T0(t_pl);
-    const uint32_t plen = kCoop ? uni(ctl.cx_top_len[pb]) : uni(E.L.heap[0].len);
+    uint32_t plen;
+    if constexpr (kCoop) plen = uni(coopx().top_len[pb]);
+    else plen = uni(E.L.heap[0].len);
     // the processed counts of the top's length, loaded first (HBM, under
     // one wait) while the threshold walks and the sift run
     const uint32_t pc_pre0 = trk_load(&pc[0][WC_IX(plen, L2)]), pc_pre1 = trk_load(&pc[1][WC_IX(plen, L2)]);
@@ -1121,9 +1139,9 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     W.heap_n--;
     HeapEntry top;
     if constexpr (kCoop) {
-      top.cost = ((uint64_t)uni((uint32_t)(ctl.cx_top_cost[pb] >> 32)) << 32) | uni((uint32_t)ctl.cx_top_cost[pb]);
-      top.len = uni(ctl.cx_top_len[pb]);
-      top.slot = uni(ctl.cx_top_slot[pb]);
+      top.cost = ((uint64_t)uni((uint32_t)(coopx().top_cost[pb] >> 32)) << 32) | uni((uint32_t)coopx().top_cost[pb]);
+      top.len = uni(coopx().top_len[pb]);
+      top.slot = uni(coopx().top_slot[pb]);
       pb ^= 1u;
     } else {
       top = wheap_pop(E.L.heap, W.heap_n);
@@ -1231,11 +1249,11 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
         if (tdual) nom_put(R1 + r, mn[1][0]);
       }
       if (lane == 0)
-        ctl.cx_flags[wave_id()] = (any_wide ? 1u : 0u) | (any_end ? 2u : 0u) | (any_multi ? 4u : 0u) | (odd_split ? 8u : 0u);
+        coopx().flags[wave_id()] = (any_wide ? 1u : 0u) | (any_end ? 2u : 0u) | (any_multi ? 4u : 0u) | (odd_split ? 8u : 0u);
       __syncthreads();
       uint32_t fw = 0;
 #pragma unroll
-      for (int w = 0; w < kEW; ++w) fw |= uni(ctl.cx_flags[w]);
+      for (int w = 0; w < kEW; ++w) fw |= uni(coopx().flags[w]);
       any_wide = fw & 1u;
       any_end = (fw & 2u) != 0;
       any_multi = (fw & 4u) != 0;
