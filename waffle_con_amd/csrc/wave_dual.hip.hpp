@@ -33,6 +33,13 @@
 // partial sums in coopx()), and wave 0 alone writes the shared state: heap,
 // trackers, free stack, slot metadata and consensus bytes (thread 0).
 constexpr bool kCoop = kEW > 1;
+// the lean path's pushes leave advancing tips' row entries to the RState
+// (hot_flush_rows below); WC_EAGER_ROWS keeps every row entry written
+#ifdef WC_EAGER_ROWS
+constexpr bool kLazyRows = false;
+#else
+constexpr bool kLazyRows = true;
+#endif
 // the first read of this wave
 __device__ __forceinline__ uint32_t read_base() { return kCoop ? 64u * (uint32_t)wave_id() : 0u; }
 // (coop) between every wave's reads of shared state and wave 0's writes
@@ -206,6 +213,34 @@ __device__ __forceinline__ void hot_fetch_slot(Eng& E, uint32_t slot, bool dual)
     if (dual) rstate_store(&E.L.hot[E.nmax + r], b);
   }
 }
+// Lazy rows: the lean path's pushes (thread_apply<true>) do not write a tip's
+// new value into its wavefront row when it advances, only a diagonal's final
+// value when it leaves the frontier (stuck or at the read's end). Between the
+// two the RState is authoritative for its frontier diagonals, and the row for
+// every other diagonal. Readers of rows: the ED-increase loop (a read whose
+// frontier emptied, so every diagonal has been written; wide-frontier reads
+// never take the lean push), and the block engines' code (wave_rare), whose
+// pushes assume rows complete: the hot node's frontier goes into its rows
+// first (this function, at wave_rare's entry). Clones copy rows and RStates together, so the
+// invariant carries over to them.
+template <int R>
+__device__ __forceinline__ void hot_flush_rows(Eng& E, uint32_t slot, bool dual) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const uint32_t r = read_base() + (uint32_t)lane + 64u * j;
+    if (r >= E.n) continue;
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      if (sd == 1 && !dual) continue;
+      const RRaw s = rstate_load(&E.L.hot[sd * E.nmax + r]);
+      if (rraw_e(s) == kInactive || (rraw_flags(s) & kWide)) continue;
+      Front f;
+      front_load(s, f);
+      front_flush(f, E.sv(slot, sd).wf + (uint64_t)r * E.wcap);
+    }
+  }
+}
 
 // ---- the rare paths, out of line (one call site each): the pop loop's
 // register allocation does not carry theirs. The callee rebuilds the engine
@@ -370,6 +405,13 @@ __device__ __noinline__ void wave_rare(KArgs kp, DevProblem P, Sh<uint8_t>* sbas
   const SlotMeta tm = meta_get(E.L.meta[top]);
   Sh<RInfo>* R0 = E.L.rinfo;
   Sh<RInfo>* R1 = E.L.rinfo + E.nmax;
+  if constexpr (kLazyRows) {
+    // (the block code below pushes and clones from the node's rows)
+    if (op != WR_VOTES_SELECT) {
+      hot_flush_rows<R>(E, top, tdual);
+      __syncthreads();
+    }
+  }
   if (op == WR_VOTES_SELECT) {
     // the votes from the pop's RInfo (weighted, or splits that round, or
     // several children to order) and dual_main's selection; the caller
@@ -719,7 +761,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
             uint32_t x[kF];
             tips_unpack(tx[j][sd], x);
             uint32_t cmp = 0;
-            heavy = thread_apply(f, x, lr.bl[j], nl[sd] - 1, (uint8_t)sy[sd], cfg.wildcard, early,
+            heavy = thread_apply<kLazyRows>(f, x, lr.bl[j], nl[sd] - 1, (uint8_t)sy[sd], cfg.wildcard, early,
                                  E.sv(top, sd).wf + (uint64_t)r * E.wcap, cmp);
             cmps += cmp;
             front_store(hp, f);  // (a heavy read's ED-increase loop goes on from it)
