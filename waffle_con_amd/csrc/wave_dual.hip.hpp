@@ -40,6 +40,13 @@ constexpr bool kLazyRows = false;
 #else
 constexpr bool kLazyRows = true;
 #endif
+// an in-place child that the next pop would take straight back skips the
+// heap (wheap_push_pop_noop); WC_NO_REPOP keeps every push and pop
+#ifdef WC_NO_REPOP
+constexpr bool kRepop = false;
+#else
+constexpr bool kRepop = true;
+#endif
 // the first read of this wave
 __device__ __forceinline__ uint32_t read_base() { return kCoop ? 64u * (uint32_t)wave_id() : 0u; }
 // (coop) between every wave's reads of shared state and wave 0's writes
@@ -707,6 +714,37 @@ __device__ __forceinline__ HeapEntry heap_uni(const HeapEntry& e) {
   u.slot = uni(e.slot);
   return u;
 }
+// push(e) and then pop() on a heap of n entries: true when that pair returns
+// e and leaves every entry where it was, so the caller can skip both (the
+// in-place child of a pop is most often the next pop). The push takes e to
+// the root iff it beats the root strictly (ancestors of strictly lower
+// priority move down one level along its path). The pop then sifts x, the
+// entry the push moved into position n (n's parent's), down from the root; it
+// retraces the path, putting every moved entry back, iff at each ancestor the
+// path child is the child the sift picks (the larger, the left one on ties)
+// and x has strictly lower priority than it. (At n's parent x stops by the
+// heap property.) Lane k checks ancestor k + 1 levels above n.
+__device__ __forceinline__ bool wheap_push_pop_noop(const Sh<HeapEntry>* h, uint32_t n, const HeapEntry& e) {
+  if (n == 0) return true;
+  if (!prio_less(heap_uni(h[0]), e)) return false;
+  const uint32_t lane = (uint32_t)lane_id();
+  const uint32_t depth = 31u - (uint32_t)__builtin_clz(n + 1);  // ancestors of position n
+  const HeapEntry x = heap_uni(h[((n + 1) >> 1) - 1]);
+  bool bad = false;
+  if (lane >= 1 && lane < depth) {
+    const uint32_t anc = ((n + 1) >> (lane + 1)) - 1;  // (moved down to pc by the push)
+    const uint32_t pc = ((n + 1) >> lane) - 1;          // its child on the path
+    const uint32_t sib = (pc & 1u) ? pc + 1 : pc - 1;
+    const HeapEntry a = h[anc];
+    bool path = true;
+    if (sib < n) {
+      const HeapEntry b = h[sib];
+      path = (pc & 1u) ? !prio_less(a, b) : prio_less(b, a);
+    }
+    bad = !path || !prio_less(x, a);
+  }
+  return ballot(bad) == 0;
+}
 
 // ---- the in-place child of a one-child pop (dual_build_children for nc == 1,
 // no activate_dual): pushes on the hot state, ED increases through the slot
@@ -1138,26 +1176,35 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
   const uint32_t mnc32 = (uint32_t)min(cfg.max_nodes_wo_constraint, (uint64_t)0xFFFFFFFFu);
 
   uint32_t pb = 0;  // (coop) pop parity: which hand-off buffer of the popped node
+  // the last pop's in-place child when pushing it and popping it again would
+  // leave the heap as it was (wheap_push_pop_noop): it is the next top, and
+  // the heap is not touched (every wave holds the same)
+  bool stashed = false;
+  HeapEntry stash{};
   for (;;) {
     // ---- pop (dual_consensus.rs:340-397) ----
     if (W.heap_n == 0) break;
     if constexpr (kCoop) {
       // wave 0 pops (after its own writes of the last pop: heap, trackers,
       // metadata), every wave takes the node from Ctl after the barrier (the
-      // other waves never read the heap)
-      if (wave_id() == 0) {
-        const HeapEntry t = wheap_pop(E.L.heap, W.heap_n - 1);
-        if (lane == 0) {
-          coopx().top_cost[pb] = t.cost;
-          coopx().top_len[pb] = t.len;
-          coopx().top_slot[pb] = t.slot;
+      // other waves read the heap only when no wave writes it: between this
+      // barrier and the push)
+      if (!stashed) {
+        if (wave_id() == 0) {
+          const HeapEntry t = wheap_pop(E.L.heap, W.heap_n - 1);
+          if (lane == 0) {
+            coopx().top_cost[pb] = t.cost;
+            coopx().top_len[pb] = t.len;
+            coopx().top_slot[pb] = t.slot;
+          }
         }
+        __syncthreads();
       }
-      __syncthreads();
     }
     SUB_T0(t_pl);
     uint32_t plen;
-    if constexpr (kCoop) plen = uni(coopx().top_len[pb]);
+    if (stashed) plen = stash.len;
+    else if constexpr (kCoop) plen = uni(coopx().top_len[pb]);
     else plen = uni(E.L.heap[0].len);
     // the processed counts of the top's length, loaded first (HBM, under
     // one wait) while the threshold walks and the sift run
@@ -1180,7 +1227,10 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     SUB_T0(t_hp);
     W.heap_n--;
     HeapEntry top;
-    if constexpr (kCoop) {
+    if (stashed) {
+      top = stash;
+      stashed = false;
+    } else if constexpr (kCoop) {
       top.cost = ((uint64_t)uni((uint32_t)(coopx().top_cost[pb] >> 32)) << 32) | uni((uint32_t)coopx().top_cost[pb]);
       top.len = uni(coopx().top_len[pb]);
       top.slot = uni(coopx().top_slot[pb]);
@@ -1491,7 +1541,13 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
       if (threadIdx.x == 0) atomicAdd((uint32_t*)&(k ? lc[1] : lc[0])[WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
       if (k) W.total[1] += clen >= W.thr[1];
       else W.total[0] += clen >= W.thr[0];
-      if (!kCoop || wave_id() == 0) wheap_push(E.L.heap, W.heap_n, HeapEntry{ccost, clen, cslot});
+      const HeapEntry ce{ccost, clen, cslot};
+      if (kRepop && !general && wheap_push_pop_noop(E.L.heap, W.heap_n, ce)) {
+        stashed = true;  // (nc == 1: the in-place child)
+        stash = ce;
+      } else if (!kCoop || wave_id() == 0) {
+        wheap_push(E.L.heap, W.heap_n, ce);
+      }
       W.heap_n++;
     }
     PH_MARK(7);
