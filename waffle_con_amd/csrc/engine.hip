@@ -325,6 +325,36 @@ __device__ __forceinline__ void heap_push(Sh<HeapEntry>* h, Lo<uint32_t>& n, uin
   }
   h[pos] = e;
 }
+// push(e) then pop() on a heap of n entries returns e and leaves every entry
+// where it was (thread 0's form of wave_dual.hip.hpp wheap_push_pop_noop):
+// e beats the root strictly, and at each ancestor of position n the pop's
+// sift-down picks the path child (the larger, the left one on ties) and moves
+// x, the old parent of n, past it (x strictly lower)
+__device__ __forceinline__ bool heap_push_pop_noop(const Sh<HeapEntry>* h, uint32_t n, const HeapEntry& e) {
+  if (n == 0) return true;
+  if (!prio_less(h[0], e)) return false;
+  const uint32_t depth = 31u - (uint32_t)__builtin_clz(n + 1);
+  const HeapEntry x = h[((n + 1) >> 1) - 1];
+  for (uint32_t k = 1; k < depth; ++k) {
+    const uint32_t anc = ((n + 1) >> (k + 1)) - 1, pc = ((n + 1) >> k) - 1;
+    const uint32_t sib = (pc & 1u) ? pc + 1 : pc - 1;
+    const HeapEntry a = h[anc];
+    if (sib < n) {
+      const HeapEntry b = h[sib];
+      if ((pc & 1u) ? prio_less(a, b) : !prio_less(b, a)) return false;
+    }
+    if (!prio_less(x, a)) return false;
+  }
+  return true;
+}
+// Ctl::top_dual of a pending in-place child (dual_main): its push and the
+// next pop were skipped, Ctl::top_* hold it
+constexpr uint32_t kTopStashed = 0x80000000u;
+#ifdef WC_NO_REPOP
+constexpr bool kRepopBlock = false;
+#else
+constexpr bool kRepopBlock = true;
+#endif
 __device__ __forceinline__ HeapEntry heap_pop(Sh<HeapEntry>* h, Lo<uint32_t>& n, uint32_t cap) {
   HeapEntry top = h[0];
   top.slot = WC_IX(top.slot, cap);
@@ -2245,6 +2275,7 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
     E.n = E.P.n_reads;
     Gm<uint8_t>* outp = (Gm<uint8_t>*)A.out + (uint64_t)oslot * A.out_stride;
     init_problem(E, ctl);
+    if (tid == 0) ctl.top_dual = 0;  // (no stashed child from the last problem)
     const uint64_t full_min = max(cfg.min_count, ceil_u64(cfg.min_af * (double)E.n));
 
     for (;;) {
@@ -2253,10 +2284,12 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
         if (ctl.heap_n == 0) {
           ctl.action = 2;
         } else {
-          // the node to pop is heap[0] already: its HBM-resident counts
-          // (processed per length of both trackers, active_min) are loaded
-          // first, under one wait, while the threshold walk and the sift run
-          const uint32_t plen = E.L.heap[0].len;
+          // the node to pop is heap[0] already (or the stashed in-place
+          // child): its HBM-resident counts (processed per length of both
+          // trackers, active_min) are loaded first, under one wait, while the
+          // threshold walk and the sift run
+          const bool stashed = ctl.top_dual == kTopStashed;
+          const uint32_t plen = stashed ? ctl.top_len : E.L.heap[0].len;
           const uint32_t pc_pre[2] = {E.tracker(ctl, 0).processed(plen), E.tracker(ctl, 1).processed(plen)};
           const uint64_t am_pre = plen < ctl.am_len ? E.active_min[WC_IX(plen, E.lcap + 2)] : 0;
           ctl.cnt[S_PEAKQ] = max(ctl.cnt[S_PEAKQ], (uint64_t)ctl.heap_n);
@@ -2269,7 +2302,13 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
               ctl.last_constraint[k] = 0;
             }
           }
-          HeapEntry top = heap_pop(E.L.heap, ctl.heap_n, E.pcap);
+          HeapEntry top;
+          if (stashed) {
+            top = HeapEntry{ctl.top_cost, ctl.top_len, ctl.top_slot};
+            ctl.heap_n--;
+          } else {
+            top = heap_pop(E.L.heap, ctl.heap_n, E.pcap);
+          }
           const auto& m = E.L.meta[top.slot];
           const uint32_t dual = m.flags & 1u;
           TrackerRef t = E.tracker(ctl, dual);
@@ -2582,7 +2621,18 @@ __device__ __forceinline__ void dual_main(const EngineArgs& A, uint8_t* smem, Lo
         for (uint32_t c = 0; c < nc; ++c) {
           const uint32_t k = (E.L.meta[ctl.ch_slot[c]].flags & 1u) ? 1 : 0;
           E.tracker(ctl, k).insert(ctl.ch_len[c]);
-          heap_push(E.L.heap, ctl.heap_n, E.pcap, HeapEntry{ctl.ch_cost[c], ctl.ch_len[c], ctl.ch_slot[c]});
+          const HeapEntry ce{ctl.ch_cost[c], ctl.ch_len[c], ctl.ch_slot[c]};
+          // the last (in-place) child: when the next pop would take it
+          // straight back and leave the heap as it was, both are skipped
+          if (kRepopBlock && c + 1 == nc && heap_push_pop_noop(E.L.heap, ctl.heap_n, ce)) {
+            ctl.heap_n++;
+            ctl.top_cost = ce.cost;
+            ctl.top_len = ce.len;
+            ctl.top_slot = ce.slot;
+            ctl.top_dual = kTopStashed;
+          } else {
+            heap_push(E.L.heap, ctl.heap_n, E.pcap, ce);
+          }
         }
       }
       // (no barrier: the next pop is thread 0's too, and the block meets after it)
