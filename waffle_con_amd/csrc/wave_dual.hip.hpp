@@ -1181,6 +1181,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
   // the heap is not touched (every wave holds the same)
   bool stashed = false;
   HeapEntry stash{};
+  uint32_t stash_k = 0;  // its tracker (1: dual)
   for (;;) {
     // ---- pop (dual_consensus.rs:340-397) ----
     if (W.heap_n == 0) break;
@@ -1218,7 +1219,8 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       while ((W.total[k] > mqs32 || W.lastc[k] >= mnc32) && W.thr[k] < W.far[k]) {
-        W.total[k] -= uni(trk_load(&lc[k][WC_IX(W.thr[k], L2)]));  // increment_threshold
+        W.total[k] -= uni(trk_load(&lc[k][WC_IX(W.thr[k], L2)])) +  // increment_threshold
+                      ((stashed && stash_k == (uint32_t)k && stash.len == W.thr[k]) ? 1u : 0u);
         W.thr[k]++;
         W.lastc[k] = 0;
       }
@@ -1227,6 +1229,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     SUB_T0(t_hp);
     W.heap_n--;
     HeapEntry top;
+    const bool from_stash = stashed;
     if (stashed) {
       top = stash;
       stashed = false;
@@ -1247,7 +1250,7 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
     // (the per-tracker fields by constant index only: a runtime index into
     // WCtl's arrays keeps the whole struct in scratch memory)
     const uint32_t thr_d = dual ? W.thr[1] : W.thr[0];
-    if (threadIdx.x == 0) atomicSub((uint32_t*)&(dual ? lc[1] : lc[0])[WC_IX(top.len, L2)], 1u);
+    if (threadIdx.x == 0 && !from_stash) atomicSub((uint32_t*)&(dual ? lc[1] : lc[0])[WC_IX(top.len, L2)], 1u);
     if (top.len >= thr_d) {
       if (dual) W.total[1]--;
       else W.total[0]--;
@@ -1538,15 +1541,19 @@ __device__ __forceinline__ void wave_problem(const EngineArgs& A, Eng& E, Lo<Ctl
         clen = uni(ctl.ch_len[c]);
       }
       const uint32_t k = !general ? (tdual ? 1u : 0u) : ((uni(E.L.meta[cslot].flags) & 1u) ? 1u : 0u);
-      if (threadIdx.x == 0) atomicAdd((uint32_t*)&(k ? lc[1] : lc[0])[WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
       if (k) W.total[1] += clen >= W.thr[1];
       else W.total[0] += clen >= W.thr[0];
       const HeapEntry ce{ccost, clen, cslot};
       if (kRepop && !general && wheap_push_pop_noop(E.L.heap, W.heap_n, ce)) {
-        stashed = true;  // (nc == 1: the in-place child)
+        // (nc == 1: the in-place child) its tracker count too stays out of
+        // HBM: the next pop's remove cancels the insert, and the threshold
+        // walk between them adds it (stash_k)
+        stashed = true;
         stash = ce;
-      } else if (!kCoop || wave_id() == 0) {
-        wheap_push(E.L.heap, W.heap_n, ce);
+        stash_k = k;
+      } else {
+        if (threadIdx.x == 0) atomicAdd((uint32_t*)&(k ? lc[1] : lc[0])[WC_IX(clen, L2)], 1u);  // tracker(k).insert(len)
+        if (!kCoop || wave_id() == 0) wheap_push(E.L.heap, W.heap_n, ce);
       }
       W.heap_n++;
     }
