@@ -765,7 +765,10 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
 #pragma unroll
   for (int sd = 0; sd < 2; ++sd) {
     if (sy[sd] >= 0) {
-      if (threadIdx.x == 0) E.sv(top, sd).con[WC_IX(m.len[sd], E.lcap)] = (uint8_t)sy[sd];
+      // (every wave stores the byte: coop waves run their ED-increase loops,
+      // which read it, with no barrier after this store; stored after the
+      // lane pass instead, a 4-wave problem faulted, cause not found)
+      if (lane == 0) E.sv(top, sd).con[WC_IX(m.len[sd], E.lcap)] = (uint8_t)sy[sd];
       m.len[sd]++;
     } else if (kind == 0) {
       m.flags |= (sd == 0 ? 2u : 4u);  // lock_sequence
