@@ -261,7 +261,9 @@ __device__ inline void chain_prepare(Eng& E, Lo<Ctl>& ctl, uint32_t top, uint32_
     }
     const uint64_t hm = ballot(hv);
     if (lane == 0) ctl.deal_cnt[wave_id()] = (uint32_t)__popcll((unsigned long long)hm);
+    if (tid >= 1 && (uint32_t)tid <= K) con_store_wait();  // (the predictions stored above: the walk's ED increases read them)
     __syncthreads();
+    l1_drop();
     uint32_t hb = 0, H = 0;
     for (uint32_t w = 0; w < (uint32_t)kEW; ++w) {
       const uint32_t c = ctl.deal_cnt[w];

@@ -136,6 +136,9 @@ __device__ inline void dual_chain_prepare(Eng& E, Lo<Ctl>& ctl, const DualChainA
   // (positions >= its length are not part of the node)
   for (uint32_t s = 0; s < 2; ++s)
     if (((walk >> s) & 1u) && tid >= 1 && (uint32_t)tid <= K) E.sv(top, s).con[l0[s] + tid - 1] = A.pred[s][tid];
+  con_store_wait();  // (the walk's ED increases read them)
+  __syncthreads();
+  l1_drop();
 }
 
 // (C) push the predictions through both sides of every read, thread per read,

@@ -1666,6 +1666,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       }
       ctl.nheavy = 0;
       ctl.nwide = 0;
+      con_store_wait();  // (the children's consensus bytes: the ED increases below read them)
     }
     __syncthreads();
     if (uni(ctl.status) != ST_OK) return;
@@ -1750,6 +1751,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
     PH_MARK(5);
     // the ED-increase loops: eight reads per wave in 8-lane groups ...
     const uint32_t nh = uni(ctl.nheavy), nw = uni(ctl.nwide);
+    if (nh + nw) l1_drop();  // (they read the children's consensus bytes; con_store_wait above)
     SUB_CNT(16, nh);
     SUB_CNT(17, nw);
     SUB_T0(tg);
@@ -2206,8 +2208,12 @@ __global__ void __launch_bounds__(kEB) __attribute__((amdgpu_waves_per_eu(WC_SIN
         if (uni(ctl.status) != ST_OK) break;
         const uint32_t slot = uni(ctl.cur_slot);
         if (slot != top) copy_side<true>(E, top, 0, slot, 0, plen);
-        if (tid == 0) E.sv(slot, 0).con[plen] = (uint8_t)ctl.ch_s[c][0];
+        if (tid == 0) {
+          E.sv(slot, 0).con[plen] = (uint8_t)ctl.ch_s[c][0];
+          con_store_wait();  // (the ED increases below read it)
+        }
         __syncthreads();
+        l1_drop();
         PH_MARK(4);
         // clones read the parent from LDS and write their own slot; the last
         // child is pushed in place on the LDS copy

@@ -279,6 +279,16 @@ struct WaveCounters {
 #endif
 };
 
+// The CU's vector L1 keeps its copy of a line across this workgroup's own
+// byte stores to it: a wave that stored a consensus byte and read it back in
+// its ED-increase loop got the old byte, even after waiting for the store
+// (wave_dual.hip.hpp, a fault on a 4-wave problem). Code that stores
+// consensus bytes which ED-increase loops then read waits for the stores
+// (con_store_wait, in the storing waves) and, after whatever orders the
+// readers behind them, drops the CU's L1 lines (l1_drop: buffer_inv sc1).
+__device__ __forceinline__ void con_store_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void l1_drop() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+
 // ---- packed match runs (dynamic_wfa.rs:122-150) ----
 // 8 bytes at p[pos..pos+8): two aligned 8-byte loads and a funnel shift.
 // Reads start 16-byte aligned with 64 bytes of arena tail padding and the

@@ -765,11 +765,7 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
 #pragma unroll
   for (int sd = 0; sd < 2; ++sd) {
     if (sy[sd] >= 0) {
-      // (every wave stores the byte: coop waves run their ED-increase loops,
-      // which read it, with no barrier after this store; stored after the
-      // lane pass instead, a 4-wave problem faulted, cause not found)
-      if (lane == 0) E.sv(top, sd).con[WC_IX(m.len[sd], E.lcap)] = (uint8_t)sy[sd];
-      m.len[sd]++;
+      m.len[sd]++;  // (the consensus byte is stored after the lane pass)
     } else if (kind == 0) {
       m.flags |= (sd == 0 ? 2u : 4u);  // lock_sequence
     }
@@ -829,6 +825,17 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
   lcnt[1] += wout;
   lcnt[2] += cmps;
   SUB_T1(48, t_pl);  // (push: the lane pass and its counters)
+  // The consensus bytes, after the lane pass (which compares against sy, not
+  // memory). The ED-increase loops below read them back: each wave stores
+  // them itself (coop waves run those loops with no barrier) and, before the
+  // loops, waits for its stores and invalidates the CU's vector L1, whose
+  // copy of the line a byte store leaves stale (measured: without the
+  // invalidate a 4-wave problem read the old byte and faulted; with the store
+  // at the push's start instead, only the lane pass's traffic evicting the
+  // line kept it right). The block code reads them later, after barriers.
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd)
+    if (sy[sd] >= 0 && lane == 0) E.sv(top, sd).con[WC_IX(nl[sd] - 1, E.lcap)] = (uint8_t)sy[sd];
   uint32_t hovf = 0;  // (coop) this wave's ED-increase overflow bits, exchanged with the cost partials
   if (nheavy) {
     // the ED-increase loops, out of line; then the rebuilt states and their
@@ -837,6 +844,8 @@ __device__ __forceinline__ uint64_t wave_push_fast(Eng& E, Lo<Ctl>& ctl, KArgs k
     SUB_CNT(53, 1);
     SUB_CNT(55, nheavy);
     SUB_T0(t_hv);
+    con_store_wait();  // (this wave's consensus byte stores)
+    l1_drop();
     if constexpr (!kCoop) {
       if (lane == 0) ctl.ovf = 0;
       __syncthreads();
