@@ -1858,6 +1858,7 @@ __device__ inline void dual_build_children(Eng& E, Lo<Ctl>& ctl, uint32_t top, c
       const uint32_t slot = WC_IX(uni(ctl.ch_slot[c]), E.pcap);
       const uint32_t nl0 = uni(E.L.meta[slot].len[0]), nl1 = uni(E.L.meta[slot].len[1]);
       if (max(nl0, nl1) > E.P.max_act) continue;
+      if (!activated && nh + nw == 0) l1_drop();  // (activation reads the new consensus bytes too)
       activated = true;
       if (kDH && slot == top) {
         activate_side<true>(E, ctl, slot, 0, nl0, max(nl0, nl1), false, nullptr);
